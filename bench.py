@@ -1,0 +1,198 @@
+"""Benchmark: feature-timesteps/sec (fwd+bwd) of the tri-modal MMCTransformer training step.
+
+    python bench.py [--gpus N --steps K --warmup W]          (N > 1: under torch.distributed.run)
+
+Workload (BASELINE.json metric): configs/Repurpose.yaml model — tri-modal
+(512 + 2048 + 384 -> 512), 16 pre-LN encoder layers, 8 heads, d_ff 2048, heads + focal loss —
+T = 2048, B = 8 sequences per GPU, bf16 MFMA compute (fp32 master weights, residual stream, LN,
+softmax and accumulators), dropout 0.1 active.  One step = forward + losses + backward + gradient
+all-reduce over RCCL (N > 1) + fused Adam (lr 1e-3, weight decay 1e-4).  Synthetic seeded inputs
+with the feature statistics of SURVEY §8d, random-init weights (seed 1234); inputs resident in HBM.
+
+Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel's achieved MFMA rate measured
+live with HIP events on the launch stream during the timed steps; `cpu_baseline` is the oracle
+(stock torch CPU modules, fp32, the reference's own arithmetic) timed on this host.
+"""
+import argparse
+import json
+import math
+import os
+import subprocess
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MODEL_CFG = dict(vis_dim=512, aud_dim=2048, text_dim=384, d_model=512, self_num_layers=16, text_num_layers=3,
+                 cross_num_layers=3, num_heads=8)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def flops_per_timestep(T, L=16, d=512, dff=2048, din=2944):
+    """Algorithmic FLOPs per timestep, fwd+bwd: 311,167,488 + 98,304*T at L=16."""
+    per_layer_linear = 2 * d * 3 * d + 2 * d * d + 2 * 2 * d * dff
+    lin = 3 * L * per_layer_linear
+    attn = L * (4 * T * d + 8 * T * d)
+    inp = 2 * (2 * din * d)
+    fm = 3 * 2 * d * d
+    cls = 3 * (2 * d * 256 + 2 * 256 * 256 + 2 * 256)
+    reg = 2 * d * 256 + 2 * 256 * 256 + 2 * 256 * 2
+    return lin + attn + inp + fm + cls + reg
+
+
+def synth_batch(B, T, dev, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    v = torch.randn(B, T, 512, generator=g)
+    v = v / v.norm(dim=-1, keepdim=True)
+    a = torch.relu(torch.randn(B, T, 2048, generator=g))
+    t = torch.randn(B, T, 384, generator=g)
+    t = t / t.norm(dim=-1, keepdim=True)
+    t = t * (torch.rand(B, T, 1, generator=g) > 0.3)
+    lab = torch.zeros(B, T)
+    for b in range(B):  # run-length segments, coverage ~0.35
+        pos = 0
+        while pos < T:
+            gap = int(torch.randint(20, 120, (1,), generator=g))
+            ln = int(torch.randint(10, 70, (1,), generator=g))
+            lab[b, pos + gap: pos + gap + ln] = 1
+            pos += gap + ln
+    batch = {"visual_feats": v, "audio_feats": a, "text_feats": t,
+             "masks": torch.ones(B, 1, T, dtype=torch.bool), "labels": lab,
+             "segments": torch.rand(B, T, 2, generator=g) * 30}
+    return {k: x.to(dev) for k, x in batch.items()}
+
+
+def cpu_baseline(T, budget_s=25.0):
+    """Oracle (reference arithmetic on stock torch CPU modules, fp32) fwd+bwd at the metric shape,
+    B = 1, train mode; bounded sample."""
+    from oracle.mmct_oracle import MMCTransformer as Oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(1234)
+    m = Oracle(**MODEL_CFG).train()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    b = synth_batch(1, T, torch.device("cpu"), 999)
+    times = []
+    t_start = time.perf_counter()
+    steps = 0
+    while True:
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        out = m(b)
+        loss = m.losses(*out)["cls_loss"]
+        loss.backward()
+        opt.step()
+        times.append(time.perf_counter() - t0)
+        steps += 1
+        if time.perf_counter() - t_start > budget_s or steps >= 6:
+            break
+    timed = times[1:] if len(times) > 1 else times
+    med = sorted(timed)[len(timed) // 2]
+    try:
+        model = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
+        model = [l.split(":", 1)[1].strip() for l in model.splitlines() if l.startswith("Model name")][0]
+    except Exception:
+        model = "unknown"
+    return {"value": T / med, "unit": "feature-timesteps/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 train step (fwd+focal+bwd+Adam), L=16 tri-modal, B=1, T={T}; "
+                      f"{len(timed)} timed of {steps} steps, median {med:.2f}s; cpu '{model}'"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seq-len", type=int, default=2048)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-kernel", default="attn_fwd")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from repurpose_amd import kernels as K
+    from repurpose_amd.MMCTransformer import MMCTransformer
+    from repurpose_amd.distributed import GradAllReducer
+    from repurpose_amd.optim import FusedAdam
+
+    torch.manual_seed(1234)
+    model = MMCTransformer(**MODEL_CFG, compute_dtype=args.dtype).to(dev).train()
+    opt = FusedAdam(model, lr=1e-3, weight_decay=1e-4)
+    reducer = GradAllReducer(model) if world > 1 else None
+    B, T = args.batch, args.seq_len
+    batch = synth_batch(B, T, dev, 1000 + rank)
+
+    def step():
+        opt.zero_grad()
+        out = model(batch)
+        loss = model.losses(*out)["cls_loss"] / B
+        loss.backward()
+        if reducer is not None:
+            reducer.wait()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    K.timer_start(args.roofline_kernel)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = K.timer_stop()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    value = world * B * T * args.steps / elapsed
+    if rank == 0:
+        fpt = flops_per_timestep(T)
+        H, dk = 8, 64
+        if args.roofline_kernel == "attn_fwd":
+            kflops = 4.0 * B * H * T * T * dk
+        else:
+            kflops = float("nan")
+        achieved = kflops / (kern_ms * 1e-3) / 1e12 if kern_ms else None
+        roof = {"kernel": args.roofline_kernel, "bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s", "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": None,
+                "avg_launch_ms": kern_ms, "flops_per_launch": kflops,
+                "step_tflops": fpt * value / world / 1e12, "step_frac": fpt * value / world / 1e12 / PEAK_BF16_TFLOPS}
+        res = {"metric": "feature-timesteps/sec (fwd+bwd) tri-modal T=2048", "value": value,
+               "unit": "feature-timesteps/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded, SURVEY §8d statistics)",
+               "config": {"workload": f"tri-modal MMCTransformer L=16 d=512 H=8 dff=2048, T={T}, B={B}/GPU, "
+                                      f"train step fwd+focal+bwd+allreduce+Adam",
+                          "model": "MMCTransformer (configs/Repurpose.yaml)", "global_batch": B * world,
+                          "seq_len": T, "parallelism": f"dp{world}"},
+               "loss": float(loss.item()), "roofline": roof}
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(T)
+            res["speedup_vs_cpu"] = value / res["cpu_baseline"]["value"]
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,212 @@
+/*
+ * rp_api.h — C ABI of librepurpose_amd.so, the MI355X (gfx950) HIP implementation of the
+ * Repurpose tri-modal temporal-localisation hot path.
+ *
+ * Every entry point takes raw device pointers, sizes, leading dimensions and a hipStream_t
+ * (passed as void*), enqueues asynchronously on that stream, never allocates or frees caller
+ * memory, and returns 0 (RP_OK) or an RP_ERR_* code; rp_last_error() returns the message
+ * (thread-local).  No torch types cross this boundary.
+ *
+ * Which reference interface each family replaces (paths relative to the reference repo):
+ *   rp_concat_rows        torch.cat of the three modalities      models/MMCTransformer.py:118
+ *   rp_gemm               nn.Linear fwd/dgrad/wgrad              models/MMCTransformer.py:32,121,63-93;
+ *                         and MHA in_proj/out_proj, linear1/2 of the 16 nn.TransformerEncoderLayer
+ *                         (constructed at models/MMCTransformer.py:41-55)
+ *   rp_layernorm_fwd/bwd  nn.LayerNorm (+ PE add, ReLU, dropout)  models/MMCTransformer.py:35,124,127,
+ *                         58,141,65,72,84; encoder-layer norm1/norm2
+ *   rp_attn_fwd/bwd       nn.MultiheadAttention -> SDPA (key padding mask, dropout 0.1)
+ *                         models/MMCTransformer.py:132-138
+ *   rp_focal_*            sigmoid_focal_loss + mask + sum        models/losses.py:4-53,
+ *                         models/MMCTransformer.py:159-179
+ *   rp_rowdot_*           final Linear(256->1 / 256->2) of cls/reg heads models/MMCTransformer.py:71-93
+ *   rp_colsum             bias / LayerNorm-affine gradient reductions (autograd of the above)
+ *   rp_adam_step          torch.optim.Adam(lr, weight_decay) step  main.py:190-191,369
+ *   rp_infer_select       inference_single_video                 models/MMCTransformer.py:181-229
+ *   rp_softnms            soft_nms_intervals_cpu                 models/softnms.py:3-38
+ *   (gradient all-reduce over RCCL is issued by the host layer through torch.distributed,
+ *    replacing utils/distributed.py:396-433 DDP; no collective lives in this library)
+ */
+#ifndef RP_API_H
+#define RP_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { RP_OK = 0, RP_ERR_ARG = 1, RP_ERR_LAUNCH = 2 };
+enum { RP_F32 = 0, RP_BF16 = 1 };
+
+int rp_version(void);
+/* Copies the last error message of the calling thread into buf (NUL-terminated). */
+int rp_last_error(char* buf, size_t n);
+
+/* K1: out[r, :] = [v[r, 0:dv] | a[r, 0:da] | t[r, 0:dt]] (inputs fp32, contiguous rows),
+ * out row stride dv+da+dt, out dtype RP_F32 or RP_BF16.  dv/da/dt may be 0. */
+int rp_concat_rows(const float* v, int dv, const float* a, int da, const float* t, int dt,
+                   int64_t rows, void* out, int out_dtype, void* stream);
+
+/* dst[i] = bf16(src[i]) (round to nearest even) */
+int rp_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* GEMM: C[m, n] = epilogue( alpha * sum_k A(m, k) * B(n, k) )
+ *   A(m, k) = A[m*lda + k] if a_kmajor else A[k*lda + m]
+ *   B(n, k) = B[n*ldb + k] if b_kmajor else B[k*ldb + n]
+ * A and B share `dtype` (RP_F32: exact-f32 MFMA parity mode; RP_BF16: bf16 MFMA, fp32 acc).
+ * Requirements: the contiguous dimension of A, B and C is a multiple of 8 elements, leading
+ * dimensions multiples of 8, base pointers 16-byte aligned.
+ * Epilogue order: v = alpha*acc (+ bias[n]); relu; dropout(p, seed, index m*N+n);
+ *   gate: v *= gate_scale * (gate[m, n] > 0);  residual: v += residual[m, n];
+ *   accumulate (fp32 C only): C[m, n] += v, else C[m, n] = v. */
+typedef struct rp_gemm_epilogue {
+  const float* bias;
+  int relu;
+  float dropout_p;
+  uint32_t dropout_seed;
+  const float* residual;
+  int64_t ldr;
+  const void* gate;
+  int gate_dtype;
+  int64_t ldg;
+  float gate_scale;
+  int accumulate;
+} rp_gemm_epilogue;
+
+int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int a_kmajor,
+            const void* B, int64_t ldb, int b_kmajor, void* C, int64_t ldc, int c_dtype, float alpha,
+            const rp_gemm_epilogue* ep, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* LayerNorm over the last dim D (<= 4096, multiple of 4), one row per wavefront.
+ * y = ((x - mean) * rstd) * gamma + beta;  y += pe[(row % pe_period) * D + c] if pe;
+ * y = relu(y) if relu;  y = dropout(y, p, seed, index row*D+c) if dropout_p > 0.
+ * Writes y to out_f32 and/or out_lp (dtype out_lp_dtype); saves mean/rstd if non-NULL. */
+typedef struct rp_ln_fwd_args {
+  const void* x;
+  int x_dtype;
+  int64_t ldx;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  const float* pe;
+  int64_t pe_period;
+  int relu;
+  float dropout_p;
+  uint32_t dropout_seed;
+  float* out_f32;
+  int64_t ld_out_f32;
+  void* out_lp;
+  int out_lp_dtype;
+  int64_t ld_out_lp;
+  float* mean;
+  float* rstd;
+} rp_ln_fwd_args;
+
+int rp_layernorm_fwd(int64_t rows, int64_t D, const rp_ln_fwd_args* a, void* stream);
+
+/* LayerNorm backward.  dy is the gradient w.r.t. the forward output after relu/dropout.
+ *   g = dy;  if dropout_p > 0: g *= keep(seed, row*D+c) / (1-p);  if y: g *= (y > 0)  (relu)
+ *   dx = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat));  dx += dres
+ *   dx_f32 (if non-NULL) = dx;  dx_lp (if non-NULL) = dx * keep(dx_lp_seed)/(1-dx_lp_dropout_p)
+ *   dgamma_part[blk, c] = sum over the block's rows of g*xhat;  dbeta_part[blk, c] = sum g
+ * Partials have rp_layernorm_bwd_blocks(rows) rows; reduce them with rp_colsum. */
+typedef struct rp_ln_bwd_args {
+  const void* dy;
+  int dy_dtype;
+  int64_t lddy;
+  const void* x;
+  int x_dtype;
+  int64_t ldx;
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  const void* y;
+  int y_dtype;
+  int64_t ldy;
+  float dropout_p;
+  uint32_t dropout_seed;
+  const float* dres;
+  int64_t lddres;
+  float* dx_f32;
+  int64_t lddx;
+  void* dx_lp;
+  int dx_lp_dtype;
+  int64_t lddx_lp;
+  float dx_lp_dropout_p;
+  uint32_t dx_lp_seed;
+  float* dgamma_part;
+  float* dbeta_part;
+} rp_ln_bwd_args;
+
+int64_t rp_layernorm_bwd_blocks(int64_t rows);
+int rp_layernorm_bwd(int64_t rows, int64_t D, const rp_ln_bwd_args* a, void* stream);
+
+/* out[c] (+)= sum_r w[r] * X[r*ldx + c]  (w NULL -> 1).  X dtype RP_F32 / RP_BF16.
+ * workspace: rp_colsum_workspace(rows, cols) floats.  Deterministic (fixed reduction order). */
+int64_t rp_colsum_workspace(int64_t rows, int64_t cols);
+int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ldx, const float* w,
+              float* out, int accumulate, float* workspace, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Multi-head self attention, flash-style (no T x T materialisation).
+ * qkv: [B*T, 3*H*dk] rows = (q heads | k heads | v heads), dk == 64.
+ * key_valid: [B, T] uint8 (0 -> key masked with -inf, torch key_padding_mask semantics).
+ * out: [B*T, H*dk];  lse: [B, H, T] fp32 (natural-log sum-exp of scaled scores).
+ * Dropout on the attention probabilities with p, hash seed (index ((b*H+h)*T+q)*T+k). */
+int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk,
+                float scale, float dropout_p, uint32_t seed, void* out, float* lse, void* stream);
+/* Backward; dqkv: [B*T, 3*H*dk] (fully overwritten); delta_ws: [B, H, T] fp32 workspace. */
+int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
+                const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
+                uint32_t seed, void* dqkv, float* delta_ws, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Focal loss (alpha, gamma) on n frames.  mask may be NULL (all ones).
+ * fwd_sum: *loss = sum_i mask_i * focal(x_i, t_i)   (single deterministic reduction)
+ * elementwise: out_i = focal(x_i, t_i)
+ * bwd: dx_i = (*grad_out) * mask_i * d focal / d x_i  (grad_out: device scalar, or per-element
+ *      array when grad_per_elem != 0) */
+int rp_focal_fwd_sum(const float* x, const float* t, const uint8_t* mask, int64_t n, float alpha,
+                     float gamma, float* loss, void* stream);
+int rp_focal_elementwise(const float* x, const float* t, int64_t n, float alpha, float gamma,
+                         float* out, void* stream);
+int rp_focal_bwd(const float* x, const float* t, const uint8_t* mask, int64_t n, float alpha,
+                 float gamma, const float* grad_out, int grad_per_elem, float* dx, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Small-N linear (N <= 4): out[r, j] = act(sum_k X[r, k] * W[j, k] + b[j]).
+ * bwd_dx: dX[r, k] = (sum_j dout[r, j] * W[j, k]) * gate_scale * (G[r, k] > 0 if G) */
+int rp_rowdot_fwd(int x_dtype, const void* X, int64_t ldx, int64_t rows, int K, const float* W,
+                  const float* b, int nout, int relu, float* out, int64_t ldo, void* stream);
+int rp_rowdot_bwd_dx(const float* dout, int64_t ldd, int64_t rows, int K, const float* W, int nout,
+                     const void* G, int g_dtype, int64_t ldg, float gate_scale, void* dX,
+                     int dx_dtype, int64_t lddx, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* torch.optim.Adam (coupled L2 weight decay) over a flat fp32 buffer; step is 1-based.
+ * p_lp (optional): refreshed bf16 copy of the updated parameters. */
+int rp_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, int step, void* p_lp, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Inference.  rp_infer_select: per video b (one workgroup), prob = sigmoid(logit)*mask,
+ * candidates prob > thresh, stable sort (prob desc, index asc), first min(topk, n),
+ * left = idx - off0, right = idx + off1, keep dur_min < right-left < dur_max.
+ * Outputs: count[b]; idx/score/seg rows [b, 0:count[b]] (capacity topk per video).  T <= 8192. */
+int rp_infer_select(const float* logits, const uint8_t* mask, const float* offsets, int B, int T,
+                    float thresh, int topk, float dur_min, float dur_max, int* count,
+                    int64_t* idx, float* score, float* seg, void* stream);
+/* Soft-NMS with the exact semantics of soft_nms_intervals_cpu (one workgroup per video,
+ * n = count[b] <= cap <= 1024).  keep[b, 0:keep_count[b]] = positions into the candidate list.
+ * final_scores (optional): the decayed, permuted score array the reference leaves behind. */
+int rp_softnms(const float* scores, const float* segs, const int* count, int B, int cap,
+               float sigma, float thresh, const int* max_seg, int* keep, int* keep_count,
+               float* final_scores, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RP_API_H */

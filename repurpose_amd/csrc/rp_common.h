@@ -1,0 +1,107 @@
+// Shared device/host helpers for the Repurpose MI355X (gfx950) kernels.
+//
+// Conventions used by every kernel in this directory
+//   * element types: RP_F32 (float) and RP_BF16 (__bf16 storage, fp32 math)
+//   * one wavefront = 64 lanes; MFMA 16x16x32 bf16 / 16x16x4 f32 (exact-f32 parity mode)
+//   * every launcher is enqueued on the caller's hipStream_t and never synchronises
+//   * dropout masks are regenerated from a counter hash (seed, stream index), never stored
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <type_traits>
+
+#include "../../include/rp_api.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+#define RP_WAVE 64
+
+// ----------------------------------------------------------------------------------------------
+// host-side error plumbing (rp_last_error)
+// ----------------------------------------------------------------------------------------------
+void rp_set_error(const char* fmt, ...);
+int rp_check_launch(const char* what);
+
+#define RP_REQUIRE(cond, ...)                 \
+  do {                                        \
+    if (!(cond)) {                            \
+      rp_set_error(__VA_ARGS__);              \
+      return RP_ERR_ARG;                      \
+    }                                         \
+  } while (0)
+
+static inline bool rp_aligned16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
+
+// ----------------------------------------------------------------------------------------------
+// dropout hash: lowbias32-style finaliser over (seed, index).  keep <=> (h & 0xffff) >= thresh16
+// thresh16 = round(p * 65536); kept values are scaled by 1/(1-p).
+// ----------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rp_hash(uint32_t seed, uint32_t idx) {
+  uint32_t h = idx * 0x9E3779B1u + seed;
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ bool rp_keep(uint32_t seed, uint32_t idx, uint32_t thresh16) {
+  return (rp_hash(seed, idx) & 0xFFFFu) >= thresh16;
+}
+
+static inline uint32_t rp_dropout_thresh(float p) {
+  if (p <= 0.f) return 0u;
+  double t = (double)p * 65536.0 + 0.5;
+  if (t > 65536.0) t = 65536.0;
+  return (uint32_t)t;
+}
+
+// ----------------------------------------------------------------------------------------------
+// element load/store helpers (fp32 math everywhere)
+// ----------------------------------------------------------------------------------------------
+__device__ __forceinline__ float rp_ld(const float* p) { return *p; }
+__device__ __forceinline__ float rp_ld(const bf16* p) { return (float)(*p); }
+__device__ __forceinline__ void rp_st(float* p, float v) { *p = v; }
+__device__ __forceinline__ void rp_st(bf16* p, float v) { *p = (bf16)v; }
+
+template <typename T>
+struct rp_vec16;  // 16-byte vector of T
+template <>
+struct rp_vec16<float> {
+  typedef float4 type;
+  static constexpr int n = 4;
+};
+template <>
+struct rp_vec16<bf16> {
+  typedef uint4 type;
+  static constexpr int n = 8;
+};
+
+// wave-wide reductions (64 lanes)
+__device__ __forceinline__ float rp_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float rp_wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective workgroup remap (MI355X: 8 XCDs, blocks dealt round-robin).
+// Consecutive logical tiles end up on one XCD so they share its L2.
+__device__ __forceinline__ int rp_xcd_remap(int bid, int nwg) {
+  const int nx = 8;
+  int q = nwg / nx, r = nwg % nx;
+  int x = bid % nx, i = bid / nx;
+  int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + i;
+}

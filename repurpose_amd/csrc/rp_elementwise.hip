@@ -1,0 +1,324 @@
+// HBM-bound helpers of the hot path:
+//   rp_concat_rows      K1, modality concat (+ bf16 cast)      models/MMCTransformer.py:118
+//   rp_cast_f32_to_bf16 master-weight -> bf16 operand copy
+//   rp_colsum           bias / LayerNorm affine gradients (deterministic two-pass column sum)
+//   rp_focal_*          sigmoid_focal_loss (alpha .7, gamma 2) + mask + sum and its gradient
+//                       models/losses.py:4-53, models/MMCTransformer.py:159-179
+//   rp_rowdot_*         the N<=4 head outputs (cls_head[7], reg_head[7]+ReLU) :71-93
+//   rp_adam_step        torch.optim.Adam with coupled weight decay over one flat buffer
+#include <math.h>
+
+#include "rp_common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- concat / cast ------------
+template <typename TO>
+__global__ void concat_kernel(const float* __restrict__ v, int dv, const float* __restrict__ a, int da,
+                              const float* __restrict__ t, int dt, int64_t rows, TO* __restrict__ out) {
+  const int D = dv + da + dt;
+  const int64_t n4 = rows * (int64_t)(D / 4);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / (D / 4);
+    const int c = (int)(i % (D / 4)) * 4;
+    float4 q;
+    if (c < dv)
+      q = *reinterpret_cast<const float4*>(v + r * dv + c);
+    else if (c < dv + da)
+      q = *reinterpret_cast<const float4*>(a + r * da + (c - dv));
+    else
+      q = *reinterpret_cast<const float4*>(t + r * dt + (c - dv - da));
+    TO* o = out + r * D + c;
+    rp_st(o + 0, q.x);
+    rp_st(o + 1, q.y);
+    rp_st(o + 2, q.z);
+    rp_st(o + 3, q.w);
+  }
+}
+
+__global__ void cast_bf16_kernel(const float* __restrict__ s, bf16* __restrict__ d, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = (bf16)s[i];
+}
+
+inline unsigned grid_for(int64_t n, int bs) {
+  int64_t g = (n + bs - 1) / bs;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// ---------------------------------------------------------------- colsum -------------------
+constexpr int CS_ROWS = 256;
+constexpr int CS_THREADS = 256;
+
+template <typename T>
+__global__ void colsum_pass1(const T* __restrict__ X, int64_t rows, int64_t cols, int64_t ldx,
+                             const float* __restrict__ w, float* __restrict__ ws) {
+  const int64_t c = (int64_t)blockIdx.y * CS_THREADS + threadIdx.x;
+  if (c >= cols) return;
+  const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS;
+  int64_t r1 = r0 + CS_ROWS;
+  if (r1 > rows) r1 = rows;
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) {
+    float x = rp_ld(X + r * ldx + c);
+    s += w ? w[r] * x : x;
+  }
+  ws[(int64_t)blockIdx.x * cols + c] = s;
+}
+
+__global__ void colsum_pass2(const float* __restrict__ ws, int64_t nrb, int64_t cols, float* __restrict__ out,
+                             int accumulate) {
+  const int64_t c = (int64_t)blockIdx.x * CS_THREADS + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < nrb; ++b) s += ws[b * cols + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ---------------------------------------------------------------- focal loss ---------------
+struct Focal {
+  float loss, grad;
+};
+
+__device__ __forceinline__ Focal focal_eval(float x, float t, float alpha, float gamma, bool need_grad) {
+  const float p = 1.f / (1.f + expf(-x));
+  const float ce = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+  const float pt = p * t + (1.f - p) * (1.f - t);
+  const float omp = 1.f - pt;
+  const float mod = (gamma == 2.f) ? omp * omp : powf(omp, gamma);
+  const float at = alpha >= 0.f ? alpha * t + (1.f - alpha) * (1.f - t) : 1.f;
+  Focal f;
+  f.loss = at * ce * mod;
+  f.grad = 0.f;
+  if (need_grad) {
+    const float dmod = (gamma == 2.f) ? 2.f * omp : gamma * powf(omp, gamma - 1.f);
+    const float dpt = p * (1.f - p) * (2.f * t - 1.f);
+    f.grad = at * ((p - t) * mod - ce * dmod * dpt);
+  }
+  return f;
+}
+
+__global__ __launch_bounds__(1024) void focal_sum_kernel(const float* __restrict__ x, const float* __restrict__ t,
+                                                         const uint8_t* __restrict__ mask, int64_t n, float alpha,
+                                                         float gamma, float* __restrict__ loss) {
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (mask && !mask[i]) continue;
+    s += focal_eval(x[i], t[i], alpha, gamma, false).loss;
+  }
+  s = rp_wave_sum(s);
+  __shared__ float red[16];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += red[w];
+    *loss = tot;
+  }
+}
+
+__global__ void focal_elem_kernel(const float* __restrict__ x, const float* __restrict__ t, int64_t n, float alpha,
+                                  float gamma, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = focal_eval(x[i], t[i], alpha, gamma, false).loss;
+}
+
+__global__ void focal_bwd_kernel(const float* __restrict__ x, const float* __restrict__ t,
+                                 const uint8_t* __restrict__ mask, int64_t n, float alpha, float gamma,
+                                 const float* __restrict__ gout, int per_elem, float* __restrict__ dx) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float g = per_elem ? gout[i] : gout[0];
+    if (mask && !mask[i]) g = 0.f;
+    dx[i] = g == 0.f ? 0.f : g * focal_eval(x[i], t[i], alpha, gamma, true).grad;
+  }
+}
+
+// ---------------------------------------------------------------- rowdot (N <= 4) ----------
+template <typename T>
+__global__ __launch_bounds__(256) void rowdot_fwd_kernel(const T* __restrict__ X, int64_t ldx, int64_t rows, int K,
+                                                         const float* __restrict__ W, const float* __restrict__ b,
+                                                         int nout, int relu, float* __restrict__ out, int64_t ldo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k = lane; k < K; k += 64) {
+    const float xv = rp_ld(X + r * ldx + k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < nout) acc[j] += xv * W[(int64_t)j * K + k];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j >= nout) break;
+    float s = rp_wave_sum(acc[j]) + (b ? b[j] : 0.f);
+    if (relu) s = fmaxf(s, 0.f);
+    if (lane == 0) out[r * ldo + j] = s;
+  }
+}
+
+template <typename TG, typename TX>
+__global__ void rowdot_bwd_kernel(const float* __restrict__ dout, int64_t ldd, int64_t rows, int K,
+                                  const float* __restrict__ W, int nout, const TG* __restrict__ G, int64_t ldg,
+                                  float gate_scale, TX* __restrict__ dX, int64_t lddx) {
+  const int64_t n = rows * (int64_t)K;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / K;
+    const int k = (int)(i % K);
+    float s = 0.f;
+    for (int j = 0; j < nout; ++j) s += dout[r * ldd + j] * W[(int64_t)j * K + k];
+    if (G) s = rp_ld(G + r * ldg + k) > 0.f ? s * gate_scale : 0.f;
+    rp_st(dX + r * lddx + k, s);
+  }
+}
+
+// ---------------------------------------------------------------- Adam ---------------------
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, float lr_bc1, float beta1, float beta2, float eps,
+                            float wd, float sqrt_bc2, bf16* __restrict__ plp) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float pi = p[i];
+    float gi = g[i];
+    if (wd != 0.f) gi = gi + wd * pi;
+    float mi = m[i];
+    mi = mi + (1.f - beta1) * (gi - mi);
+    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    const float denom = sqrtf(vi) / sqrt_bc2 + eps;
+    pi = pi - lr_bc1 * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+    if (plp) plp[i] = (bf16)pi;
+  }
+}
+
+}  // namespace
+
+extern "C" int rp_concat_rows(const float* v, int dv, const float* a, int da, const float* t, int dt, int64_t rows,
+                              void* out, int out_dtype, void* stream) {
+  RP_REQUIRE(dv >= 0 && da >= 0 && dt >= 0 && rows >= 0, "rp_concat_rows: negative size");
+  RP_REQUIRE(dv % 4 == 0 && da % 4 == 0 && dt % 4 == 0, "rp_concat_rows: widths must be multiples of 4");
+  RP_REQUIRE((dv == 0 || v) && (da == 0 || a) && (dt == 0 || t) && out, "rp_concat_rows: null pointer");
+  const int64_t n4 = rows * (int64_t)((dv + da + dt) / 4);
+  if (n4 == 0) return RP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (out_dtype == RP_BF16)
+    hipLaunchKernelGGL(concat_kernel<bf16>, dim3(grid_for(n4, 256)), dim3(256), 0, s, v, dv, a, da, t, dt, rows, (bf16*)out);
+  else if (out_dtype == RP_F32)
+    hipLaunchKernelGGL(concat_kernel<float>, dim3(grid_for(n4, 256)), dim3(256), 0, s, v, dv, a, da, t, dt, rows, (float*)out);
+  else {
+    rp_set_error("rp_concat_rows: bad dtype");
+    return RP_ERR_ARG;
+  }
+  return rp_check_launch("rp_concat_rows");
+}
+
+extern "C" int rp_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream) {
+  RP_REQUIRE(n >= 0, "rp_cast_f32_to_bf16: negative n");
+  if (n == 0) return RP_OK;
+  RP_REQUIRE(src && dst, "rp_cast_f32_to_bf16: null");
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, src, (bf16*)dst, n);
+  return rp_check_launch("rp_cast_f32_to_bf16");
+}
+
+extern "C" int64_t rp_colsum_workspace(int64_t rows, int64_t cols) {
+  return ((rows + CS_ROWS - 1) / CS_ROWS) * cols;
+}
+
+extern "C" int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ldx, const float* w, float* out,
+                         int accumulate, float* workspace, void* stream) {
+  RP_REQUIRE(rows >= 0 && cols >= 0, "rp_colsum: negative size");
+  if (cols == 0) return RP_OK;
+  RP_REQUIRE(out && workspace, "rp_colsum: null output/workspace");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nrb = (rows + CS_ROWS - 1) / CS_ROWS;
+  if (nrb > 0) {
+    RP_REQUIRE(X, "rp_colsum: null X");
+    dim3 g1((unsigned)nrb, (unsigned)((cols + CS_THREADS - 1) / CS_THREADS));
+    if (dtype == RP_BF16)
+      hipLaunchKernelGGL(colsum_pass1<bf16>, g1, dim3(CS_THREADS), 0, s, (const bf16*)X, rows, cols, ldx, w, workspace);
+    else
+      hipLaunchKernelGGL(colsum_pass1<float>, g1, dim3(CS_THREADS), 0, s, (const float*)X, rows, cols, ldx, w, workspace);
+  }
+  hipLaunchKernelGGL(colsum_pass2, dim3((unsigned)((cols + CS_THREADS - 1) / CS_THREADS)), dim3(CS_THREADS), 0, s,
+                     workspace, nrb, cols, out, accumulate);
+  return rp_check_launch("rp_colsum");
+}
+
+extern "C" int rp_focal_fwd_sum(const float* x, const float* t, const uint8_t* mask, int64_t n, float alpha, float gamma,
+                                float* loss, void* stream) {
+  RP_REQUIRE(n >= 0 && loss, "rp_focal_fwd_sum: bad args");
+  RP_REQUIRE(n == 0 || (x && t), "rp_focal_fwd_sum: null input");
+  hipLaunchKernelGGL(focal_sum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, t, mask, n, alpha, gamma, loss);
+  return rp_check_launch("rp_focal_fwd_sum");
+}
+
+extern "C" int rp_focal_elementwise(const float* x, const float* t, int64_t n, float alpha, float gamma, float* out,
+                                    void* stream) {
+  RP_REQUIRE(n >= 0, "rp_focal_elementwise: negative n");
+  if (n == 0) return RP_OK;
+  RP_REQUIRE(x && t && out, "rp_focal_elementwise: null");
+  hipLaunchKernelGGL(focal_elem_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, x, t, n, alpha, gamma, out);
+  return rp_check_launch("rp_focal_elementwise");
+}
+
+extern "C" int rp_focal_bwd(const float* x, const float* t, const uint8_t* mask, int64_t n, float alpha, float gamma,
+                            const float* grad_out, int grad_per_elem, float* dx, void* stream) {
+  RP_REQUIRE(n >= 0, "rp_focal_bwd: negative n");
+  if (n == 0) return RP_OK;
+  RP_REQUIRE(x && t && grad_out && dx, "rp_focal_bwd: null");
+  hipLaunchKernelGGL(focal_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, x, t, mask, n, alpha,
+                     gamma, grad_out, grad_per_elem, dx);
+  return rp_check_launch("rp_focal_bwd");
+}
+
+extern "C" int rp_rowdot_fwd(int x_dtype, const void* X, int64_t ldx, int64_t rows, int K, const float* W, const float* b,
+                             int nout, int relu, float* out, int64_t ldo, void* stream) {
+  RP_REQUIRE(nout >= 1 && nout <= 4, "rp_rowdot_fwd: nout must be 1..4");
+  RP_REQUIRE(rows >= 0 && K > 0, "rp_rowdot_fwd: bad size");
+  if (rows == 0) return RP_OK;
+  RP_REQUIRE(X && W && out, "rp_rowdot_fwd: null");
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+  if (x_dtype == RP_BF16)
+    hipLaunchKernelGGL(rowdot_fwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)X, ldx, rows, K, W, b, nout, relu, out, ldo);
+  else
+    hipLaunchKernelGGL(rowdot_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)X, ldx, rows, K, W, b, nout, relu, out, ldo);
+  return rp_check_launch("rp_rowdot_fwd");
+}
+
+extern "C" int rp_rowdot_bwd_dx(const float* dout, int64_t ldd, int64_t rows, int K, const float* W, int nout, const void* G,
+                                int g_dtype, int64_t ldg, float gate_scale, void* dX, int dx_dtype, int64_t lddx,
+                                void* stream) {
+  RP_REQUIRE(nout >= 1 && nout <= 4, "rp_rowdot_bwd_dx: nout must be 1..4");
+  if (rows <= 0) return RP_OK;
+  RP_REQUIRE(dout && W && dX, "rp_rowdot_bwd_dx: null");
+  const int64_t n = rows * (int64_t)K;
+  dim3 grid(grid_for(n, 256));
+  hipStream_t s = (hipStream_t)stream;
+#define RP_RD_LAUNCH(TG, TX) \
+  hipLaunchKernelGGL((rowdot_bwd_kernel<TG, TX>), grid, dim3(256), 0, s, dout, ldd, rows, K, W, nout, (const TG*)G, ldg, gate_scale, (TX*)dX, lddx)
+  if (g_dtype == RP_BF16) {
+    if (dx_dtype == RP_BF16) RP_RD_LAUNCH(bf16, bf16); else RP_RD_LAUNCH(bf16, float);
+  } else {
+    if (dx_dtype == RP_BF16) RP_RD_LAUNCH(float, bf16); else RP_RD_LAUNCH(float, float);
+  }
+#undef RP_RD_LAUNCH
+  return rp_check_launch("rp_rowdot_bwd_dx");
+}
+
+extern "C" int rp_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                            float eps, float weight_decay, int step, void* p_lp, void* stream) {
+  RP_REQUIRE(n >= 0 && step >= 1, "rp_adam_step: bad n/step");
+  if (n == 0) return RP_OK;
+  RP_REQUIRE(p && g && m && v, "rp_adam_step: null");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  const float lr_bc1 = (float)(lr / bc1);
+  const float sqrt_bc2 = (float)sqrt(bc2);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr_bc1, beta1,
+                     beta2, eps, weight_decay, sqrt_bc2, (bf16*)p_lp);
+  return rp_check_launch("rp_adam_step");
+}

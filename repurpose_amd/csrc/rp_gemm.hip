@@ -1,0 +1,311 @@
+// rp_gemm — MFMA GEMM with fused epilogues for every nn.Linear on the Repurpose hot path
+// (input projection, MHA in/out projections, FFN linear1/linear2, feature_map, head hidden
+// layers; reference models/MMCTransformer.py:32-93 and the stock encoder layer built at :41-55).
+//
+// One kernel template serves the three shapes autograd needs for y = x W^T:
+//   forward  C = X  . W^T      A k-major (X [M,K]),    B k-major (W [N,K])
+//   dgrad    dX = dY . W       A k-major (dY [M,N]),   B n-major (W [N,K] read as [K][N])
+//   wgrad    dW = dY^T . X     A m-major (dY^T),       B n-major (X)
+// Layout-aware LDS staging: tiles are copied to LDS in their memory order (16-byte coalesced
+// loads), and fragments are read either row-wise (ds_read_b128) or column-wise with the gfx950
+// transposed read ds_read_b64_tr_b16 — no transposed copies of activations are ever written.
+//
+// Tile 128x128, 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16 tiles, register-staged double
+// buffer (one barrier per K step), XCD-aware tile order.  bf16: v_mfma_f32_16x16x32_bf16, K-step
+// 64; f32 parity mode: exact v_mfma_f32_16x16x4_f32, K-step 32.
+#include "rp_common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128;
+constexpr int NT = 256;
+constexpr int PAD = 16;  // bytes of padding per LDS row
+
+template <typename T>
+struct GemmCfg {
+  static constexpr int BK = 128 / (int)sizeof(T);          // 64 bf16 / 32 f32 -> 128-byte rows
+  static constexpr int KROW = BK * (int)sizeof(T) + PAD;   // bytes per k-major LDS row (144)
+  static constexpr int MROW = BM * (int)sizeof(T) + PAD;   // bytes per m-major LDS row
+  static constexpr int KTILE = BM * KROW;                  // bytes of a k-major tile
+  static constexpr int MTILE = BK * MROW;                  // bytes of an m-major tile
+  static constexpr int VEC = 16 / (int)sizeof(T);          // elements per 16-byte chunk
+};
+
+struct EpiDev {
+  const float* bias;
+  int relu;
+  uint32_t drop_thresh;
+  float drop_scale;
+  uint32_t drop_seed;
+  const float* residual;
+  int64_t ldr;
+  const void* gate;
+  int gate_bf16;
+  int64_t ldg;
+  float gate_scale;
+  int accumulate;
+};
+
+// --- global -> register staging -----------------------------------------------------------
+// Each operand tile is 1024 chunks of 16 bytes; 256 threads own 4 chunks each.
+template <typename T, bool KMAJ>
+__device__ __forceinline__ void stage_load(uint4 (&r)[4], const T* __restrict__ base, int64_t ld,
+                                           int64_t rows_lim /* M or N */, int64_t k_lim, int64_t row0,
+                                           int64_t k0, int tid) {
+  using C = GemmCfg<T>;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int id = tid + NT * i;
+    int64_t rr, cc;  // memory row / element column of this chunk
+    bool ok;
+    if (KMAJ) {  // tile [BM rows][BK] ; chunks per row = BK / VEC = 8
+      int row = id >> 3, c = id & 7;
+      rr = row0 + row;
+      cc = k0 + c * C::VEC;
+      ok = (rr < rows_lim) && (cc < k_lim);
+    } else {  // tile [BK rows (k)][BM cols] ; chunks per row = BM / VEC
+      constexpr int CPR = BM / C::VEC;
+      int row = id / CPR, c = id % CPR;
+      rr = k0 + row;
+      cc = row0 + c * C::VEC;
+      ok = (rr < k_lim) && (cc < rows_lim);
+    }
+    if (ok)
+      r[i] = *reinterpret_cast<const uint4*>(base + rr * ld + cc);
+    else
+      r[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
+template <typename T, bool KMAJ>
+__device__ __forceinline__ void stage_store(const uint4 (&r)[4], char* lds, int tid) {
+  using C = GemmCfg<T>;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int id = tid + NT * i;
+    int off;
+    if (KMAJ) {
+      int row = id >> 3, c = id & 7;
+      off = row * C::KROW + c * 16;
+    } else {
+      constexpr int CPR = BM / C::VEC;
+      int row = id / CPR, c = id % CPR;
+      off = row * C::MROW + c * 16;
+    }
+    *reinterpret_cast<uint4*>(lds + off) = r[i];
+  }
+}
+
+// --- fragment reads ----------------------------------------------------------------------
+// bf16: fragment of 16 rows x 32 k for v_mfma_f32_16x16x32_bf16:
+//   lane l holds X[row = l&15][k = 8*(l>>4) + j], j = 0..7
+__device__ __forceinline__ bf16x8 frag_bf16(const char* lds, bool kmaj, int rbase, int kbase, int lane) {
+  using C = GemmCfg<bf16>;
+  int g = lane >> 4, i = lane & 15;
+  if (kmaj) {
+    const char* p = lds + (rbase + i) * C::KROW + (kbase + 8 * g) * 2;
+    return *reinterpret_cast<const bf16x8*>(p);
+  } else {
+    int q = i >> 2, pp = i & 3;
+    const char* p0 = lds + (kbase + 8 * g + q) * C::MROW + (rbase + 4 * pp) * 2;
+    const char* p1 = p0 + 4 * C::MROW;
+    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p0));
+    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p1));
+    bf16x8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+}
+
+// f32: fragment for v_mfma_f32_16x16x4_f32: lane l holds X[row = l&15][k = l>>4]
+__device__ __forceinline__ float frag_f32(const char* lds, bool kmaj, int rbase, int kbase, int lane) {
+  using C = GemmCfg<float>;
+  int g = lane >> 4, i = lane & 15;
+  if (kmaj) return *reinterpret_cast<const float*>(lds + (rbase + i) * C::KROW + (kbase + g) * 4);
+  return *reinterpret_cast<const float*>(lds + (kbase + g) * C::MROW + (rbase + i) * 4);
+}
+
+template <typename T, bool AK, bool BKM>
+__device__ __forceinline__ void compute_tile(f32x4 (&acc)[4][4], const char* ldsA, const char* ldsB,
+                                             int wm, int wn, int lane) {
+  using C = GemmCfg<T>;
+  if constexpr (std::is_same<T, bf16>::value) {
+#pragma unroll
+    for (int ks = 0; ks < C::BK; ks += 32) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag_bf16(ldsA, AK, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = frag_bf16(ldsB, BKM, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < C::BK; ks += 4) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag_f32(ldsA, AK, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = frag_f32(ldsB, BKM, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+}
+
+template <typename T, bool AK, bool BKM, typename TC>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64_t K, const T* __restrict__ A,
+                                                     int64_t lda, const T* __restrict__ B, int64_t ldb,
+                                                     TC* __restrict__ Cout, int64_t ldc, float alpha,
+                                                     EpiDev ep) {
+  using C = GemmCfg<T>;
+  constexpr int TA = AK ? C::KTILE : C::MTILE;
+  constexpr int TB = BKM ? C::KTILE : C::MTILE;
+  __shared__ __attribute__((aligned(16))) char lds[2 * (TA + TB)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (int)((N + BN - 1) / BN);
+  const int tiles_m = (int)((M + BM - 1) / BM);
+  const int t = rp_xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int64_t m0 = (int64_t)(t / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(t % tiles_n) * BN;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[4], rb[4];
+  const int nk = (int)((K + C::BK - 1) / C::BK);
+  stage_load<T, AK>(ra, A, lda, M, K, m0, 0, tid);
+  stage_load<T, BKM>(rb, B, ldb, N, K, n0, 0, tid);
+  stage_store<T, AK>(ra, lds, tid);
+  stage_store<T, BKM>(rb, lds + TA, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = lds + (kt & 1) * (TA + TB);
+    char* nxt = lds + ((kt + 1) & 1) * (TA + TB);
+    const bool more = (kt + 1) < nk;
+    if (more) {
+      stage_load<T, AK>(ra, A, lda, M, K, m0, (int64_t)(kt + 1) * C::BK, tid);
+      stage_load<T, BKM>(rb, B, ldb, N, K, n0, (int64_t)(kt + 1) * C::BK, tid);
+    }
+    compute_tile<T, AK, BKM>(acc, cur, cur + TA, wm, wn, lane);
+    if (more) {
+      stage_store<T, AK>(ra, nxt, tid);
+      stage_store<T, BKM>(rb, nxt + TA, tid);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: C-layout col = lane&15, row = (lane>>4)*4 + r ----
+  const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t n = n0 + wn * 64 + j * 16 + cl;
+    if (n >= N) continue;
+    const float bias = ep.bias ? ep.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 64 + i * 16 + g * 4 + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r] * alpha + bias;
+        if (ep.relu) v = fmaxf(v, 0.f);
+        if (ep.drop_thresh) {
+          uint32_t idx = (uint32_t)(m * N + n);
+          v = rp_keep(ep.drop_seed, idx, ep.drop_thresh) ? v * ep.drop_scale : 0.f;
+        }
+        if (ep.gate) {
+          float gv = ep.gate_bf16 ? (float)((const bf16*)ep.gate)[m * ep.ldg + n]
+                                  : ((const float*)ep.gate)[m * ep.ldg + n];
+          v = gv > 0.f ? v * ep.gate_scale : 0.f;
+        }
+        if (ep.residual) v += ep.residual[m * ep.ldr + n];
+        TC* dst = Cout + m * ldc + n;
+        if constexpr (std::is_same<TC, float>::value) {
+          if (ep.accumulate) v += *dst;
+        }
+        rp_st(dst, v);
+      }
+    }
+  }
+}
+
+template <typename T, typename TC>
+int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int ak, const void* B,
+                  int64_t ldb, int bk, void* Cp, int64_t ldc, float alpha, const EpiDev& ep,
+                  hipStream_t s) {
+  int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  dim3 grid((unsigned)tiles), block(NT);
+  const T* a = (const T*)A;
+  const T* b = (const T*)B;
+  TC* c = (TC*)Cp;
+  if (ak && bk)
+    hipLaunchKernelGGL((gemm_kernel<T, true, true, TC>), grid, block, 0, s, M, N, K, a, lda, b, ldb, c, ldc, alpha, ep);
+  else if (ak && !bk)
+    hipLaunchKernelGGL((gemm_kernel<T, true, false, TC>), grid, block, 0, s, M, N, K, a, lda, b, ldb, c, ldc, alpha, ep);
+  else if (!ak && !bk)
+    hipLaunchKernelGGL((gemm_kernel<T, false, false, TC>), grid, block, 0, s, M, N, K, a, lda, b, ldb, c, ldc, alpha, ep);
+  else
+    hipLaunchKernelGGL((gemm_kernel<T, false, true, TC>), grid, block, 0, s, M, N, K, a, lda, b, ldb, c, ldc, alpha, ep);
+  return rp_check_launch("rp_gemm");
+}
+
+}  // namespace
+
+extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int a_kmajor,
+                       const void* B, int64_t ldb, int b_kmajor, void* C, int64_t ldc, int c_dtype, float alpha,
+                       const rp_gemm_epilogue* ep, void* stream) {
+  RP_REQUIRE(dtype == RP_F32 || dtype == RP_BF16, "rp_gemm: bad dtype %d", dtype);
+  RP_REQUIRE(c_dtype == RP_F32 || c_dtype == RP_BF16, "rp_gemm: bad c_dtype %d", c_dtype);
+  RP_REQUIRE(M >= 0 && N >= 0 && K >= 0, "rp_gemm: negative size");
+  if (M == 0 || N == 0) return RP_OK;
+  RP_REQUIRE(A && B && C, "rp_gemm: null operand");
+  const int64_t vec = 8;
+  RP_REQUIRE(K % vec == 0, "rp_gemm: K=%lld must be a multiple of 8", (long long)K);
+  RP_REQUIRE(lda % vec == 0 && ldb % vec == 0 && ldc % vec == 0, "rp_gemm: leading dims must be multiples of 8");
+  RP_REQUIRE(a_kmajor || M % vec == 0, "rp_gemm: m-major A needs M %% 8 == 0");
+  RP_REQUIRE(b_kmajor || N % vec == 0, "rp_gemm: n-major B needs N %% 8 == 0");
+  RP_REQUIRE(rp_aligned16(A) && rp_aligned16(B), "rp_gemm: operands must be 16-byte aligned");
+  RP_REQUIRE(a_kmajor ? lda >= K : lda >= M, "rp_gemm: lda too small");
+  RP_REQUIRE(b_kmajor ? ldb >= K : ldb >= N, "rp_gemm: ldb too small");
+  RP_REQUIRE(ldc >= N, "rp_gemm: ldc too small");
+  EpiDev e{};
+  e.gate_scale = 1.f;
+  if (ep) {
+    e.bias = ep->bias;
+    e.relu = ep->relu;
+    e.drop_thresh = rp_dropout_thresh(ep->dropout_p);
+    e.drop_scale = ep->dropout_p > 0.f ? 1.f / (1.f - ep->dropout_p) : 1.f;
+    e.drop_seed = ep->dropout_seed;
+    e.residual = ep->residual;
+    e.ldr = ep->ldr;
+    e.gate = ep->gate;
+    e.gate_bf16 = ep->gate_dtype == RP_BF16;
+    e.ldg = ep->ldg;
+    e.gate_scale = ep->gate_scale;
+    e.accumulate = ep->accumulate;
+    RP_REQUIRE(!e.accumulate || c_dtype == RP_F32, "rp_gemm: accumulate needs an fp32 C");
+    RP_REQUIRE(!e.drop_thresh || M * N < (int64_t)UINT32_MAX, "rp_gemm: dropout index overflow");
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RP_BF16) {
+    if (c_dtype == RP_BF16) return launch_gemm_t<bf16, bf16>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, e, s);
+    return launch_gemm_t<bf16, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, e, s);
+  }
+  if (c_dtype == RP_BF16) return launch_gemm_t<float, bf16>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, e, s);
+  return launch_gemm_t<float, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, e, s);
+}

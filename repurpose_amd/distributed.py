@@ -1,0 +1,336 @@
+"""Drop-in ``utils/distributed.py`` (reference) for one process per MI355X, RCCL over xGMI.
+
+API kept from the reference (``utils/distributed.py``): ``MultiGPUStrategy(strategy, backend,
+timeout, find_unused_parameters)`` with ``setup() -> bool`` (:355-389), ``wrap_model`` (:396-433,
+returns a wrapper exposing ``.module`` as the trainer needs at ``main.py:323-326``),
+``create_dataloader`` (:435-473, ``DistributedSampler`` partitioning), ``reduce_tensor`` (:475-498),
+``barrier``, ``cleanup``, ``print_setup_info``, ``get_effective_batch_size``, ``save_checkpoint`` /
+``load_checkpoint``; free functions ``setup_distributed``, ``cleanup_distributed``, ``get_rank``,
+``get_world_size``, ``is_main_process``, ``get_device``, ``detect_slurm_env``,
+``auto_select_strategy`` and the ``DistributedManager`` context manager.
+
+What changes underneath (MI355X-first, not a translation of torch DDP):
+
+* gradients live in ONE flat fp32 buffer (``MMCTransformer.flat_grads``).  ``GradAllReducer``
+  receives "this contiguous range is final" callbacks from the hand-written backward (encoder
+  layers finish in reverse order), coalesces them into ~``bucket_mb`` buckets and issues one
+  asynchronous RCCL all-reduce per bucket (``backend="nccl"`` is RCCL on ROCm) while the backward
+  of earlier layers keeps the GPU busy; the last wait is enqueued (stream-ordered, no host sync)
+  at the end of backward, so ``.grad`` is averaged when ``loss.backward()`` returns, as with DDP;
+* the DDP per-forward buffer broadcast (the constant ``pe`` table) and the unused-parameter
+  bitmap all-reduce are dropped: the unused set (``reg_head``) is static;
+* parameters are broadcast from rank 0 once, as one flat buffer, at wrap time (C2).
+"""
+import datetime
+import logging
+import os
+import socket
+import time
+from typing import Any, Dict, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+log = logging.getLogger(__name__)
+
+
+def find_free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def detect_slurm_env() -> Dict[str, Any]:
+    """Reference ``utils/distributed.py:32-74`` (SLURM_* variables -> rank / world / master)."""
+    env = os.environ
+    info = {"is_slurm": "SLURM_PROCID" in env and "SLURM_NTASKS" in env}
+    if info["is_slurm"]:
+        nodes = env.get("SLURM_JOB_NODELIST", env.get("SLURM_NODELIST", "127.0.0.1"))
+        master = nodes.split(",")[0].split("[")[0]
+        info.update(rank=int(env["SLURM_PROCID"]), world_size=int(env["SLURM_NTASKS"]),
+                    local_rank=int(env.get("SLURM_LOCALID", 0)), master_addr=env.get("MASTER_ADDR", master),
+                    master_port=int(env.get("MASTER_PORT", 29500)))
+    return info
+
+
+def setup_distributed(rank: int, world_size: int, backend: str = "nccl", master_addr: str = "127.0.0.1",
+                      master_port: Optional[str] = None, timeout: int = 1800) -> bool:
+    """Initialise the process group and run the reference's comm self-test (:180-193)."""
+    try:
+        s = detect_slurm_env()
+        if s["is_slurm"]:
+            rank, world_size, local_rank = s["rank"], s["world_size"], s["local_rank"]
+            master_addr, master_port = s["master_addr"], str(s["master_port"])
+        else:
+            rank = int(os.environ.get("RANK", rank))
+            world_size = int(os.environ.get("WORLD_SIZE", world_size))
+            master_addr = os.environ.get("MASTER_ADDR", master_addr)
+            ndev = torch.cuda.device_count() if torch.cuda.is_available() else 1
+            local_rank = int(os.environ.get("LOCAL_RANK", rank % max(ndev, 1)))
+            master_port = master_port or os.environ.get("MASTER_PORT") or str(find_free_port())
+        os.environ.update(MASTER_ADDR=master_addr, MASTER_PORT=str(master_port), RANK=str(rank),
+                          WORLD_SIZE=str(world_size), LOCAL_RANK=str(local_rank))
+        kw = {}
+        if backend == "nccl":
+            dev = local_rank % torch.cuda.device_count()
+            torch.cuda.set_device(dev)
+            kw["device_id"] = torch.device("cuda", dev)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world_size,
+                                timeout=datetime.timedelta(seconds=timeout), **kw)
+        probe = torch.ones(1, device=torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else "cpu")
+        dist.all_reduce(probe)
+        if abs(probe.item() - world_size) > 1e-6:
+            log.error("distributed self-test failed: %s != %s", probe.item(), world_size)
+            return False
+        return True
+    except Exception as e:  # the reference reports and returns False (:197-202)
+        log.error("failed to set up distributed training: %s", e)
+        return False
+
+
+def cleanup_distributed():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def get_rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def get_world_size() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def is_main_process() -> bool:
+    return get_rank() == 0
+
+
+def get_device() -> torch.device:
+    if torch.cuda.is_available():
+        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)) % torch.cuda.device_count())
+    return torch.device("cpu")
+
+
+# ---------------------------------------------------------------------------------------------
+class GradAllReducer:
+    """Bucketed, backward-overlapped gradient averaging over a flat gradient buffer.
+
+    ``ready(lo, hi)`` is called by the backward whenever flat range [lo, hi) holds final gradients
+    (ranges arrive in reverse layout order); ``finish()`` closes the step.  Works with any object
+    exposing ``flat_grads()``, ``trainable_numel()`` and ``_grad_ready_hooks``.
+    """
+
+    def __init__(self, model, bucket_mb: float = 25.0, group=None):
+        self.model = model
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.bucket_elems = max(1, int(bucket_mb * 2 ** 20 / 4))
+        self.backend = dist.get_backend(group)
+        self.pending = None  # [lo, hi) not yet launched
+        self.works = []
+        self.launched = []
+        model._grad_ready_hooks = [self.ready]
+        model._grad_done_hooks = [self.finish]
+
+    def _launch(self, lo, hi):
+        g = self.model.flat_grads()[lo:hi]
+        if self.backend == "nccl":
+            w = dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+            self.works.append((w, None))
+        else:  # gloo has no AVG
+            w = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self.works.append((w, g))
+        self.launched.append((lo, hi))
+
+    def ready(self, lo, hi):
+        n = self.model.trainable_numel()
+        hi = min(hi, n)
+        if lo >= hi:
+            return
+        if self.pending is None:
+            self.pending = [lo, hi]
+        elif hi == self.pending[0]:  # ranges arrive in reverse layout order
+            self.pending[0] = lo
+        elif lo == self.pending[1]:
+            self.pending[1] = hi
+        else:
+            self._launch(*self.pending)
+            self.pending = [lo, hi]
+        if self.pending[1] - self.pending[0] >= self.bucket_elems:
+            self._launch(*self.pending)
+            self.pending = None
+
+    def finish(self):
+        if self.pending is not None:
+            self._launch(*self.pending)
+            self.pending = None
+        for w, g in self.works:
+            w.wait()  # stream-ordered for RCCL: no host synchronisation
+            if g is not None:
+                g.div_(self.world)
+        self.works = []
+
+    def wait(self):
+        self.finish()
+        covered = sorted(self.launched)
+        self.launched = []
+        return covered
+
+
+class DistributedModel(nn.Module):
+    """What ``wrap_model`` returns under DDP: ``.module`` is the drop-in model, forward delegates,
+    gradients are averaged by a ``GradAllReducer`` inside backward."""
+
+    def __init__(self, module, bucket_mb=25.0, broadcast=True):
+        super().__init__()
+        self.module = module
+        if broadcast:
+            flat = module.flat_params()
+            dist.broadcast(flat, src=0)
+        self.reducer = GradAllReducer(module, bucket_mb=bucket_mb)
+
+    def forward(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
+
+
+class MultiGPUStrategy:
+    """Reference ``utils/distributed.py:242-625`` with RCCL underneath."""
+
+    def __init__(self, strategy: str = "auto", backend: str = "nccl", timeout: int = 1800,
+                 find_unused_parameters: bool = False):
+        self.logger = log
+        self.strategy = strategy
+        self.backend = backend
+        self.timeout = timeout
+        self.find_unused_parameters = find_unused_parameters  # static unused set: nothing to find
+        self.world_size, self.rank, self.local_rank = 1, 0, 0
+        self.device = torch.device("cpu")
+        self.is_distributed = False
+        self.slurm_info = detect_slurm_env()
+        if strategy == "auto":
+            self.strategy = self._auto_detect_strategy()
+        self._setup_device_info()
+
+    def _auto_detect_strategy(self) -> str:
+        if self.slurm_info["is_slurm"] and self.slurm_info["world_size"] > 1:
+            return "ddp"
+        if "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            return "ddp"
+        if not torch.cuda.is_available():
+            return "single"
+        return "ddp" if torch.cuda.device_count() > 1 else "single"
+
+    def _setup_device_info(self):
+        if self.strategy in ("single", "dp"):
+            if self.strategy == "dp":
+                # single-process DataParallel cannot replicate a flat-buffer model; one process per
+                # GPU (ddp) is the MI355X path, 'dp' runs on one device
+                self.logger.warning("strategy 'dp' runs single-device on MI355X; launch one process per GPU")
+            self.device = get_device()
+            self.world_size, self.rank, self.local_rank = 1, 0, 0
+            return
+        self.is_distributed = True
+        if self.slurm_info["is_slurm"]:
+            self.rank, self.world_size = self.slurm_info["rank"], self.slurm_info["world_size"]
+            self.local_rank = self.slurm_info["local_rank"]
+        elif "RANK" in os.environ:
+            self.rank = int(os.environ["RANK"])
+            self.world_size = int(os.environ["WORLD_SIZE"])
+            ndev = torch.cuda.device_count() if torch.cuda.is_available() else 1
+            self.local_rank = int(os.environ.get("LOCAL_RANK", self.rank % max(ndev, 1)))
+        else:
+            self.rank, self.local_rank = 0, 0
+            self.world_size = torch.cuda.device_count() if torch.cuda.is_available() else 1
+        self.device = (torch.device("cuda", self.local_rank) if torch.cuda.is_available() and self.backend == "nccl"
+                       else torch.device("cpu"))
+
+    def setup(self) -> bool:
+        if self.strategy == "ddp" and self.world_size > 1:
+            s = self.slurm_info
+            addr = s["master_addr"] if s["is_slurm"] else os.environ.get("MASTER_ADDR", "127.0.0.1")
+            port = str(s["master_port"]) if s["is_slurm"] else os.environ.get("MASTER_PORT")
+            ok = setup_distributed(self.rank, self.world_size, self.backend, addr, port, self.timeout)
+            if not ok:  # reference falls back and reports success (:379-386)
+                self.logger.warning("DDP setup failed, continuing on a single device")
+                self.strategy, self.is_distributed, self.world_size, self.rank = "single", False, 1, 0
+                return True
+            return True
+        return True
+
+    def cleanup(self):
+        if self.strategy == "ddp":
+            cleanup_distributed()
+
+    def wrap_model(self, model: nn.Module) -> nn.Module:
+        model = model.to(self.device)
+        if self.strategy == "ddp" and self.world_size > 1:
+            return DistributedModel(model)
+        return model
+
+    def create_dataloader(self, dataset, batch_size: int, shuffle: bool = True, num_workers: int = 0, **kwargs):
+        from torch.utils.data import DataLoader
+        from torch.utils.data.distributed import DistributedSampler
+        sampler = None
+        if self.strategy == "ddp" and self.world_size > 1:
+            sampler = DistributedSampler(dataset, num_replicas=self.world_size, rank=self.rank, shuffle=shuffle)
+            shuffle = False
+        return DataLoader(dataset, batch_size=batch_size, shuffle=shuffle, sampler=sampler, num_workers=num_workers,
+                          pin_memory=torch.cuda.is_available(), **kwargs)
+
+    def reduce_tensor(self, tensor: torch.Tensor, average: bool = True) -> torch.Tensor:
+        if self.strategy != "ddp" or self.world_size <= 1:
+            return tensor
+        out = tensor.clone()
+        dist.all_reduce(out, op=dist.ReduceOp.SUM)
+        if average:
+            out /= self.world_size
+        return out
+
+    def barrier(self):
+        if self.strategy == "ddp" and self.world_size > 1:
+            dist.barrier()
+
+    def print_setup_info(self):
+        if is_main_process():
+            self.logger.info("strategy=%s world=%d rank=%d device=%s backend=%s", self.strategy.upper(),
+                             self.world_size, self.rank, self.device, self.backend)
+
+    def save_checkpoint(self, state_dict: Dict[str, Any], filepath: str):
+        if not is_main_process():
+            return
+        m = state_dict.get("model")
+        if hasattr(m, "module"):
+            state_dict["model"] = m.module.state_dict()
+        torch.save(state_dict, filepath)
+
+    def load_checkpoint(self, model: nn.Module, filepath: str, optimizer=None) -> Dict[str, Any]:
+        ckpt = torch.load(filepath, map_location=self.device, weights_only=True)
+        if "model" in ckpt:
+            (model.module if hasattr(model, "module") else model).load_state_dict(ckpt["model"])
+        if optimizer is not None and "optimizer" in ckpt:
+            optimizer.load_state_dict(ckpt["optimizer"])
+        return ckpt
+
+    def get_effective_batch_size(self, batch_size: int) -> int:
+        return batch_size * self.world_size if self.strategy == "ddp" else batch_size
+
+
+def auto_select_strategy() -> str:
+    """Reference :628-657 recommends dp for 2-4 GPUs; on MI355X one process per GPU is always used."""
+    if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
+        return "single"
+    return "ddp"
+
+
+class DistributedManager:
+    def __init__(self, strategy: str = "auto", backend: str = "nccl"):
+        self.strategy_manager = MultiGPUStrategy(strategy, backend)
+
+    def __enter__(self):
+        if not self.strategy_manager.setup():
+            raise RuntimeError("Failed to setup distributed training")
+        return self.strategy_manager
+
+    def __exit__(self, exc_type, exc_val, exc_tb):
+        self.strategy_manager.cleanup()

@@ -1,0 +1,316 @@
+"""Thin torch-tensor front end of the C ABI (``include/rp_api.h``).
+
+Every function validates device / dtype / layout on the host, then enqueues the HIP kernel on the
+current torch stream through ``_native.call``.  Outputs are allocated with the torch caching
+allocator; the library itself never allocates.  There is no CPU path: CPU tensors raise.
+"""
+import ctypes
+
+import torch
+
+from . import _native as N
+
+_DT = {torch.float32: N.RP_F32, torch.bfloat16: N.RP_BF16}
+
+# Live per-kernel timing with HIP events recorded on the launch stream (bench.py roofline).
+_timer = {"name": None, "ev": []}
+
+
+def timer_start(name):
+    _timer["name"] = name
+    _timer["ev"] = []
+
+
+def timer_stop():
+    """Average duration (ms) of the timed kernel's launches since timer_start, or None."""
+    ev = _timer["ev"]
+    _timer["name"] = None
+    _timer["ev"] = []
+    if not ev:
+        return None
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+
+
+def _tick(name):
+    if _timer["name"] != name:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def _tock(e0):
+    if e0 is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        _timer["ev"].append((e0, e1))
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _dt(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"repurpose_amd: unsupported dtype {t.dtype} (float32 / bfloat16)") from None
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("repurpose_amd: HIP kernels need tensors on a ROCm device "
+                               f"(got {t.device}); there is no CPU path")
+
+
+def _contig(*ts):
+    for t in ts:
+        if t is not None and not t.is_contiguous():
+            raise ValueError("repurpose_amd: tensor must be contiguous")
+
+
+# ------------------------------------------------------------------------------------- K1, casts
+def concat_rows(v, a, t, out_dtype):
+    """[v | a | t] along the last dim; inputs [..., d] fp32 -> [rows, dv+da+dt] of out_dtype."""
+    _gpu(v, a, t)
+    v, a, t = (x.contiguous().float() for x in (v, a, t))
+    rows = v.numel() // max(v.shape[-1], 1) if v.shape[-1] else a.numel() // max(a.shape[-1], 1)
+    dv, da, dt = v.shape[-1], a.shape[-1], t.shape[-1]
+    out = torch.empty(rows, dv + da + dt, device=v.device, dtype=out_dtype)
+    N.call("rp_concat_rows", _p(v), dv, _p(a), da, _p(t), dt, rows, _p(out), _DT[out_dtype], _stream(v))
+    return out
+
+
+def cast_bf16(src, dst):
+    _gpu(src, dst)
+    _contig(src, dst)
+    assert src.dtype == torch.float32 and dst.dtype == torch.bfloat16 and src.numel() == dst.numel()
+    N.call("rp_cast_f32_to_bf16", _p(src), _p(dst), src.numel(), _stream(src))
+    return dst
+
+
+# ------------------------------------------------------------------------------------- GEMM
+def gemm(A, B, C, M, Nn, K, lda, a_kmajor, ldb, b_kmajor, ldc, alpha=1.0, bias=None, relu=False,
+         dropout_p=0.0, seed=0, residual=None, ldr=0, gate=None, ldg=0, gate_scale=1.0,
+         accumulate=False):
+    """Raw rp_gemm (see include/rp_api.h for the operand conventions)."""
+    _gpu(A, B, C, bias, residual, gate)
+    if A.dtype != B.dtype:
+        raise TypeError("rp_gemm: A and B must share a dtype")
+    ep = N.GemmEpilogue(_p(bias).value, int(relu), float(dropout_p), int(seed) & 0xFFFFFFFF,
+                        _p(residual).value, int(ldr), _p(gate).value,
+                        _dt(gate) if gate is not None else 0, int(ldg), float(gate_scale),
+                        int(accumulate))
+    N.call("rp_gemm", _dt(A), int(M), int(Nn), int(K), _p(A), int(lda), int(a_kmajor), _p(B), int(ldb),
+           int(b_kmajor), _p(C), int(ldc), _dt(C), float(alpha), ctypes.byref(ep), _stream(A))
+    return C
+
+
+def linear_fwd(x, W, b=None, out_dtype=None, relu=False, dropout_p=0.0, seed=0, residual=None, tag=None):
+    """y = epilogue(x W^T + b); x [M, K], W [N, K] (same dtype), residual fp32 [M, N]."""
+    M, K = x.shape
+    Nn = W.shape[0]
+    out = torch.empty(M, Nn, device=x.device, dtype=out_dtype or x.dtype)
+    e0 = _tick(tag) if tag else None
+    gemm(x, W, out, M, Nn, K, K, True, K, True, Nn, bias=b, relu=relu, dropout_p=dropout_p,
+         seed=seed, residual=residual, ldr=Nn)
+    _tock(e0)
+    return out
+
+
+def linear_dgrad(dy, W, out_dtype, gate=None, gate_scale=1.0):
+    """dx = (dy W) [* gate_scale * (gate > 0)]; dy [M, N], W [N, K] -> [M, K]."""
+    M, Nn = dy.shape
+    K = W.shape[1]
+    out = torch.empty(M, K, device=dy.device, dtype=out_dtype)
+    return gemm(dy, W, out, M, K, Nn, Nn, True, K, False, K, gate=gate, ldg=K, gate_scale=gate_scale)
+
+
+def linear_wgrad(dy, x, dW, accumulate=True):
+    """dW (+)= dy^T x ; dy [M, N], x [M, K], dW fp32 [N, K]."""
+    M, Nn = dy.shape
+    K = x.shape[1]
+    return gemm(dy, x, dW, Nn, K, M, Nn, False, K, False, K, accumulate=accumulate)
+
+
+# ------------------------------------------------------------------------------------- LayerNorm
+def layernorm_fwd(x, gamma, beta, eps=1e-5, pe=None, pe_period=1, relu=False, dropout_p=0.0, seed=0,
+                  out_f32=True, lp_dtype=None, save_stats=True):
+    _gpu(x, gamma, beta, pe)
+    rows, D = x.shape
+    of = torch.empty(rows, D, device=x.device, dtype=torch.float32) if out_f32 else None
+    ol = torch.empty(rows, D, device=x.device, dtype=lp_dtype) if lp_dtype is not None else None
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32) if save_stats else None
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32) if save_stats else None
+    a = N.LnFwdArgs(_p(x).value, _dt(x), x.stride(0), _p(gamma).value, _p(beta).value, float(eps),
+                    _p(pe).value, int(pe_period), int(relu), float(dropout_p), int(seed) & 0xFFFFFFFF,
+                    _p(of).value, D, _p(ol).value, _dt(ol) if ol is not None else 0, D, _p(mean).value,
+                    _p(rstd).value)
+    N.call("rp_layernorm_fwd", rows, D, ctypes.byref(a), _stream(x))
+    return of, ol, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, y=None, dropout_p=0.0, seed=0, dres=None, want_f32=True,
+                  lp_dtype=None, lp_dropout_p=0.0, lp_seed=0, dgamma=None, dbeta=None, ws=None):
+    """Returns (dx_f32, dx_lp); accumulates dgamma / dbeta (fp32 [D]) when given."""
+    _gpu(dy, x, mean, rstd, gamma, y, dres)
+    rows, D = x.shape
+    dev = x.device
+    dx = torch.empty(rows, D, device=dev, dtype=torch.float32) if want_f32 else None
+    dxl = torch.empty(rows, D, device=dev, dtype=lp_dtype) if lp_dtype is not None else None
+    nb = N.load().rp_layernorm_bwd_blocks(rows)
+    pg = torch.empty(nb, D, device=dev, dtype=torch.float32) if dgamma is not None else None
+    pb = torch.empty(nb, D, device=dev, dtype=torch.float32) if dbeta is not None else None
+    a = N.LnBwdArgs(_p(dy).value, _dt(dy), dy.stride(0), _p(x).value, _dt(x), x.stride(0),
+                    _p(mean).value, _p(rstd).value, _p(gamma).value, _p(y).value,
+                    _dt(y) if y is not None else 0, y.stride(0) if y is not None else 0,
+                    float(dropout_p), int(seed) & 0xFFFFFFFF, _p(dres).value, D, _p(dx).value, D,
+                    _p(dxl).value, _dt(dxl) if dxl is not None else 0, D, float(lp_dropout_p),
+                    int(lp_seed) & 0xFFFFFFFF, _p(pg).value, _p(pb).value)
+    N.call("rp_layernorm_bwd", rows, D, ctypes.byref(a), _stream(x))
+    if dgamma is not None:
+        colsum(pg, out=dgamma, accumulate=True, ws=ws)
+    if dbeta is not None:
+        colsum(pb, out=dbeta, accumulate=True, ws=ws)
+    return dx, dxl
+
+
+# ------------------------------------------------------------------------------------- reductions
+def colsum(X, w=None, out=None, accumulate=False, ws=None):
+    """out[c] (+)= sum_r w[r] X[r, c] (deterministic)."""
+    _gpu(X, w, out)
+    rows, cols = X.shape
+    if out is None:
+        out = torch.empty(cols, device=X.device, dtype=torch.float32)
+    need = N.load().rp_colsum_workspace(rows, cols)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(max(need, 1), device=X.device, dtype=torch.float32)
+    N.call("rp_colsum", _p(X), _dt(X), rows, cols, X.stride(0), _p(w), _p(out), int(accumulate), _p(ws),
+           _stream(X))
+    return out
+
+
+# ------------------------------------------------------------------------------------- attention
+def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0):
+    _gpu(qkv, key_valid)
+    _contig(qkv, key_valid)
+    dk = qkv.shape[1] // (3 * H)
+    out = torch.empty(B * T, H * dk, device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
+    e0 = _tick("attn_fwd")
+    N.call("rp_attn_fwd", _dt(qkv), _p(qkv), _p(key_valid), B, T, H, dk, float(scale), float(dropout_p),
+           int(seed) & 0xFFFFFFFF, _p(out), _p(lse), _stream(qkv))
+    _tock(e0)
+    return out, lse
+
+
+def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0):
+    _gpu(qkv, out, dout, lse, key_valid)
+    _contig(qkv, out, dout, lse, key_valid)
+    dk = qkv.shape[1] // (3 * H)
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
+    e0 = _tick("attn_bwd")
+    N.call("rp_attn_bwd", _dt(qkv), _p(qkv), _p(out), _p(dout), _p(lse), _p(key_valid), B, T, H, dk,
+           float(scale), float(dropout_p), int(seed) & 0xFFFFFFFF, _p(dqkv), _p(delta), _stream(qkv))
+    _tock(e0)
+    return dqkv
+
+
+# ------------------------------------------------------------------------------------- focal loss
+def focal_fwd_sum(x, t, mask=None, alpha=0.7, gamma=2.0):
+    _gpu(x, t, mask)
+    x, t = x.contiguous().float(), t.contiguous().float()
+    m = mask.contiguous().view(torch.uint8) if mask is not None else None
+    loss = torch.empty((), device=x.device, dtype=torch.float32)
+    N.call("rp_focal_fwd_sum", _p(x), _p(t), _p(m), x.numel(), float(alpha), float(gamma), _p(loss),
+           _stream(x))
+    return loss
+
+
+def focal_elementwise(x, t, alpha=0.7, gamma=2.0):
+    _gpu(x, t)
+    x, t = x.contiguous().float(), t.contiguous().float()
+    out = torch.empty_like(x)
+    N.call("rp_focal_elementwise", _p(x), _p(t), x.numel(), float(alpha), float(gamma), _p(out),
+           _stream(x))
+    return out
+
+
+def focal_bwd(x, t, mask, grad_out, alpha=0.7, gamma=2.0, per_elem=False):
+    _gpu(x, t, mask, grad_out)
+    x, t = x.contiguous().float(), t.contiguous().float()
+    m = mask.contiguous().view(torch.uint8) if mask is not None else None
+    g = grad_out.contiguous().float()
+    dx = torch.empty_like(x)
+    N.call("rp_focal_bwd", _p(x), _p(t), _p(m), x.numel(), float(alpha), float(gamma), _p(g),
+           int(per_elem), _p(dx), _stream(x))
+    return dx
+
+
+# ------------------------------------------------------------------------------------- small heads
+def rowdot_fwd(X, W, b=None, relu=False):
+    _gpu(X, W, b)
+    rows, K = X.shape
+    nout = W.shape[0]
+    out = torch.empty(rows, nout, device=X.device, dtype=torch.float32)
+    N.call("rp_rowdot_fwd", _dt(X), _p(X), X.stride(0), rows, K, _p(W), _p(b), nout, int(relu), _p(out),
+           nout, _stream(X))
+    return out
+
+
+def rowdot_bwd_dx(dout, W, gate=None, gate_scale=1.0, out_dtype=torch.float32):
+    _gpu(dout, W, gate)
+    rows, nout = dout.shape
+    K = W.shape[1]
+    dX = torch.empty(rows, K, device=dout.device, dtype=out_dtype)
+    N.call("rp_rowdot_bwd_dx", _p(dout), dout.stride(0), rows, K, _p(W), nout, _p(gate),
+           _dt(gate) if gate is not None else 0, gate.stride(0) if gate is not None else 0,
+           float(gate_scale), _p(dX), _DT[out_dtype], K, _stream(dout))
+    return dX
+
+
+# ------------------------------------------------------------------------------------- optimizer
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, p_lp=None):
+    _gpu(p, g, m, v, p_lp)
+    N.call("rp_adam_step", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
+           float(eps), float(weight_decay), int(step), _p(p_lp), _stream(p))
+
+
+# ------------------------------------------------------------------------------------- inference
+def infer_select(logits, mask, offsets, thresh, topk, dur_min, dur_max):
+    """logits [B, T] fp32, mask [B, T] bool, offsets [B, T, 2] -> (count, idx, score, seg)."""
+    _gpu(logits, mask, offsets)
+    B, T = logits.shape
+    logits = logits.contiguous().float()
+    offsets = offsets.contiguous().float()
+    m = mask.contiguous().view(torch.uint8)
+    dev = logits.device
+    count = torch.empty(B, device=dev, dtype=torch.int32)
+    idx = torch.empty(B, max(topk, 1), device=dev, dtype=torch.int64)
+    score = torch.empty(B, max(topk, 1), device=dev, dtype=torch.float32)
+    seg = torch.empty(B, max(topk, 1), 2, device=dev, dtype=torch.float32)
+    N.call("rp_infer_select", _p(logits), _p(m), _p(offsets), B, T, float(thresh), int(topk),
+           float(dur_min), float(dur_max), _p(count), _p(idx), _p(score), _p(seg), _stream(logits))
+    return count, idx, score, seg
+
+
+def softnms(scores, segs, count, sigma, thresh, max_seg, want_final_scores=False):
+    """scores [B, cap], segs [B, cap, 2], count/max_seg int32 [B] -> (keep [B, cap], keep_count)."""
+    _gpu(scores, segs, count, max_seg)
+    B, cap = scores.shape
+    scores, segs = scores.contiguous().float(), segs.contiguous().float()
+    count = count.contiguous().to(torch.int32)
+    max_seg = max_seg.contiguous().to(torch.int32)
+    keep = torch.empty(B, max(cap, 1), device=scores.device, dtype=torch.int32)
+    keep_count = torch.empty(B, device=scores.device, dtype=torch.int32)
+    final = torch.empty_like(scores) if want_final_scores else None
+    N.call("rp_softnms", _p(scores), _p(segs), _p(count), B, cap, float(sigma), float(thresh), _p(max_seg),
+           _p(keep), _p(keep_count), _p(final), _stream(scores))
+    return keep, keep_count, final

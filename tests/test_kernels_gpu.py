@@ -1,0 +1,258 @@
+"""Per-kernel numerics on the GPU, each HIP kernel against a plain PyTorch fp32/fp64 reference of
+the same op (dropout masks reproduced by a torch restatement of the counter hash)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from repurpose_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+M32 = 0xFFFFFFFF
+
+
+def rp_hash(seed, idx):
+    h = (idx * 0x9E3779B1 + seed) & M32
+    h = h ^ (h >> 16)
+    h = (h * 0x7FEB352D) & M32
+    h = h ^ (h >> 15)
+    h = (h * 0x846CA68B) & M32
+    h = h ^ (h >> 16)
+    return h
+
+
+def keep_mask(seed, idx, p):
+    thr = int(p * 65536 + 0.5)
+    return (rp_hash(seed, idx) & 0xFFFF) >= thr
+
+
+def rnd(*shape, dev, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dev)
+
+
+def close(a, b, atol, rtol=0.0, what=""):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    err = (a - b).abs()
+    lim = atol + rtol * b.abs()
+    bad = (err > lim).sum().item()
+    assert bad == 0, f"{what}: {bad} elements off, max err {err.max().item():.3e}"
+
+
+# ----------------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(256, 128, 64), (300, 136, 200), (17, 520, 2944), (1000, 1536, 512)])
+def test_gemm_three_layouts(dev, dtype, M, N, K):
+    x = rnd(M, K, dev=dev, seed=1).to(dtype)
+    w = rnd(N, K, dev=dev, seed=2, scale=0.05).to(dtype)
+    b = rnd(N, dev=dev, seed=3)
+    tol = 2e-4 if dtype == torch.float32 else 2e-3
+    xd, wd = x.double(), w.double()
+    y = K.linear_fwd(x, w, b, out_dtype=torch.float32)
+    close(y, xd @ wd.T + b.double(), atol=tol * math.sqrt(K), what="fwd")
+    dy = rnd(M, N, dev=dev, seed=4).to(dtype)
+    dx = K.linear_dgrad(dy, w, out_dtype=torch.float32)
+    close(dx, dy.double() @ wd, atol=tol * math.sqrt(N), what="dgrad")
+    dW = torch.full((N, K), 0.5, device=dev)
+    K.linear_wgrad(dy, x, dW, accumulate=True)
+    close(dW, dy.double().T @ xd + 0.5, atol=tol * math.sqrt(M) * 2, what="wgrad")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dev, dtype):
+    M, N, K = 384, 256, 128
+    x = rnd(M, K, dev=dev, seed=5).to(dtype)
+    w = rnd(N, K, dev=dev, seed=6, scale=0.1).to(dtype)
+    b = rnd(N, dev=dev, seed=7)
+    res = rnd(M, N, dev=dev, seed=8)
+    p, seed = 0.1, 12345
+    y = K.linear_fwd(x, w, b, out_dtype=torch.float32, relu=True, dropout_p=p, seed=seed, residual=res)
+    z = torch.relu(x.double() @ w.double().T + b.double())
+    idx = torch.arange(M * N, device=dev, dtype=torch.int64).view(M, N)
+    keep = keep_mask(seed, idx, p)
+    ref = torch.where(keep, z / (1 - p), torch.zeros_like(z)) + res.double()
+    tol = 1e-4 if dtype == torch.float32 else 2e-3
+    close(y, ref, atol=tol * 20, what="relu+dropout+residual")
+    frac = 1 - keep.float().mean().item()
+    assert abs(frac - 0.1) < 0.01
+    # gate (relu/dropout backward) with bf16 output
+    gate = rnd(M, N, dev=dev, seed=9).to(dtype)
+    dy = rnd(M, K, dev=dev, seed=10).to(dtype)
+    dx = K.linear_dgrad(dy, w.t().contiguous(), out_dtype=dtype, gate=gate, gate_scale=1.25)
+    ref = (dy.double() @ w.double().T) * 1.25 * (gate.double() > 0)
+    close(dx, ref, atol=(1e-4 if dtype == torch.float32 else 3e-2), rtol=(0 if dtype == torch.float32 else 1e-2),
+          what="gate")
+
+
+def test_gemm_identity_asymmetric(dev):
+    # A = I with an asymmetric B catches a transposed C write (guide §3)
+    n = 128
+    eye = torch.eye(n, device=dev, dtype=torch.bfloat16)
+    B = (torch.arange(n * n, device=dev).view(n, n) % 251).to(torch.bfloat16)
+    y = K.linear_fwd(eye, B, None, out_dtype=torch.float32)
+    assert torch.equal(y, B.float().T)
+
+
+# ----------------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("D", [256, 512])
+def test_layernorm_fwd_bwd(dev, D):
+    rows = 333
+    x = rnd(rows, D, dev=dev, seed=1, scale=3.0) + 0.5
+    gam = rnd(D, dev=dev, seed=2) * 0.2 + 1
+    bet = rnd(D, dev=dev, seed=3) * 0.1
+    T = 37
+    pe = rnd(1, 64, D, dev=dev, seed=4)
+    of, ol, mu, rs = K.layernorm_fwd(x, gam, bet, pe=pe, pe_period=T, lp_dtype=torch.bfloat16)
+    xr = x.double().requires_grad_(True)
+    ln = torch.nn.functional.layer_norm(xr, (D,), gam.double(), bet.double(), 1e-5)
+    ref = ln + pe[0].double()[torch.arange(rows, device=dev) % T]
+    close(of, ref.detach(), atol=2e-5, what="ln fwd")
+    close(ol, ref.detach(), atol=3e-2, rtol=1e-2, what="ln fwd bf16")
+    dy = rnd(rows, D, dev=dev, seed=5)
+    dres = rnd(rows, D, dev=dev, seed=6)
+    dg = torch.zeros(D, device=dev)
+    db = torch.zeros(D, device=dev)
+    dx, _ = K.layernorm_bwd(dy, x, mu, rs, gam, dres=dres, dgamma=dg, dbeta=db)
+    gr = torch.autograd.grad(ln, xr, dy.double())[0] + dres.double()
+    close(dx, gr, atol=2e-4, what="ln bwd dx")
+    xhat = (x.double() - x.double().mean(1, keepdim=True)) / torch.sqrt(x.double().var(1, unbiased=False, keepdim=True) + 1e-5)
+    close(dg, (dy.double() * xhat).sum(0), atol=5e-3, what="dgamma")
+    close(db, dy.double().sum(0), atol=5e-3, what="dbeta")
+
+
+def test_layernorm_relu_dropout(dev):
+    rows, D, p, seed = 200, 512, 0.1, 777
+    x = rnd(rows, D, dev=dev, seed=11)
+    gam = torch.ones(D, device=dev)
+    bet = rnd(D, dev=dev, seed=12) * 0.3
+    of, _, mu, rs = K.layernorm_fwd(x, gam, bet, relu=True, dropout_p=p, seed=seed)
+    xr = x.double().requires_grad_(True)
+    z = torch.relu(torch.nn.functional.layer_norm(xr, (D,), gam.double(), bet.double(), 1e-5))
+    keep = keep_mask(seed, torch.arange(rows * D, device=dev).view(rows, D), p)
+    ref = torch.where(keep, z / (1 - p), torch.zeros_like(z))
+    close(of, ref.detach(), atol=5e-5, what="ln relu dropout")
+    dy = rnd(rows, D, dev=dev, seed=13)
+    dx, dxl = K.layernorm_bwd(dy, x, mu, rs, gam, y=of, dropout_p=p, seed=seed, lp_dtype=torch.bfloat16,
+                              lp_dropout_p=p, lp_seed=99)
+    gr = torch.autograd.grad(ref, xr, dy.double())[0]
+    close(dx, gr, atol=3e-4, what="ln relu dropout bwd")
+    k2 = keep_mask(99, torch.arange(rows * D, device=dev).view(rows, D), p)
+    close(dxl, torch.where(k2, gr / (1 - p), torch.zeros_like(gr)), atol=3e-2, rtol=1e-2, what="masked lp dx")
+
+
+# ----------------------------------------------------------------------------------- attention
+def attn_ref(qkv, kv, B, T, H, p=0.0, seed=0):
+    dk = qkv.shape[1] // (3 * H)
+    q, k, v = qkv.view(B, T, 3, H, dk).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(dk)
+    s = s.masked_fill(~kv.bool().view(B, 1, 1, T), float("-inf"))
+    P = torch.softmax(s, -1)
+    if p > 0:
+        dev = qkv.device
+        bh = torch.arange(B * H, device=dev, dtype=torch.int64)
+        sbh = rp_hash(seed, bh).view(B, H, 1, 1)
+        qi = torch.arange(T, device=dev, dtype=torch.int64).view(1, 1, T, 1)
+        ki = torch.arange(T, device=dev, dtype=torch.int64).view(1, 1, 1, T)
+        keep = keep_mask(sbh, qi * T + ki, p)
+        P = torch.where(keep, P / (1 - p), torch.zeros_like(P))
+    o = P @ v
+    return o.permute(0, 2, 1, 3).reshape(B * T, H * dk)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("T,p", [(64, 0.0), (100, 0.0), (200, 0.1), (256, 0.0)])
+def test_attention_fwd_bwd(dev, dtype, T, p):
+    B, H = 2, 8
+    qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(dtype)
+    lens = torch.tensor([T, max(1, T - 37)], device=dev)
+    kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
+    seed = 4242
+    o, lse = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed)
+    ref_in = qkv.double().requires_grad_(True)
+    ref = attn_ref(ref_in, kv, B, T, H, p, seed)
+    ftol = 2e-5 if dtype == torch.float32 else 2e-2
+    close(o, ref.detach(), atol=ftol, rtol=ftol, what="attn fwd")
+    do = rnd(B * T, H * 64, dev=dev, seed=T + 1).to(dtype)
+    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, seed)
+    gref = torch.autograd.grad(ref, ref_in, do.double())[0]
+    btol = 1e-4 if dtype == torch.float32 else 6e-2
+    close(dqkv, gref, atol=btol, rtol=btol, what="attn bwd")
+
+
+def test_attention_lse(dev):
+    B, H, T = 1, 8, 96
+    qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=3)
+    kv = torch.ones(B, T, dtype=torch.uint8, device=dev)
+    _, lse = K.attn_fwd(qkv, kv, B, T, H, 0.125)
+    q, k, _ = qkv.double().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = torch.logsumexp((q @ k.transpose(-1, -2)) * 0.125, -1)
+    close(lse, ref, atol=1e-5, what="lse")
+
+
+# ----------------------------------------------------------------------------------- small ops
+def test_focal_fused(dev):
+    n = 5000
+    x = rnd(n, dev=dev, seed=1, scale=4)
+    t = (rnd(n, dev=dev, seed=2) > 0).float()
+    m = (rnd(n, dev=dev, seed=3) > -0.5).to(torch.uint8)
+    xr = x.double().requires_grad_(True)
+    pr = torch.sigmoid(xr)
+    ce = torch.nn.functional.binary_cross_entropy_with_logits(xr, t.double(), reduction="none")
+    pt = pr * t + (1 - pr) * (1 - t)
+    fl = (0.7 * t + 0.3 * (1 - t)) * ce * (1 - pt) ** 2
+    ref = (fl * m).sum()
+    s = K.focal_fwd_sum(x, t, m)
+    close(s, ref.detach(), atol=1e-3, rtol=1e-5, what="focal sum")
+    g = torch.tensor(1.7, device=dev)
+    dx = K.focal_bwd(x, t, m, g.view(1))
+    gr = torch.autograd.grad(ref * 1.7, xr)[0]
+    close(dx, gr, atol=1e-6, rtol=1e-4, what="focal grad")
+    close(K.focal_elementwise(x, t), fl.detach(), atol=1e-6, rtol=1e-5, what="focal elementwise")
+
+
+def test_rowdot_colsum_concat_cast(dev):
+    rows, Kd = 777, 256
+    X = rnd(rows, Kd, dev=dev, seed=1)
+    W = rnd(2, Kd, dev=dev, seed=2) * 0.1
+    b = rnd(2, dev=dev, seed=3)
+    out = K.rowdot_fwd(X, W, b, relu=True)
+    close(out, torch.relu(X.double() @ W.double().T + b.double()), atol=1e-5, what="rowdot")
+    dout = rnd(rows, 2, dev=dev, seed=4)
+    G = rnd(rows, Kd, dev=dev, seed=5)
+    dX = K.rowdot_bwd_dx(dout, W, gate=G, gate_scale=2.0)
+    close(dX, (dout.double() @ W.double()) * 2 * (G > 0), atol=1e-5, what="rowdot bwd")
+    w = rnd(rows, dev=dev, seed=6)
+    cs = K.colsum(X, w=w)
+    close(cs, (X.double() * w.double()[:, None]).sum(0), atol=1e-3, what="colsum")
+    Xb = X.to(torch.bfloat16)
+    close(K.colsum(Xb), Xb.double().sum(0), atol=1e-3, what="colsum bf16")
+    v = rnd(3, 5, 8, dev=dev, seed=7)
+    a = rnd(3, 5, 16, dev=dev, seed=8)
+    t = rnd(3, 5, 4, dev=dev, seed=9)
+    cat = K.concat_rows(v, a, t, torch.float32)
+    assert torch.equal(cat, torch.cat([v, a, t], -1).view(15, 28))
+    catb = K.concat_rows(v, a, t, torch.bfloat16)
+    assert torch.equal(catb, torch.cat([v, a, t], -1).view(15, 28).to(torch.bfloat16))
+    dst = torch.empty(15 * 28, dtype=torch.bfloat16, device=dev)
+    K.cast_bf16(cat.view(-1), dst)
+    assert torch.equal(dst, cat.view(-1).to(torch.bfloat16))
+
+
+def test_adam_matches_torch(dev):
+    n = 10_000
+    p0 = rnd(n, dev=dev, seed=1)
+    p_ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([p_ref], lr=1e-3, weight_decay=1e-4)
+    p = p0.clone()
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    plp = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    for step in range(1, 4):
+        g = rnd(n, dev=dev, seed=10 + step)
+        p_ref.grad = g.clone()
+        opt.step()
+        K.adam_step(p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 1e-4, step, p_lp=plp)
+    close(p, p_ref.detach(), atol=1e-6, what="adam")
+    assert torch.equal(plp, p.to(torch.bfloat16))

@@ -1,0 +1,169 @@
+"""End-to-end parity of the drop-in MMCTransformer (HIP path) with the CPU oracle.
+
+Gates: fp32 per-frame logits within 1e-3 of the oracle on identical weights/inputs
+(eval, no dropout); fp32 gradients match the oracle's autograd; bf16 logits within 5e-2 (reported).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.mmct_oracle import MMCTransformer as Oracle
+from repurpose_amd.MMCTransformer import MMCTransformer
+from repurpose_amd.optim import FusedAdam
+
+pytestmark = pytest.mark.gpu
+
+TRI = dict(vis_dim=512, aud_dim=2048, text_dim=384, d_model=512, self_num_layers=2, text_num_layers=3,
+           cross_num_layers=3, num_heads=8)
+VIDEO_ONLY = dict(TRI, aud_dim=0, text_dim=0)  # configs[0]: video-only 2-layer (Da = Dt = 0)
+
+
+def make_batch(cfg, B, T, lens, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return {"visual_feats": torch.randn(B, T, cfg["vis_dim"], generator=g),
+            "audio_feats": torch.relu(torch.randn(B, T, cfg["aud_dim"], generator=g)),
+            "text_feats": torch.randn(B, T, cfg["text_dim"], generator=g),
+            "masks": (torch.arange(T)[None] < torch.tensor(lens)[:, None]).unsqueeze(1),
+            "labels": (torch.rand(B, T, generator=g) < 0.35).float(),
+            "segments": torch.rand(B, T, 2, generator=g) * 10,
+            "video_id": [f"v{i}" for i in range(B)], "duration": [int(l) for l in lens]}
+
+
+def pair(cfg, dtype, seed=0):
+    torch.manual_seed(seed)
+    ref = Oracle(**cfg)
+    torch.manual_seed(seed)
+    m = MMCTransformer(**cfg, compute_dtype=dtype)
+    return ref, m
+
+
+def to_dev(b, dev):
+    return {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in b.items()}
+
+
+@pytest.mark.parametrize("cfg,B,T,lens", [(VIDEO_ONLY, 2, 128, [128, 128]), (TRI, 2, 100, [100, 61]),
+                                          (TRI, 3, 257, [257, 200, 130])])
+def test_forward_fp32_parity(dev, cfg, B, T, lens):
+    ref, m = pair(cfg, "fp32")
+    ref.eval()
+    m.to(dev).eval()
+    b = make_batch(cfg, B, T, lens)
+    with torch.no_grad():
+        r = ref(b)
+        out = m(to_dev(b, dev))
+    valid = b["masks"][:, 0, :]
+    err = (out[1].cpu() - r[1])[valid].abs().max().item()
+    assert err < 1e-3, f"logits max err {err}"
+    err_off = (out[2].cpu() - r[2])[valid].abs().max().item()
+    assert err_off < 1e-3, f"offsets max err {err_off}"
+    err_f = (out[5].cpu() - r[5])[valid].abs().max().item()
+    assert err_f < 1e-3, f"feats max err {err_f}"
+    lr = ref.losses(*r)["cls_loss"].item()
+    lm = m.losses(*out)["cls_loss"].item()
+    assert abs(lr - lm) < 1e-3 * max(1.0, abs(lr))
+    assert out[0] is b["masks"] or torch.equal(out[0].cpu(), b["masks"])
+
+
+def test_forward_matches_golden_fixture(dev):
+    from tests.golden.make_golden import CFG, model_inputs
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_model_L2.npz"))
+    torch.manual_seed(0)
+    m = MMCTransformer(**CFG, compute_dtype="fp32").to(dev).eval()
+    b = model_inputs()
+    with torch.no_grad():
+        out = m(to_dev(b, dev))
+        loss = m.losses(*out)["cls_loss"].item()
+    valid = b["masks"][:, 0, :].numpy()
+    assert np.abs(out[1].cpu().numpy() - d["logits"])[valid].max() < 1e-3
+    assert abs(loss - float(d["loss"])) < 1e-3 * max(1.0, abs(float(d["loss"])))
+
+
+def test_backward_fp32_parity(dev):
+    cfg = TRI
+    ref, m = pair(cfg, "fp32", seed=3)
+    ref.eval()  # dropout off; autograd runs the slow (training) path of nn.TransformerEncoderLayer
+    m.to(dev).train()
+    m.DROPOUT = 0.0
+    b = make_batch(cfg, 2, 96, [96, 70], seed=5)
+    r = ref(b)
+    lr = ref.losses(*r)["cls_loss"]
+    lr.backward()
+    out = m(to_dev(b, dev))
+    lm = m.losses(*out)["cls_loss"]
+    lm.backward()
+    torch.cuda.synchronize()
+    worst = []
+    for (n, p), (n2, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert n == n2
+        if n.startswith("reg_head."):
+            assert p.grad is None and q.grad is None
+            continue
+        g, gr = p.grad.cpu().double(), q.grad.double()
+        scale = gr.abs().max().item() + 1e-6
+        rel = (g - gr).abs().max().item() / scale
+        worst.append((rel, n))
+        assert rel < 2e-3, f"{n}: rel err {rel:.2e}"
+    print("worst grad rel err", max(worst))
+
+
+def test_bf16_forward_close(dev):
+    ref, m = pair(TRI, "bf16", seed=1)
+    ref.eval()
+    m.to(dev).eval()
+    b = make_batch(TRI, 2, 160, [160, 120], seed=2)
+    with torch.no_grad():
+        r = ref(b)
+        out = m(to_dev(b, dev))
+    valid = b["masks"][:, 0, :]
+    err = (out[1].float().cpu() - r[1])[valid].abs().max().item()
+    print("bf16 logits max err", err)
+    assert err < 5e-2
+
+
+def test_train_step_dropout_deterministic_and_adam(dev):
+    torch.manual_seed(0)
+    m = MMCTransformer(**TRI, compute_dtype="bf16").to(dev).train()
+    b = to_dev(make_batch(TRI, 2, 128, [128, 90], seed=9), dev)
+    grads = []
+    for _ in range(2):
+        torch.manual_seed(77)  # dropout seeds come from the torch CPU generator
+        m.zero_grad(set_to_none=True)
+        out = m(b)
+        loss = m.losses(*out)["cls_loss"]
+        loss.backward()
+        torch.cuda.synchronize()
+        grads.append(m.flat_grads().clone())
+        assert torch.isfinite(loss).item()
+    assert torch.equal(grads[0], grads[1]), "same seed must give bitwise-identical gradients"
+    # FusedAdam == torch Adam on the same gradients
+    n = m.trainable_numel()
+    p0 = m.flat_params()[:n].clone()
+    ref = p0.clone().requires_grad_(True)
+    topt = torch.optim.Adam([ref], lr=1e-3, weight_decay=1e-4)
+    ref.grad = grads[1][:n].clone()
+    topt.step()
+    opt = FusedAdam(m, lr=1e-3, weight_decay=1e-4)
+    opt.step()
+    torch.cuda.synchronize()
+    assert (m.flat_params()[:n] - ref.detach()).abs().max().item() < 1e-6
+    # the bf16 operand copy was refreshed by the same kernel
+    assert torch.equal(m.lowp_weights()[:n], m.flat_params()[:n].to(torch.bfloat16))
+
+
+def test_torch_adam_also_drives_the_model(dev):
+    """The reference trainer's torch.optim.Adam over model.parameters() works unchanged."""
+    torch.manual_seed(0)
+    m = MMCTransformer(**TRI, compute_dtype="bf16").to(dev).train()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    b = to_dev(make_batch(TRI, 2, 64, [64, 50], seed=4), dev)
+    losses = []
+    for _ in range(3):
+        opt.zero_grad()
+        out = m(b)
+        loss = m.losses(*out)["cls_loss"] / 2
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert all(np.isfinite(losses))
+    assert all(p.grad is None for n, p in m.named_parameters() if n.startswith("reg_head."))
