@@ -31,6 +31,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from . import _native
 from . import kernels as K
 from .losses import focal_loss_masked_sum
 from .softnms import soft_nms_intervals_cpu  # noqa: F401  (re-exported, reference import site)
@@ -149,11 +150,11 @@ class MMCTransformer(nn.Module):
         params = self._ordered_params()
         device = device or params[0][1].device
         total = sum(p.numel() for _, p in params)
-        # 16-byte align every tensor so GEMM operands are aligned
+        # align every tensor to 8 elements: 16-byte aligned in the fp32 master AND the bf16 copy
         layout, off = {}, 0
         for n, p in params:
             layout[n] = (off, tuple(p.shape))
-            off += (p.numel() + 3) // 4 * 4
+            off += (p.numel() + 7) // 8 * 8
         flat = torch.zeros(off, device=device, dtype=_F32)
         with torch.no_grad():
             for n, p in params:
@@ -225,7 +226,7 @@ class MMCTransformer(nn.Module):
         for n in self._names:
             if any(n.startswith(p) for p in prefixes):
                 o, shp = self._layout[n]
-                e = o + (int(np.prod(shp)) + 3) // 4 * 4  # include the alignment pad: ranges tile
+                e = o + (int(np.prod(shp)) + 7) // 8 * 8  # include the alignment pad: ranges tile
                 lo = o if lo is None else min(lo, o)
                 hi = e if hi is None else max(hi, e)
         return lo, hi
@@ -430,7 +431,7 @@ class _Schedule:
         sd = self.scale_drop
         S = self.saved
         self._g = m._bind_grads()
-        ws = torch.empty(max(K._native.load().rp_colsum_workspace(M, max(m.d_ff, 3 * m.d_model)), 1),
+        ws = torch.empty(max(_native.load().rp_colsum_workspace(M, max(m.d_ff, 3 * m.d_model)), 1),
                          device=dlogits.device, dtype=_F32)
         G = self.G
 

@@ -275,7 +275,7 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
   if (M == 0 || N == 0) return RP_OK;
   RP_REQUIRE(A && B && C, "rp_gemm: null operand");
   const int64_t vec = 8;
-  RP_REQUIRE(K % vec == 0, "rp_gemm: K=%lld must be a multiple of 8", (long long)K);
+  RP_REQUIRE((!a_kmajor && !b_kmajor) || K % vec == 0, "rp_gemm: K=%lld must be a multiple of 8", (long long)K);
   RP_REQUIRE(lda % vec == 0 && ldb % vec == 0 && ldc % vec == 0, "rp_gemm: leading dims must be multiples of 8");
   RP_REQUIRE(a_kmajor || M % vec == 0, "rp_gemm: m-major A needs M %% 8 == 0");
   RP_REQUIRE(b_kmajor || N % vec == 0, "rp_gemm: n-major B needs N %% 8 == 0");

@@ -43,28 +43,28 @@ def close(a, b, atol, rtol=0.0, what=""):
 
 # ----------------------------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,N,K", [(256, 128, 64), (300, 136, 200), (17, 520, 2944), (1000, 1536, 512)])
-def test_gemm_three_layouts(dev, dtype, M, N, K):
-    x = rnd(M, K, dev=dev, seed=1).to(dtype)
-    w = rnd(N, K, dev=dev, seed=2, scale=0.05).to(dtype)
+@pytest.mark.parametrize("M,N,Kd", [(256, 128, 64), (300, 136, 200), (17, 520, 2944), (1000, 1536, 512)])
+def test_gemm_three_layouts(dev, dtype, M, N, Kd):
+    x = rnd(M, Kd, dev=dev, seed=1).to(dtype)
+    w = rnd(N, Kd, dev=dev, seed=2, scale=0.05).to(dtype)
     b = rnd(N, dev=dev, seed=3)
     tol = 2e-4 if dtype == torch.float32 else 2e-3
     xd, wd = x.double(), w.double()
     y = K.linear_fwd(x, w, b, out_dtype=torch.float32)
-    close(y, xd @ wd.T + b.double(), atol=tol * math.sqrt(K), what="fwd")
+    close(y, xd @ wd.T + b.double(), atol=tol * math.sqrt(Kd), what="fwd")
     dy = rnd(M, N, dev=dev, seed=4).to(dtype)
     dx = K.linear_dgrad(dy, w, out_dtype=torch.float32)
     close(dx, dy.double() @ wd, atol=tol * math.sqrt(N), what="dgrad")
-    dW = torch.full((N, K), 0.5, device=dev)
+    dW = torch.full((N, Kd), 0.5, device=dev)
     K.linear_wgrad(dy, x, dW, accumulate=True)
     close(dW, dy.double().T @ xd + 0.5, atol=tol * math.sqrt(M) * 2, what="wgrad")
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_epilogues(dev, dtype):
-    M, N, K = 384, 256, 128
-    x = rnd(M, K, dev=dev, seed=5).to(dtype)
-    w = rnd(N, K, dev=dev, seed=6, scale=0.1).to(dtype)
+    M, N, Kd = 384, 256, 128
+    x = rnd(M, Kd, dev=dev, seed=5).to(dtype)
+    w = rnd(N, Kd, dev=dev, seed=6, scale=0.1).to(dtype)
     b = rnd(N, dev=dev, seed=7)
     res = rnd(M, N, dev=dev, seed=8)
     p, seed = 0.1, 12345
@@ -79,7 +79,7 @@ def test_gemm_epilogues(dev, dtype):
     assert abs(frac - 0.1) < 0.01
     # gate (relu/dropout backward) with bf16 output
     gate = rnd(M, N, dev=dev, seed=9).to(dtype)
-    dy = rnd(M, K, dev=dev, seed=10).to(dtype)
+    dy = rnd(M, Kd, dev=dev, seed=10).to(dtype)
     dx = K.linear_dgrad(dy, w.t().contiguous(), out_dtype=dtype, gate=gate, gate_scale=1.25)
     ref = (dy.double() @ w.double().T) * 1.25 * (gate.double() > 0)
     close(dx, ref, atol=(1e-4 if dtype == torch.float32 else 3e-2), rtol=(0 if dtype == torch.float32 else 1e-2),
