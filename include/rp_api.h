@@ -79,6 +79,17 @@ int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t l
             const void* B, int64_t ldb, int b_kmajor, void* C, int64_t ldc, int c_dtype, float alpha,
             const rp_gemm_epilogue* ep, void* stream);
 
+/* Weight gradient of a Linear layer: dW[m, n] (+)= sum_k dY[k, m] * X[k, n] and (if db)
+ * db[m] (+)= sum_k dY[k, m] — the token dimension K is split over workgroups (deterministic
+ * split-K: fp32 partial slabs in `workspace`, reduced in a fixed order); the bias gradient is
+ * accumulated from the dY tiles the GEMM already stages (no separate pass over dY).
+ * dY [K, ldy] and X [K, ldx] share `dtype`; dW is fp32 [M, N] contiguous.
+ * workspace: at least rp_gemm_wgrad_workspace(M, N, K) bytes, 16-byte aligned. */
+int64_t rp_gemm_wgrad_workspace(int64_t M, int64_t N, int64_t K);
+int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, int64_t ldy, const void* X,
+                  int64_t ldx, float* dW, float* db, int accumulate, void* workspace, int64_t ws_bytes,
+                  void* stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* LayerNorm over the last dim D (<= 4096, multiple of 4), one row per wavefront.
  * y = ((x - mean) * rstd) * gamma + beta;  y += pe[(row % pe_period) * D + c] if pe;

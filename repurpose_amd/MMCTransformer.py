@@ -431,12 +431,17 @@ class _Schedule:
         sd = self.scale_drop
         S = self.saved
         self._g = m._bind_grads()
-        ws = torch.empty(max(_native.load().rp_colsum_workspace(M, max(m.d_ff, 3 * m.d_model)), 1),
-                         device=dlogits.device, dtype=_F32)
+        lib = _native.load()
+        ws = torch.empty(max(lib.rp_colsum_workspace(M, 256), 1), device=dlogits.device, dtype=_F32)
+        d, dff = m.d_model, m.d_ff
+        din = m.vis_dim + m.aud_dim + m.text_dim
+        shapes = [(3 * d, d), (d, d), (dff, d), (d, dff), (d, din), (256, d), (256, 256), (d, d)]
+        wws = torch.empty(max(lib.rp_gemm_wgrad_workspace(a, b, M) for a, b in shapes) // 4 + 4,
+                          device=dlogits.device, dtype=_F32)
         G = self.G
 
-        def bias_grad(dy, name):
-            K.colsum(dy, out=G(name), accumulate=True, ws=ws)
+        def wgrad(dy, x, wname, bname):
+            K.linear_wgrad(dy, x, G(wname), db=G(bname), ws=wws)
 
         dl = dlogits.reshape(M, 1).contiguous().float()
         # cls_head[7]  (N = 1)
@@ -444,12 +449,10 @@ class _Schedule:
         K.colsum(dl, out=G("cls_head.7.bias"), accumulate=True, ws=ws)
         dz2 = K.rowdot_bwd_dx(dl, self.P("cls_head.7.weight"), gate=S["c2"], gate_scale=sd, out_dtype=dt)
         # cls_head[4]
-        K.linear_wgrad(dz2, S["c1"], G("cls_head.4.weight"))
-        bias_grad(dz2, "cls_head.4.bias")
+        wgrad(dz2, S["c1"], "cls_head.4.weight", "cls_head.4.bias")
         dz1 = K.linear_dgrad(dz2, self.W("cls_head.4.weight"), out_dtype=dt, gate=S["c1"], gate_scale=sd)
         # cls_head[1]
-        K.linear_wgrad(dz1, S["c0"], G("cls_head.1.weight"))
-        bias_grad(dz1, "cls_head.1.bias")
+        wgrad(dz1, S["c0"], "cls_head.1.weight", "cls_head.1.bias")
         dc0 = K.linear_dgrad(dz1, self.W("cls_head.1.weight"), out_dtype=_F32)
         # cls_head[0] LayerNorm (+ any external gradient on feats)
         dres = dfeats.reshape(M, -1).contiguous().float() if dfeats is not None else None
@@ -459,8 +462,7 @@ class _Schedule:
         _, dz = K.layernorm_bwd(dfe, S["z"], S["muF"], S["rsF"], self.P("feature_map.1.weight"), y=S["feats"],
                                 dropout_p=p, seed=self.seed(1), want_f32=False, lp_dtype=dt,
                                 dgamma=G("feature_map.1.weight"), dbeta=G("feature_map.1.bias"), ws=ws)
-        K.linear_wgrad(dz, S["e"], G("feature_map.0.weight"))
-        bias_grad(dz, "feature_map.0.bias")
+        wgrad(dz, S["e"], "feature_map.0.weight", "feature_map.0.bias")
         de = K.linear_dgrad(dz, self.W("feature_map.0.weight"), out_dtype=_F32)
         # encoder_norm; emit the masked lp gradient for the last layer's dropout2
         dx, g2 = K.layernorm_bwd(de, S["xL"], S["muE"], S["rsE"], self.P("encoder_norm.weight"), lp_dtype=dt,
@@ -471,26 +473,22 @@ class _Schedule:
             pre = f"multimodal_encoder.layers.{l}."
             x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, f = S["layers"][l]
             # linear2 (+dropout2 handled by g2's mask)
-            K.linear_wgrad(g2, f, G(pre + "linear2.weight"))
-            bias_grad(g2, pre + "linear2.bias")
+            wgrad(g2, f, pre + "linear2.weight", pre + "linear2.bias")
             dzf = K.linear_dgrad(g2, self.W(pre + "linear2.weight"), out_dtype=dt, gate=f, gate_scale=sd)
             # linear1 (ReLU + dropout folded into the gate above)
-            K.linear_wgrad(dzf, h2, G(pre + "linear1.weight"))
-            bias_grad(dzf, pre + "linear1.bias")
+            wgrad(dzf, h2, pre + "linear1.weight", pre + "linear1.bias")
             dh2 = K.linear_dgrad(dzf, self.W(pre + "linear1.weight"), out_dtype=_F32)
             # norm2 + residual; masked lp gradient for dropout1
             dx1, g1 = K.layernorm_bwd(dh2, x1, mu2, rs2, self.P(pre + "norm2.weight"), dres=dx, lp_dtype=dt,
                                       lp_dropout_p=p, lp_seed=self.seed(101 + 4 * l),
                                       dgamma=G(pre + "norm2.weight"), dbeta=G(pre + "norm2.bias"), ws=ws)
             # out_proj
-            K.linear_wgrad(g1, o, G(pre + "self_attn.out_proj.weight"))
-            bias_grad(g1, pre + "self_attn.out_proj.bias")
+            wgrad(g1, o, pre + "self_attn.out_proj.weight", pre + "self_attn.out_proj.bias")
             do = K.linear_dgrad(g1, self.W(pre + "self_attn.out_proj.weight"), out_dtype=dt)
             # attention
             dqkv = K.attn_bwd(qkv, o, do, lse, self.kv, B, T, H, self.scale, p, self.seed(100 + 4 * l))
             # in_proj
-            K.linear_wgrad(dqkv, h1, G(pre + "self_attn.in_proj_weight"))
-            bias_grad(dqkv, pre + "self_attn.in_proj_bias")
+            wgrad(dqkv, h1, pre + "self_attn.in_proj_weight", pre + "self_attn.in_proj_bias")
             dh1 = K.linear_dgrad(dqkv, self.W(pre + "self_attn.in_proj_weight"), out_dtype=_F32)
             # norm1 + residual; masked lp gradient for the previous layer's dropout2
             last = l == 0
@@ -502,8 +500,7 @@ class _Schedule:
         # input LayerNorm (+PE, no grad) and input projection (weight/bias grads only)
         _, dproj = K.layernorm_bwd(dx, S["proj"], S["mu0"], S["rs0"], self.P("input_norm.weight"), want_f32=False,
                                    lp_dtype=dt, dgamma=G("input_norm.weight"), dbeta=G("input_norm.bias"), ws=ws)
-        K.linear_wgrad(dproj, S["xin"], G("input_projection.weight"))
-        bias_grad(dproj, "input_projection.bias")
+        wgrad(dproj, S["xin"], "input_projection.weight", "input_projection.bias")
         m._grads_ready(["input_projection.", "input_norm."])
         for h in m._grad_done_hooks:
             h()

@@ -50,6 +50,8 @@ _SIGNATURES = {
     "rp_cast_f32_to_bf16": (c_i, [c_vp, c_vp, c_i64, c_vp]),
     "rp_gemm": (c_i, [c_i, c_i64, c_i64, c_i64, c_vp, c_i64, c_i, c_vp, c_i64, c_i, c_vp, c_i64, c_i,
                       c_f, ctypes.POINTER(GemmEpilogue), c_vp]),
+    "rp_gemm_wgrad_workspace": (c_i64, [c_i64, c_i64, c_i64]),
+    "rp_gemm_wgrad": (c_i, [c_i, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i, c_vp, c_i64, c_vp]),
     "rp_layernorm_fwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnFwdArgs), c_vp]),
     "rp_layernorm_bwd_blocks": (c_i64, [c_i64]),
     "rp_layernorm_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnBwdArgs), c_vp]),

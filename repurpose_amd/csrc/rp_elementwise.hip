@@ -49,7 +49,7 @@ inline unsigned grid_for(int64_t n, int bs) {
 }
 
 // ---------------------------------------------------------------- colsum -------------------
-constexpr int CS_ROWS = 256;
+constexpr int CS_ROWS = 64;
 constexpr int CS_THREADS = 256;
 
 template <typename T>
@@ -58,14 +58,21 @@ __global__ void colsum_pass1(const T* __restrict__ X, int64_t rows, int64_t cols
   const int64_t c = (int64_t)blockIdx.y * CS_THREADS + threadIdx.x;
   if (c >= cols) return;
   const int64_t r0 = (int64_t)blockIdx.x * CS_ROWS;
-  int64_t r1 = r0 + CS_ROWS;
-  if (r1 > rows) r1 = rows;
-  float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) {
-    float x = rp_ld(X + r * ldx + c);
-    s += w ? w[r] * x : x;
+  const int n = (int)(rows - r0 < CS_ROWS ? rows - r0 : CS_ROWS);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int r = 0;
+  for (; r + 8 <= n; r += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float x = rp_ld(X + (r0 + r + u) * ldx + c);
+      s[u] += w ? w[r0 + r + u] * x : x;
+    }
   }
-  ws[(int64_t)blockIdx.x * cols + c] = s;
+  for (; r < n; ++r) {
+    const float x = rp_ld(X + (r0 + r) * ldx + c);
+    s[0] += w ? w[r0 + r] * x : x;
+  }
+  ws[(int64_t)blockIdx.x * cols + c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
 __global__ void colsum_pass2(const float* __restrict__ ws, int64_t nrb, int64_t cols, float* __restrict__ out,

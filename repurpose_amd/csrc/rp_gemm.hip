@@ -161,15 +161,41 @@ __device__ __forceinline__ void compute_tile(f32x4 (&acc)[4][4], const char* lds
   }
 }
 
-template <typename T, bool AK, bool BKM, typename TC>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64_t K, const T* __restrict__ A,
-                                                     int64_t lda, const T* __restrict__ B, int64_t ldb,
-                                                     TC* __restrict__ Cout, int64_t ldc, float alpha,
-                                                     EpiDev ep) {
+// accumulate the column sums of an m-major A tile straight from the staging registers
+// (bias gradient of the wgrad GEMM: db[m] = sum_k dY[k][m]); a thread always owns the same
+// 16-byte column chunk because NT is a multiple of the chunks per row
+template <typename T>
+__device__ __forceinline__ void accum_chunks(float (&b)[GemmCfg<T>::VEC], const uint4 (&r)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const T* e = reinterpret_cast<const T*>(&r[i]);
+#pragma unroll
+    for (int j = 0; j < GemmCfg<T>::VEC; ++j) b[j] += (float)e[j];
+  }
+}
+
+constexpr int CST = BN + 4;                 // fp32 LDS row stride of the staged C tile
+constexpr int CTILE_BYTES = BM * CST * 4;
+
+template <typename T, bool AK, bool BKM>
+constexpr int gemm_lds_bytes() {
   using C = GemmCfg<T>;
   constexpr int TA = AK ? C::KTILE : C::MTILE;
   constexpr int TB = BKM ? C::KTILE : C::MTILE;
-  __shared__ __attribute__((aligned(16))) char lds[2 * (TA + TB)];
+  return 2 * (TA + TB) > CTILE_BYTES ? 2 * (TA + TB) : CTILE_BYTES;
+}
+
+// MODE 0: full-K tile with the fused epilogue;  MODE 1: split-K partial tile -> fp32 slab
+// (blockIdx.y = split), optional bias column sums of A -> bias slab.
+template <typename T, bool AK, bool BKM, typename TC, int MODE>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64_t K, const T* __restrict__ A,
+                                                     int64_t lda, const T* __restrict__ B, int64_t ldb,
+                                                     TC* __restrict__ Cout, int64_t ldc, float alpha,
+                                                     EpiDev ep, int64_t kchunk, float* __restrict__ bslab) {
+  using C = GemmCfg<T>;
+  constexpr int TA = AK ? C::KTILE : C::MTILE;
+  constexpr int TB = BKM ? C::KTILE : C::MTILE;
+  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<T, AK, BKM>()];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -178,19 +204,31 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64
   const int t = rp_xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int64_t m0 = (int64_t)(t / tiles_n) * BM;
   const int64_t n0 = (int64_t)(t % tiles_n) * BN;
+  int64_t kbeg = 0, kend = K;
+  if (MODE == 1) {
+    kbeg = (int64_t)blockIdx.y * kchunk;
+    kend = kbeg + kchunk < K ? kbeg + kchunk : K;
+  }
+  const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
 
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[C::VEC];
+#pragma unroll
+  for (int j = 0; j < C::VEC; ++j) bacc[j] = 0.f;
 
   uint4 ra[4], rb[4];
-  const int nk = (int)((K + C::BK - 1) / C::BK);
-  stage_load<T, AK>(ra, A, lda, M, K, m0, 0, tid);
-  stage_load<T, BKM>(rb, B, ldb, N, K, n0, 0, tid);
-  stage_store<T, AK>(ra, lds, tid);
-  stage_store<T, BKM>(rb, lds + TA, tid);
+  const int nk = kend > kbeg ? (int)((kend - kbeg + C::BK - 1) / C::BK) : 0;
+  if (nk > 0) {
+    stage_load<T, AK>(ra, A, lda, M, kend, m0, kbeg, tid);
+    stage_load<T, BKM>(rb, B, ldb, N, kend, n0, kbeg, tid);
+    if (want_bias) accum_chunks<T>(bacc, ra);
+    stage_store<T, AK>(ra, lds, tid);
+    stage_store<T, BKM>(rb, lds + TA, tid);
+  }
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
@@ -198,8 +236,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64
     char* nxt = lds + ((kt + 1) & 1) * (TA + TB);
     const bool more = (kt + 1) < nk;
     if (more) {
-      stage_load<T, AK>(ra, A, lda, M, K, m0, (int64_t)(kt + 1) * C::BK, tid);
-      stage_load<T, BKM>(rb, B, ldb, N, K, n0, (int64_t)(kt + 1) * C::BK, tid);
+      const int64_t k1 = kbeg + (int64_t)(kt + 1) * C::BK;
+      stage_load<T, AK>(ra, A, lda, M, kend, m0, k1, tid);
+      stage_load<T, BKM>(rb, B, ldb, N, kend, n0, k1, tid);
+      if (want_bias) accum_chunks<T>(bacc, ra);
     }
     compute_tile<T, AK, BKM>(acc, cur, cur + TA, wm, wn, lane);
     if (more) {
@@ -209,59 +249,162 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64
     __syncthreads();
   }
 
-  // ---- epilogue: C-layout col = lane&15, row = (lane>>4)*4 + r ----
-  const int g = lane >> 4, cl = lane & 15;
+  // ---- epilogue: stage the 128x128 fp32 tile in LDS, then 16-byte row chunks per thread ----
+  float* cs = reinterpret_cast<float*>(lds);
+  {
+    const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t n = n0 + wn * 64 + j * 16 + cl;
-    if (n >= N) continue;
-    const float bias = ep.bias ? ep.bias[n] : 0.f;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wm * 64 + i * 16 + g * 4 + r;
-        if (m >= M) continue;
-        float v = acc[i][j][r] * alpha + bias;
-        if (ep.relu) v = fmaxf(v, 0.f);
-        if (ep.drop_thresh) {
-          uint32_t idx = (uint32_t)(m * N + n);
-          v = rp_keep(ep.drop_seed, idx, ep.drop_thresh) ? v * ep.drop_scale : 0.f;
+        for (int r = 0; r < 4; ++r)
+          cs[(wm * 64 + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
+  }
+  __syncthreads();
+  constexpr int OV = 16 / (int)sizeof(TC);
+  constexpr int CPRO = BN / OV;
+  TC* Cbase = Cout + (MODE == 1 ? (int64_t)blockIdx.y * M * ldc : 0);
+  for (int id = tid; id < BM * CPRO; id += NT) {
+    const int row = id / CPRO, cc = (id % CPRO) * OV;
+    const int64_t m = m0 + row, n = n0 + cc;
+    if (m >= M || n >= N) continue;
+    float v[OV];
+#pragma unroll
+    for (int e = 0; e < OV; e += 4) {
+      float4 q = *reinterpret_cast<const float4*>(cs + row * CST + cc + e);
+      v[e] = q.x * alpha; v[e + 1] = q.y * alpha; v[e + 2] = q.z * alpha; v[e + 3] = q.w * alpha;
+    }
+    if (MODE == 0) {
+      if (ep.bias) {
+#pragma unroll
+        for (int e = 0; e < OV; e += 4) {
+          float4 q = *reinterpret_cast<const float4*>(ep.bias + n + e);
+          v[e] += q.x; v[e + 1] += q.y; v[e + 2] += q.z; v[e + 3] += q.w;
         }
-        if (ep.gate) {
-          float gv = ep.gate_bf16 ? (float)((const bf16*)ep.gate)[m * ep.ldg + n]
-                                  : ((const float*)ep.gate)[m * ep.ldg + n];
-          v = gv > 0.f ? v * ep.gate_scale : 0.f;
-        }
-        if (ep.residual) v += ep.residual[m * ep.ldr + n];
-        TC* dst = Cout + m * ldc + n;
-        if constexpr (std::is_same<TC, float>::value) {
-          if (ep.accumulate) v += *dst;
-        }
-        rp_st(dst, v);
       }
+      if (ep.relu) {
+#pragma unroll
+        for (int e = 0; e < OV; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (ep.drop_thresh) {
+        const uint32_t base = (uint32_t)(m * N + n);
+#pragma unroll
+        for (int e = 0; e < OV; ++e) v[e] = rp_keep(ep.drop_seed, base + e, ep.drop_thresh) ? v[e] * ep.drop_scale : 0.f;
+      }
+      if (ep.gate) {
+        if (ep.gate_bf16) {
+          const bf16* gp = (const bf16*)ep.gate + m * ep.ldg + n;
+#pragma unroll
+          for (int e = 0; e < OV; ++e) v[e] = (float)gp[e] > 0.f ? v[e] * ep.gate_scale : 0.f;
+        } else {
+          const float* gp = (const float*)ep.gate + m * ep.ldg + n;
+#pragma unroll
+          for (int e = 0; e < OV; ++e) v[e] = gp[e] > 0.f ? v[e] * ep.gate_scale : 0.f;
+        }
+      }
+      if (ep.residual) {
+#pragma unroll
+        for (int e = 0; e < OV; e += 4) {
+          float4 q = *reinterpret_cast<const float4*>(ep.residual + m * ep.ldr + n + e);
+          v[e] += q.x; v[e + 1] += q.y; v[e + 2] += q.z; v[e + 3] += q.w;
+        }
+      }
+    }
+    TC* dst = Cbase + m * ldc + n;
+    if constexpr (std::is_same<TC, float>::value) {
+      if (MODE == 0 && ep.accumulate) {
+        float4 q = *reinterpret_cast<const float4*>(dst);
+        v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+      }
+      *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      uint4 o;
+      bf16* ob = reinterpret_cast<bf16*>(&o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ob[e] = (bf16)v[e];
+      *reinterpret_cast<uint4*>(dst) = o;
+    }
+  }
+  if (MODE == 1 && want_bias) {
+    __syncthreads();
+    constexpr int CPR = BM / C::VEC;  // column chunks per m-major A row
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int j = 0; j < C::VEC; ++j) red[tid * C::VEC + j] = bacc[j];
+    __syncthreads();
+    if (tid < BM && m0 + tid < M) {
+      const int c = tid / C::VEC, e = tid % C::VEC;
+      float sum = 0.f;
+      for (int j = 0; j < NT / CPR; ++j) sum += red[(c + CPR * j) * C::VEC + e];
+      bslab[(int64_t)blockIdx.y * M + m0 + tid] = sum;
     }
   }
 }
 
+// dst[i] (+)= sum_s slab[s][i]  (fixed order: deterministic)
+__global__ void splitk_reduce_kernel(const float* __restrict__ slab, int S, int64_t n, float* __restrict__ dst,
+                                     int accumulate) {
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 acc = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < S; ++s) {
+      float4 q = reinterpret_cast<const float4*>(slab + (int64_t)s * n)[i];
+      acc.x += q.x; acc.y += q.y; acc.z += q.z; acc.w += q.w;
+    }
+    reinterpret_cast<float4*>(dst)[i] = acc;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float acc = accumulate ? dst[i] : 0.f;
+    for (int s = 0; s < S; ++s) acc += slab[(int64_t)s * n + i];
+    dst[i] = acc;
+  }
+}
+
+#define RP_GEMM_LAUNCH(AKV, BKV, MODEV, GRID)                                                              \
+  hipLaunchKernelGGL((gemm_kernel<T, AKV, BKV, TC, MODEV>), GRID, dim3(NT), 0, s, M, N, K, a, lda, b, ldb, c, \
+                     ldc, alpha, ep, kchunk, bslab)
+
 template <typename T, typename TC>
 int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int ak, const void* B,
                   int64_t ldb, int bk, void* Cp, int64_t ldc, float alpha, const EpiDev& ep,
-                  hipStream_t s) {
+                  hipStream_t s, int splits = 0, int64_t kchunk = 0, float* bslab = nullptr) {
   int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  dim3 grid((unsigned)tiles), block(NT);
   const T* a = (const T*)A;
   const T* b = (const T*)B;
   TC* c = (TC*)Cp;
-  if (ak && bk)
-    hipLaunchKernelGGL((gemm_kernel<T, true, true, TC>), grid, block, 0, s, M, N, K, a, lda, b, ldb, c, ldc, alpha, ep);
-  else if (ak && !bk)
-    hipLaunchKernelGGL((gemm_kernel<T, true, false, TC>), grid, block, 0, s, M, N, K, a, lda, b, ldb, c, ldc, alpha, ep);
-  else if (!ak && !bk)
-    hipLaunchKernelGGL((gemm_kernel<T, false, false, TC>), grid, block, 0, s, M, N, K, a, lda, b, ldb, c, ldc, alpha, ep);
-  else
-    hipLaunchKernelGGL((gemm_kernel<T, false, true, TC>), grid, block, 0, s, M, N, K, a, lda, b, ldb, c, ldc, alpha, ep);
+  if (splits == 0) {
+    dim3 grid((unsigned)tiles);
+    if (ak && bk) RP_GEMM_LAUNCH(true, true, 0, grid);
+    else if (ak && !bk) RP_GEMM_LAUNCH(true, false, 0, grid);
+    else if (!ak && !bk) RP_GEMM_LAUNCH(false, false, 0, grid);
+    else RP_GEMM_LAUNCH(false, true, 0, grid);
+  } else {
+    dim3 grid((unsigned)tiles, (unsigned)splits);
+    if (ak && bk) RP_GEMM_LAUNCH(true, true, 1, grid);
+    else if (ak && !bk) RP_GEMM_LAUNCH(true, false, 1, grid);
+    else if (!ak && !bk) RP_GEMM_LAUNCH(false, false, 1, grid);
+    else RP_GEMM_LAUNCH(false, true, 1, grid);
+  }
   return rp_check_launch("rp_gemm");
+}
+
+// split count for the wgrad shape (tokens are the reduction): aim at ~2 workgroups per CU,
+// each split at least 8 K-steps long
+void wgrad_plan(int64_t M, int64_t N, int64_t K, int bk, int& splits, int64_t& kchunk) {
+  if (K <= 0) {
+    splits = 1;
+    kchunk = bk;
+    return;
+  }
+  const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int64_t sp = 512 / (tiles > 0 ? tiles : 1);
+  const int64_t maxsp = K / (8 * bk);
+  if (sp > maxsp) sp = maxsp;
+  if (sp < 1) sp = 1;
+  kchunk = ((K + sp - 1) / sp + bk - 1) / bk * bk;
+  splits = (int)((K + kchunk - 1) / kchunk);
+  if (splits < 1) splits = 1;
 }
 
 }  // namespace
@@ -283,6 +426,8 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
   RP_REQUIRE(a_kmajor ? lda >= K : lda >= M, "rp_gemm: lda too small");
   RP_REQUIRE(b_kmajor ? ldb >= K : ldb >= N, "rp_gemm: ldb too small");
   RP_REQUIRE(ldc >= N, "rp_gemm: ldc too small");
+  RP_REQUIRE(N % vec == 0, "rp_gemm: N=%lld must be a multiple of 8 (use rp_rowdot_* for N <= 4)", (long long)N);
+  RP_REQUIRE(rp_aligned16(C), "rp_gemm: C must be 16-byte aligned");
   EpiDev e{};
   e.gate_scale = 1.f;
   if (ep) {
@@ -300,6 +445,8 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
     e.accumulate = ep->accumulate;
     RP_REQUIRE(!e.accumulate || c_dtype == RP_F32, "rp_gemm: accumulate needs an fp32 C");
     RP_REQUIRE(!e.drop_thresh || M * N < (int64_t)UINT32_MAX, "rp_gemm: dropout index overflow");
+    RP_REQUIRE(!e.bias || rp_aligned16(e.bias), "rp_gemm: bias must be 16-byte aligned");
+    RP_REQUIRE(!e.residual || (rp_aligned16(e.residual) && e.ldr % 4 == 0), "rp_gemm: residual alignment");
   }
   hipStream_t s = (hipStream_t)stream;
   if (dtype == RP_BF16) {
@@ -308,4 +455,55 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
   }
   if (c_dtype == RP_BF16) return launch_gemm_t<float, bf16>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, e, s);
   return launch_gemm_t<float, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, e, s);
+}
+
+extern "C" int64_t rp_gemm_wgrad_workspace(int64_t M, int64_t N, int64_t K) {
+  int splits;
+  int64_t kchunk;
+  wgrad_plan(M, N, K, GemmCfg<bf16>::BK, splits, kchunk);
+  int s2;
+  int64_t k2;
+  wgrad_plan(M, N, K, GemmCfg<float>::BK, s2, k2);
+  if (s2 > splits) splits = s2;
+  return (int64_t)splits * (M * N + M) * 4;
+}
+
+extern "C" int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, int64_t ldy, const void* X,
+                             int64_t ldx, float* dW, float* db, int accumulate, void* workspace, int64_t ws_bytes,
+                             void* stream) {
+  RP_REQUIRE(dtype == RP_F32 || dtype == RP_BF16, "rp_gemm_wgrad: bad dtype %d", dtype);
+  RP_REQUIRE(M >= 0 && N >= 0 && K >= 0, "rp_gemm_wgrad: negative size");
+  if (M == 0 || N == 0) return RP_OK;
+  RP_REQUIRE(dW && workspace, "rp_gemm_wgrad: null output / workspace");
+  RP_REQUIRE(K == 0 || (dY && X), "rp_gemm_wgrad: null operand");
+  RP_REQUIRE(M % 8 == 0 && N % 8 == 0 && ldy % 8 == 0 && ldx % 8 == 0 && ldy >= M && ldx >= N,
+             "rp_gemm_wgrad: M, N and leading dims must be multiples of 8");
+  RP_REQUIRE(rp_aligned16(dY) && rp_aligned16(X) && rp_aligned16(dW) && rp_aligned16(workspace),
+             "rp_gemm_wgrad: 16-byte alignment required");
+  const int bk = dtype == RP_BF16 ? GemmCfg<bf16>::BK : GemmCfg<float>::BK;
+  int splits;
+  int64_t kchunk;
+  wgrad_plan(M, N, K, bk, splits, kchunk);
+  RP_REQUIRE(ws_bytes >= (int64_t)splits * (M * N + M) * 4, "rp_gemm_wgrad: workspace too small");
+  float* slab = (float*)workspace;
+  float* bslab = db ? slab + (int64_t)splits * M * N : nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  EpiDev e{};
+  e.gate_scale = 1.f;
+  int rc;
+  if (dtype == RP_BF16)
+    rc = launch_gemm_t<bf16, float>(M, N, K, dY, ldy, 0, X, ldx, 0, slab, N, 1.f, e, s, splits, kchunk, bslab);
+  else
+    rc = launch_gemm_t<float, float>(M, N, K, dY, ldy, 0, X, ldx, 0, slab, N, 1.f, e, s, splits, kchunk, bslab);
+  if (rc) return rc;
+  const int64_t n = M * N;
+  unsigned g = (unsigned)((n / 4 + 255) / 256);
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, s, slab, splits, n, dW, accumulate);
+  if (db) {
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((M / 4 + 255) / 256 + 1)), dim3(256), 0, s, bslab, splits, M,
+                       db, accumulate);
+  }
+  return rp_check_launch("rp_gemm_wgrad");
 }

@@ -14,8 +14,26 @@ template <int VPT>
 __device__ __forceinline__ void load_row(float (&v)[VPT], const void* base, int dtype, int64_t off) {
   if (dtype == RP_BF16) {
     const bf16* p = (const bf16*)base + off;
+    if constexpr (VPT % 8 == 0) {
 #pragma unroll
-    for (int i = 0; i < VPT; ++i) v[i] = (float)p[i];
+      for (int i = 0; i < VPT; i += 8) {
+        uint4 q = *reinterpret_cast<const uint4*>(p + i);
+        const bf16* e = reinterpret_cast<const bf16*>(&q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i + j] = (float)e[j];
+      }
+    } else if constexpr (VPT % 4 == 0) {
+#pragma unroll
+      for (int i = 0; i < VPT; i += 4) {
+        uint2 q = *reinterpret_cast<const uint2*>(p + i);
+        const bf16* e = reinterpret_cast<const bf16*>(&q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i + j] = (float)e[j];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) v[i] = (float)p[i];
+    }
   } else {
     const float* p = (const float*)base + off;
     if constexpr (VPT % 4 == 0) {
@@ -35,8 +53,28 @@ template <int VPT>
 __device__ __forceinline__ void store_row(const float (&v)[VPT], void* base, int dtype, int64_t off) {
   if (dtype == RP_BF16) {
     bf16* p = (bf16*)base + off;
+    if constexpr (VPT % 8 == 0) {
 #pragma unroll
-    for (int i = 0; i < VPT; ++i) p[i] = (bf16)v[i];
+      for (int i = 0; i < VPT; i += 8) {
+        uint4 q;
+        bf16* e = reinterpret_cast<bf16*>(&q);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) e[j] = (bf16)v[i + j];
+        *reinterpret_cast<uint4*>(p + i) = q;
+      }
+    } else if constexpr (VPT % 4 == 0) {
+#pragma unroll
+      for (int i = 0; i < VPT; i += 4) {
+        uint2 q;
+        bf16* e = reinterpret_cast<bf16*>(&q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = (bf16)v[i + j];
+        *reinterpret_cast<uint2*>(p + i) = q;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) p[i] = (bf16)v[i];
+    }
   } else {
     float* p = (float*)base + off;
     if constexpr (VPT % 4 == 0) {
@@ -80,11 +118,13 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_fwd_kernel(int64_t rows, LnF
   }
   const float var = rp_wave_sum(q) * (1.f / D);
   const float rstd = rsqrtf(var + a.eps);
-  float pe[VPT];
+  float pe[VPT], gm[VPT], bt[VPT];
   if (a.pe) load_row<VPT>(pe, a.pe, RP_F32, (row % a.pe_period) * D + c0);
+  load_row<VPT>(gm, a.gamma, RP_F32, c0);
+  load_row<VPT>(bt, a.beta, RP_F32, c0);
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    float y = (v[i] - mean) * rstd * a.gamma[c0 + i] + a.beta[c0 + i];
+    float y = (v[i] - mean) * rstd * gm[i] + bt[i];
     if (a.pe) y += pe[i];
     if (a.relu) y = fmaxf(y, 0.f);
     if (a.drop_thresh)
@@ -121,8 +161,7 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_bwd_kernel(int64_t rows, LnB
 #pragma unroll
   for (int i = 0; i < VPT; ++i) pg[i] = pb[i] = 0.f;
   float gam[VPT];
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) gam[i] = a.gamma[c0 + i];
+  load_row<VPT>(gam, a.gamma, RP_F32, c0);
 
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK;
   for (int rr = w; rr < LN_ROWS_PER_BLOCK; rr += LN_WAVES) {

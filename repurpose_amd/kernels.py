@@ -132,11 +132,19 @@ def linear_dgrad(dy, W, out_dtype, gate=None, gate_scale=1.0):
     return gemm(dy, W, out, M, K, Nn, Nn, True, K, False, K, gate=gate, ldg=K, gate_scale=gate_scale)
 
 
-def linear_wgrad(dy, x, dW, accumulate=True):
-    """dW (+)= dy^T x ; dy [M, N], x [M, K], dW fp32 [N, K]."""
-    M, Nn = dy.shape
+def linear_wgrad(dy, x, dW, db=None, accumulate=True, ws=None):
+    """dW (+)= dy^T x and db (+)= colsum(dy); dy [T, N], x [T, K], dW fp32 [N, K] (split-K over T)."""
+    _gpu(dy, x, dW, db)
+    T, Nn = dy.shape
     K = x.shape[1]
-    return gemm(dy, x, dW, Nn, K, M, Nn, False, K, False, K, accumulate=accumulate)
+    if dy.dtype != x.dtype:
+        raise TypeError("rp_gemm_wgrad: dy and x must share a dtype")
+    need = N.load().rp_gemm_wgrad_workspace(Nn, K, T)
+    if ws is None or ws.numel() * ws.element_size() < need:
+        ws = torch.empty(max(need // 4, 4), device=dy.device, dtype=torch.float32)
+    N.call("rp_gemm_wgrad", _dt(dy), Nn, K, T, _p(dy), dy.stride(0), _p(x), x.stride(0), _p(dW), _p(db),
+           int(accumulate), _p(ws), ws.numel() * ws.element_size(), _stream(dy))
+    return dW
 
 
 # ------------------------------------------------------------------------------------- LayerNorm

@@ -256,3 +256,24 @@ def test_adam_matches_torch(dev):
         K.adam_step(p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 1e-4, step, p_lp=plp)
     close(p, p_ref.detach(), atol=1e-6, what="adam")
     assert torch.equal(plp, p.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("T,Nn,Kd", [(16384, 512, 512), (771, 2048, 512), (100, 256, 2944), (5000, 1536, 512)])
+def test_wgrad_splitk_with_bias(dev, dtype, T, Nn, Kd):
+    dy = rnd(T, Nn, dev=dev, seed=1).to(dtype)
+    x = rnd(T, Kd, dev=dev, seed=2).to(dtype)
+    dW = torch.full((Nn, Kd), 0.25, device=dev)
+    db = torch.full((Nn,), -1.0, device=dev)
+    K.linear_wgrad(dy, x, dW, db=db, accumulate=True)
+    ref = dy.double().T @ x.double() + 0.25
+    tol = (1e-4 if dtype == torch.float32 else 1e-3) * math.sqrt(T)
+    close(dW, ref, atol=tol, what="wgrad")
+    close(db, dy.double().sum(0) - 1.0, atol=tol, what="bias grad")
+    # overwrite mode and determinism
+    dW2 = torch.empty_like(dW)
+    K.linear_wgrad(dy, x, dW2, accumulate=False)
+    dW3 = torch.empty_like(dW)
+    K.linear_wgrad(dy, x, dW3, accumulate=False)
+    assert torch.equal(dW2, dW3)
+    close(dW2, ref - 0.25, atol=tol, what="wgrad overwrite")

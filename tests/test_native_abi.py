@@ -50,6 +50,7 @@ def test_zero_sized_calls_are_noops():
 
 def test_workspace_queries():
     lib = N.load()
-    assert lib.rp_colsum_workspace(16384, 2048) == 64 * 2048
+    assert lib.rp_colsum_workspace(16384, 2048) == 256 * 2048
+    assert lib.rp_gemm_wgrad_workspace(2048, 512, 16384) >= 2048 * 512 * 4
     assert lib.rp_layernorm_bwd_blocks(16384) == 256
     assert lib.rp_layernorm_bwd_blocks(1) == 1
