@@ -166,13 +166,20 @@ int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ldx,
  * qkv: [B*T, 3*H*dk] rows = (q heads | k heads | v heads), dk == 64.
  * key_valid: [B, T] uint8 (0 -> key masked with -inf, torch key_padding_mask semantics).
  * out: [B*T, H*dk];  lse: [B, H, T] fp32 (natural-log sum-exp of scaled scores).
- * Dropout on the attention probabilities with p, hash seed (index ((b*H+h)*T+q)*T+k). */
+ * Dropout on the attention probabilities with probability p: keep(q, k) is the 16-bit half
+ * (k & 1) of rp_hash(rp_hash(seed, b*H+h), q*T + (k & ~1)) compared with round(p*65536).
+ * The forward writes the keep bits to `dropmask` (uint16 [B*H][ceil(T/64)][4][roundup(T,64)],
+ * bit (kt*4 + r) of word (bh, tile, g, q) = keep(q, 64*tile + 16*kt + 4*g + r);
+ * rp_attn_dropmask_elems() words), the backward reads them back.  dropmask may be NULL when
+ * p == 0. */
+int64_t rp_attn_dropmask_elems(int B, int T, int H);
 int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk,
-                float scale, float dropout_p, uint32_t seed, void* out, float* lse, void* stream);
+                float scale, float dropout_p, uint32_t seed, void* out, float* lse, uint16_t* dropmask,
+                void* stream);
 /* Backward; dqkv: [B*T, 3*H*dk] (fully overwritten); delta_ws: [B, H, T] fp32 workspace. */
 int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
                 const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
-                uint32_t seed, void* dqkv, float* delta_ws, void* stream);
+                const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Focal loss (alpha, gamma) on n frames.  mask may be NULL (all ones).

@@ -57,8 +57,9 @@ _SIGNATURES = {
     "rp_layernorm_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnBwdArgs), c_vp]),
     "rp_colsum_workspace": (c_i64, [c_i64, c_i64]),
     "rp_colsum": (c_i, [c_vp, c_i, c_i64, c_i64, c_i64, c_vp, c_vp, c_i, c_vp, c_vp]),
-    "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp]),
-    "rp_attn_bwd": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32,
+    "rp_attn_dropmask_elems": (c_i64, [c_i, c_i, c_i]),
+    "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp, c_vp]),
+    "rp_attn_bwd": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp,
                           c_vp, c_vp, c_vp]),
     "rp_focal_fwd_sum": (c_i, [c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_vp]),
     "rp_focal_elementwise": (c_i, [c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_vp]),

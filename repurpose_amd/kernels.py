@@ -206,27 +206,34 @@ def colsum(X, w=None, out=None, accumulate=False, ws=None):
 
 # ------------------------------------------------------------------------------------- attention
 def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0):
+    """-> (out [B*T, H*dk], lse [B, H, T], dropmask or None).  The dropout keep bits drawn by the
+    forward are returned and must be handed to attn_bwd."""
     _gpu(qkv, key_valid)
     _contig(qkv, key_valid)
     dk = qkv.shape[1] // (3 * H)
     out = torch.empty(B * T, H * dk, device=qkv.device, dtype=qkv.dtype)
     lse = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
+    mask = None
+    if dropout_p > 0:
+        mask = torch.empty(N.load().rp_attn_dropmask_elems(B, T, H), device=qkv.device, dtype=torch.int16)
     e0 = _tick("attn_fwd")
     N.call("rp_attn_fwd", _dt(qkv), _p(qkv), _p(key_valid), B, T, H, dk, float(scale), float(dropout_p),
-           int(seed) & 0xFFFFFFFF, _p(out), _p(lse), _stream(qkv))
+           int(seed) & 0xFFFFFFFF, _p(out), _p(lse), _p(mask), _stream(qkv))
     _tock(e0)
-    return out, lse
+    return out, lse, mask
 
 
-def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0):
-    _gpu(qkv, out, dout, lse, key_valid)
+def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, dropmask=None):
+    _gpu(qkv, out, dout, lse, key_valid, dropmask)
     _contig(qkv, out, dout, lse, key_valid)
+    if dropout_p > 0 and dropmask is None:
+        raise ValueError("attn_bwd: dropout needs the forward's dropmask")
     dk = qkv.shape[1] // (3 * H)
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
     e0 = _tick("attn_bwd")
     N.call("rp_attn_bwd", _dt(qkv), _p(qkv), _p(out), _p(dout), _p(lse), _p(key_valid), B, T, H, dk,
-           float(scale), float(dropout_p), int(seed) & 0xFFFFFFFF, _p(dqkv), _p(delta), _stream(qkv))
+           float(scale), float(dropout_p), _p(dropmask), _p(dqkv), _p(delta), _stream(qkv))
     _tock(e0)
     return dqkv
 

@@ -1,0 +1,85 @@
+"""Per-kernel timings at the bench shape (B=8, T=2048, d=512, H=8, dff=2048), HIP-event timed,
+interleaved rounds in one process (guide rule 24).  Prints one line per kernel: avg ms and TFLOP/s
+or GB/s.  Usage: python scripts/microbench.py [--only attn|gemm|ln] [--reps N]"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from repurpose_amd import kernels as K  # noqa: E402
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--B", type=int, default=8)
+    ap.add_argument("--T", type=int, default=2048)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    B, T, H, d, dff = a.B, a.T, 8, 512, 2048
+    M = B * T
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(0)
+    res = []
+    if a.only in ("", "attn"):
+        qkv = torch.randn(M, 3 * d, generator=g).to(dev, bf)
+        kv = torch.ones(B, T, dtype=torch.uint8, device=dev)
+        do = torch.randn(M, d, generator=g).to(dev, bf)
+        fl = 4.0 * B * H * T * T * 64
+        for p in (0.0, 0.1):
+            r = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 1)
+            o, lse = r[0], r[1]
+            extra = r[2:]
+            t = timeit(lambda: K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 1), a.reps)
+            res.append((f"attn_fwd p={p}", t, fl / t / 1e9, "TFLOP/s"))
+            t = timeit(lambda: K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, 1, *extra), a.reps)
+            res.append((f"attn_bwd p={p} (3 kernels)", t, 2 * fl / t / 1e9, "TFLOP/s alg"))
+    if a.only in ("", "gemm"):
+        for (n, k, name) in [(3 * d, d, "qkv"), (d, d, "out_proj"), (dff, d, "linear1"), (d, dff, "linear2")]:
+            x = torch.randn(M, k, generator=g).to(dev, bf)
+            w = (torch.randn(n, k, generator=g) * 0.02).to(dev, bf)
+            b = torch.zeros(n, device=dev)
+            fl = 2.0 * M * n * k
+            t = timeit(lambda: K.linear_fwd(x, w, b, out_dtype=bf), a.reps)
+            res.append((f"gemm fwd {name} {M}x{n}x{k} bf16out", t, fl / t / 1e9, "TFLOP/s"))
+            dy = torch.randn(M, n, generator=g).to(dev, bf)
+            t = timeit(lambda: K.linear_dgrad(dy, w, out_dtype=torch.float32), a.reps)
+            res.append((f"gemm dgrad {name} f32out", t, fl / t / 1e9, "TFLOP/s"))
+            dW = torch.zeros(n, k, device=dev)
+            db = torch.zeros(n, device=dev)
+            ws = torch.empty(64 << 20, device=dev)
+            t = timeit(lambda: K.linear_wgrad(dy, x, dW, db=db, ws=ws), a.reps)
+            res.append((f"gemm wgrad {name} (+bias, split-K)", t, fl / t / 1e9, "TFLOP/s"))
+    if a.only in ("", "ln"):
+        x = torch.randn(M, d, generator=g).to(dev)
+        gm = torch.ones(d, device=dev)
+        bt = torch.zeros(d, device=dev)
+        t = timeit(lambda: K.layernorm_fwd(x, gm, bt, out_f32=False, lp_dtype=bf), a.reps)
+        res.append(("ln fwd f32->bf16", t, M * d * 6 / t / 1e6, "GB/s"))
+        _, _, mu, rs = K.layernorm_fwd(x, gm, bt, out_f32=False, lp_dtype=bf)
+        dy = torch.randn(M, d, generator=g).to(dev)
+        dg = torch.zeros(d, device=dev)
+        t = timeit(lambda: K.layernorm_bwd(dy, x, mu, rs, gm, dres=dy, lp_dtype=bf, lp_dropout_p=0.1, dgamma=dg,
+                                           dbeta=dg), a.reps)
+        res.append(("ln bwd (+dres, lp out, dgamma/dbeta)", t, M * d * 18 / t / 1e6, "GB/s"))
+    for name, t, r, u in res:
+        print(f"{name:48s} {t * 1e3:9.1f} us  {r:8.1f} {u}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

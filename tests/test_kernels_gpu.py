@@ -143,6 +143,17 @@ def test_layernorm_relu_dropout(dev):
 
 
 # ----------------------------------------------------------------------------------- attention
+def attn_keep(B, H, T, p, seed, dev):
+    """torch restatement of the attention dropout bits (include/rp_api.h, rp_attn_fwd)."""
+    bh = torch.arange(B * H, device=dev, dtype=torch.int64)
+    sbh = rp_hash(seed, bh).view(B, H, 1, 1)
+    qi = torch.arange(T, device=dev, dtype=torch.int64).view(1, 1, T, 1)
+    ki = torch.arange(T, device=dev, dtype=torch.int64).view(1, 1, 1, T)
+    h = rp_hash(sbh, qi * T + (ki & ~1))
+    half = torch.where((ki & 1) == 1, h >> 16, h & 0xFFFF)
+    return half >= int(p * 65536 + 0.5)
+
+
 def attn_ref(qkv, kv, B, T, H, p=0.0, seed=0):
     dk = qkv.shape[1] // (3 * H)
     q, k, v = qkv.view(B, T, 3, H, dk).permute(2, 0, 3, 1, 4)
@@ -150,32 +161,34 @@ def attn_ref(qkv, kv, B, T, H, p=0.0, seed=0):
     s = s.masked_fill(~kv.bool().view(B, 1, 1, T), float("-inf"))
     P = torch.softmax(s, -1)
     if p > 0:
-        dev = qkv.device
-        bh = torch.arange(B * H, device=dev, dtype=torch.int64)
-        sbh = rp_hash(seed, bh).view(B, H, 1, 1)
-        qi = torch.arange(T, device=dev, dtype=torch.int64).view(1, 1, T, 1)
-        ki = torch.arange(T, device=dev, dtype=torch.int64).view(1, 1, 1, T)
-        keep = keep_mask(sbh, qi * T + ki, p)
+        keep = attn_keep(B, H, T, p, seed, qkv.device)
         P = torch.where(keep, P / (1 - p), torch.zeros_like(P))
     o = P @ v
     return o.permute(0, 2, 1, 3).reshape(B * T, H * dk)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("T,p", [(64, 0.0), (100, 0.0), (200, 0.1), (256, 0.0)])
+@pytest.mark.parametrize("T,p", [(64, 0.0), (100, 0.0), (200, 0.1), (256, 0.0), (333, 0.1)])
 def test_attention_fwd_bwd(dev, dtype, T, p):
     B, H = 2, 8
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(dtype)
     lens = torch.tensor([T, max(1, T - 37)], device=dev)
     kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
     seed = 4242
-    o, lse = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed)
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed)
     ref_in = qkv.double().requires_grad_(True)
     ref = attn_ref(ref_in, kv, B, T, H, p, seed)
     ftol = 2e-5 if dtype == torch.float32 else 2e-2
     close(o, ref.detach(), atol=ftol, rtol=ftol, what="attn fwd")
+    if p > 0:  # the stored keep bits are exactly the restated ones
+        KT, ldm = (T + 63) // 64, (T + 63) // 64 * 64
+        words = mask.view(B * H, KT, 4, ldm)[..., :T].to(torch.int64) & 0xFFFF  # [bh, tile, g, q]
+        bits = (words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1       # [bh, tile, g, q, kt*4+r]
+        bits = bits.view(B * H, KT, 4, T, 4, 4)                                  # [bh, tile, g, q, kt, r]
+        got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, T, KT * 64)[:, :, :T].bool()
+        assert torch.equal(got, attn_keep(B, H, T, p, seed, dev).view(B * H, T, T))
     do = rnd(B * T, H * 64, dev=dev, seed=T + 1).to(dtype)
-    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, seed)
+    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask)
     gref = torch.autograd.grad(ref, ref_in, do.double())[0]
     btol = 1e-4 if dtype == torch.float32 else 6e-2
     close(dqkv, gref, atol=btol, rtol=btol, what="attn bwd")
@@ -185,7 +198,7 @@ def test_attention_lse(dev):
     B, H, T = 1, 8, 96
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=3)
     kv = torch.ones(B, T, dtype=torch.uint8, device=dev)
-    _, lse = K.attn_fwd(qkv, kv, B, T, H, 0.125)
+    _, lse, _ = K.attn_fwd(qkv, kv, B, T, H, 0.125)
     q, k, _ = qkv.double().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = torch.logsumexp((q @ k.transpose(-1, -2)) * 0.125, -1)
     close(lse, ref, atol=1e-5, what="lse")

@@ -33,7 +33,7 @@ def test_argument_errors_are_reported():
         N.call("rp_gemm", 0, 8, 8, 7, ctypes.c_void_p(16), 8, 1, ctypes.c_void_p(16), 8, 1, ctypes.c_void_p(16), 8, 0,
                1.0, None, None)
     with pytest.raises(RuntimeError, match="head dim"):
-        N.call("rp_attn_fwd", 0, None, None, 1, 1, 1, 32, 1.0, 0.0, 0, None, None, None)
+        N.call("rp_attn_fwd", 0, None, None, 1, 1, 1, 32, 1.0, 0.0, 0, None, None, None, None)
     with pytest.raises(RuntimeError, match="cap must be"):
         N.call("rp_softnms", None, None, None, 1, 2000, 0.5, 0.01, None, None, None, None, None)
     with pytest.raises(RuntimeError, match="D=300 unsupported"):
