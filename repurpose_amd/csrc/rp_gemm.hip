@@ -13,6 +13,8 @@
 // Tile 128x128, 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16 tiles, register-staged double
 // buffer (one barrier per K step), XCD-aware tile order.  bf16: v_mfma_f32_16x16x32_bf16, K-step
 // 64; f32 parity mode: exact v_mfma_f32_16x16x4_f32, K-step 32.
+#include <stdlib.h>
+
 #include "rp_common.h"
 
 namespace {
@@ -185,71 +187,13 @@ constexpr int gemm_lds_bytes() {
   return 2 * (TA + TB) > CTILE_BYTES ? 2 * (TA + TB) : CTILE_BYTES;
 }
 
-// MODE 0: full-K tile with the fused epilogue;  MODE 1: split-K partial tile -> fp32 slab
-// (blockIdx.y = split), optional bias column sums of A -> bias slab.
-template <typename T, bool AK, bool BKM, typename TC, int MODE>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64_t K, const T* __restrict__ A,
-                                                     int64_t lda, const T* __restrict__ B, int64_t ldb,
-                                                     TC* __restrict__ Cout, int64_t ldc, float alpha,
-                                                     EpiDev ep, int64_t kchunk, float* __restrict__ bslab) {
-  using C = GemmCfg<T>;
-  constexpr int TA = AK ? C::KTILE : C::MTILE;
-  constexpr int TB = BKM ? C::KTILE : C::MTILE;
-  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<T, AK, BKM>()];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int tiles_n = (int)((N + BN - 1) / BN);
-  const int tiles_m = (int)((M + BM - 1) / BM);
-  const int t = rp_xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int64_t m0 = (int64_t)(t / tiles_n) * BM;
-  const int64_t n0 = (int64_t)(t % tiles_n) * BN;
-  int64_t kbeg = 0, kend = K;
-  if (MODE == 1) {
-    kbeg = (int64_t)blockIdx.y * kchunk;
-    kend = kbeg + kchunk < K ? kbeg + kchunk : K;
-  }
-  const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bacc[C::VEC];
-#pragma unroll
-  for (int j = 0; j < C::VEC; ++j) bacc[j] = 0.f;
-
-  uint4 ra[4], rb[4];
-  const int nk = kend > kbeg ? (int)((kend - kbeg + C::BK - 1) / C::BK) : 0;
-  if (nk > 0) {
-    stage_load<T, AK>(ra, A, lda, M, kend, m0, kbeg, tid);
-    stage_load<T, BKM>(rb, B, ldb, N, kend, n0, kbeg, tid);
-    if (want_bias) accum_chunks<T>(bacc, ra);
-    stage_store<T, AK>(ra, lds, tid);
-    stage_store<T, BKM>(rb, lds + TA, tid);
-  }
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = lds + (kt & 1) * (TA + TB);
-    char* nxt = lds + ((kt + 1) & 1) * (TA + TB);
-    const bool more = (kt + 1) < nk;
-    if (more) {
-      const int64_t k1 = kbeg + (int64_t)(kt + 1) * C::BK;
-      stage_load<T, AK>(ra, A, lda, M, kend, m0, k1, tid);
-      stage_load<T, BKM>(rb, B, ldb, N, kend, n0, k1, tid);
-      if (want_bias) accum_chunks<T>(bacc, ra);
-    }
-    compute_tile<T, AK, BKM>(acc, cur, cur + TA, wm, wn, lane);
-    if (more) {
-      stage_store<T, AK>(ra, nxt, tid);
-      stage_store<T, BKM>(rb, nxt + TA, tid);
-    }
-    __syncthreads();
-  }
-
-  // ---- epilogue: stage the 128x128 fp32 tile in LDS, then 16-byte row chunks per thread ----
+// ---- shared epilogue: stage the 128x128 fp32 tile in LDS, then 16-byte row chunks per thread ----
+// MODE 0 applies the fused epilogue (bias, relu, dropout, gate, residual, accumulate) and converts;
+// MODE 1 stores the raw fp32 partial tile into split blockIdx.y's slab.
+template <typename TC, int MODE>
+__device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* lds, int tid, int lane, int wm, int wn,
+                                              int64_t m0, int64_t n0, int64_t M, int64_t N, TC* __restrict__ Cout,
+                                              int64_t ldc, float alpha, const EpiDev& ep) {
   float* cs = reinterpret_cast<float*>(lds);
   {
     const int g = lane >> 4, cl = lane & 15;
@@ -326,20 +270,230 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64
       *reinterpret_cast<uint4*>(dst) = o;
     }
   }
-  if (MODE == 1 && want_bias) {
-    __syncthreads();
-    constexpr int CPR = BM / C::VEC;  // column chunks per m-major A row
-    float* red = reinterpret_cast<float*>(lds);
+}
+
+// bias-gradient partials: thread t holds VEC column sums of column chunk t % (BM/VEC); reduce the
+// threads sharing a chunk through LDS and write this split's partial row
+template <int VEC>
+__device__ __forceinline__ void bias_reduce(const float (&bacc)[VEC], char* lds, int tid, int64_t m0, int64_t M,
+                                            float* __restrict__ bslab) {
+  __syncthreads();
+  constexpr int CPR = BM / VEC;
+  float* red = reinterpret_cast<float*>(lds);
 #pragma unroll
-    for (int j = 0; j < C::VEC; ++j) red[tid * C::VEC + j] = bacc[j];
-    __syncthreads();
-    if (tid < BM && m0 + tid < M) {
-      const int c = tid / C::VEC, e = tid % C::VEC;
-      float sum = 0.f;
-      for (int j = 0; j < NT / CPR; ++j) sum += red[(c + CPR * j) * C::VEC + e];
-      bslab[(int64_t)blockIdx.y * M + m0 + tid] = sum;
-    }
+  for (int j = 0; j < VEC; ++j) red[tid * VEC + j] = bacc[j];
+  __syncthreads();
+  if (tid < BM && m0 + tid < M) {
+    const int c = tid / VEC, e = tid % VEC;
+    float sum = 0.f;
+    for (int j = 0; j < NT / CPR; ++j) sum += red[(c + CPR * j) * VEC + e];
+    bslab[(int64_t)blockIdx.y * M + m0 + tid] = sum;
   }
+}
+
+// MODE 0: full-K tile with the fused epilogue;  MODE 1: split-K partial tile -> fp32 slab
+// (blockIdx.y = split), optional bias column sums of A -> bias slab.
+template <typename T, bool AK, bool BKM, typename TC, int MODE>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64_t K, const T* __restrict__ A,
+                                                     int64_t lda, const T* __restrict__ B, int64_t ldb,
+                                                     TC* __restrict__ Cout, int64_t ldc, float alpha,
+                                                     EpiDev ep, int64_t kchunk, float* __restrict__ bslab) {
+  using C = GemmCfg<T>;
+  constexpr int TA = AK ? C::KTILE : C::MTILE;
+  constexpr int TB = BKM ? C::KTILE : C::MTILE;
+  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<T, AK, BKM>()];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (int)((N + BN - 1) / BN);
+  const int tiles_m = (int)((M + BM - 1) / BM);
+  const int t = rp_xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int64_t m0 = (int64_t)(t / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(t % tiles_n) * BN;
+  int64_t kbeg = 0, kend = K;
+  if (MODE == 1) {
+    kbeg = (int64_t)blockIdx.y * kchunk;
+    kend = kbeg + kchunk < K ? kbeg + kchunk : K;
+  }
+  const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[C::VEC];
+#pragma unroll
+  for (int j = 0; j < C::VEC; ++j) bacc[j] = 0.f;
+
+  uint4 ra[4], rb[4];
+  const int nk = kend > kbeg ? (int)((kend - kbeg + C::BK - 1) / C::BK) : 0;
+  if (nk > 0) {
+    stage_load<T, AK>(ra, A, lda, M, kend, m0, kbeg, tid);
+    stage_load<T, BKM>(rb, B, ldb, N, kend, n0, kbeg, tid);
+    if (want_bias) accum_chunks<T>(bacc, ra);
+    stage_store<T, AK>(ra, lds, tid);
+    stage_store<T, BKM>(rb, lds + TA, tid);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = lds + (kt & 1) * (TA + TB);
+    char* nxt = lds + ((kt + 1) & 1) * (TA + TB);
+    const bool more = (kt + 1) < nk;
+    if (more) {
+      const int64_t k1 = kbeg + (int64_t)(kt + 1) * C::BK;
+      stage_load<T, AK>(ra, A, lda, M, kend, m0, k1, tid);
+      stage_load<T, BKM>(rb, B, ldb, N, kend, n0, k1, tid);
+      if (want_bias) accum_chunks<T>(bacc, ra);
+    }
+    compute_tile<T, AK, BKM>(acc, cur, cur + TA, wm, wn, lane);
+    if (more) {
+      stage_store<T, AK>(ra, nxt, tid);
+      stage_store<T, BKM>(rb, nxt + TA, tid);
+    }
+    __syncthreads();
+  }
+
+  gemm_epilogue<TC, MODE>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep);
+  if (MODE == 1 && want_bias) bias_reduce<C::VEC>(bacc, lds, tid, m0, M, bslab);
+}
+
+// ============================ bf16 fast path: LDS-DMA staged main loop ============================
+// global_load_lds_dwordx4 writes each wave-instruction's 64 x 16 B lane-linearly into LDS, so the
+// LDS images are unpadded and the bank-conflict XOR swizzle goes on the per-lane SOURCE address
+// (guide §5.4 rule 21); the fragment reads apply the same involution:
+//   k-major tile [128 rows][64 k] (128-B rows): 16-B chunk c of row r lives at chunk c ^ ((r>>1)&7)
+//     -> every ds_read_b128 lane group of the 16x16x32 A/B fragment read hits 16 distinct slots;
+//   m-major tile [64 k][128 cols] (256-B rows): chunk c of row k lives at c ^ 2*s(k),
+//     s(k) = (k&3) | ((k>>3)&1)<<2 -> the 8 rows of a ds_read_b64_tr_b16 half-wave read hit
+//     8 distinct 32-B slots.
+// Two LDS stages (2 x 32 KiB), one barrier per 64-deep K step; rows past M/N are clamped to the last
+// valid row (their outputs are discarded), so the path requires full 64-deep K steps.
+constexpr int GT = 16384;  // bytes of one operand tile (one stage)
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ int kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
+__device__ __forceinline__ int mswz(int k, int c) { return c ^ (2 * ((k & 3) | (((k >> 3) & 1) << 2))); }
+
+template <bool KMAJ>
+__device__ __forceinline__ void glds_tile(const bf16* __restrict__ base, int64_t ld, int64_t rows_lim, int64_t row0,
+                                          int64_t k0, char* tile, int wid, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int I = wid * 4 + j;  // wave-instruction index (1 KiB of the 16 KiB tile)
+    const bf16* src;
+    if (KMAJ) {
+      const int r = I * 8 + (lane >> 3);
+      const int lc = kswz(r, lane & 7);
+      int64_t rr = row0 + r;
+      if (rr >= rows_lim) rr = rows_lim - 1;
+      src = base + rr * ld + k0 + lc * 8;
+    } else {
+      const int k = I * 4 + (lane >> 4);
+      const int lc = mswz(k, lane & 15);
+      int64_t cc = row0 + lc * 8;
+      if (cc >= rows_lim) cc = rows_lim - 8;
+      src = base + (k0 + k) * ld + cc;
+    }
+    __builtin_amdgcn_global_load_lds(src, (lds_void*)(tile + I * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 frag_k_swz(const char* t, int rbase, int kbase, int lane) {
+  const int r = rbase + (lane & 15);
+  const int lc = (kbase >> 3) + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(t + r * 128 + kswz(r, lc) * 16);
+}
+
+__device__ __forceinline__ bf16x8 frag_m_swz(const char* t, int rbase, int kbase, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int k0 = kbase + 8 * g + q, k1 = k0 + 4;
+  const int lc = (rbase >> 3) + (p >> 1);
+  const char* p0 = t + k0 * 256 + mswz(k0, lc) * 16 + (p & 1) * 8;
+  const char* p1 = t + k1 * 256 + mswz(k1, lc) * 16 + (p & 1) * 8;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+template <bool AK, bool BKM, typename TC, int MODE>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t N, int64_t K,
+                                                              const bf16* __restrict__ A, int64_t lda,
+                                                              const bf16* __restrict__ B, int64_t ldb,
+                                                              TC* __restrict__ Cout, int64_t ldc, float alpha,
+                                                              EpiDev ep, int64_t kchunk, float* __restrict__ bslab) {
+  constexpr int LDS = 4 * GT > CTILE_BYTES ? 4 * GT : CTILE_BYTES;
+  __shared__ __attribute__((aligned(16))) char lds[LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (int)((N + BN - 1) / BN);
+  const int tiles_m = (int)((M + BM - 1) / BM);
+  const int t = rp_xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int64_t m0 = (int64_t)(t / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(t % tiles_n) * BN;
+  int64_t kbeg = 0, kend = K;
+  if (MODE == 1) {
+    kbeg = (int64_t)blockIdx.y * kchunk;
+    kend = kbeg + kchunk < K ? kbeg + kchunk : K;
+  }
+  const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+
+  const int nk = kend > kbeg ? (int)((kend - kbeg) / 64) : 0;
+  if (nk > 0) {
+    glds_tile<AK>(A, lda, M, m0, kbeg, lds, wid, lane);
+    glds_tile<BKM>(B, ldb, N, n0, kbeg, lds + GT, wid, lane);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = lds + (kt & 1) * 2 * GT;
+    char* nxt = lds + ((kt + 1) & 1) * 2 * GT;
+    if (kt + 1 < nk) {
+      const int64_t k1 = kbeg + (int64_t)(kt + 1) * 64;
+      glds_tile<AK>(A, lda, M, m0, k1, nxt, wid, lane);
+      glds_tile<BKM>(B, ldb, N, n0, k1, nxt + GT, wid, lane);
+    }
+    if (want_bias) {  // column sums of the staged dY tile (bias gradient), 4 x 16 B per thread
+      const int cg = tid & 15;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = (tid >> 4) + 16 * j;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(cur + k * 256 + mswz(k, cg) * 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bacc[e] += (float)v[e];
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 64; ks += 32) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = AK ? frag_k_swz(cur, wm * 64 + i * 16, ks, lane) : frag_m_swz(cur, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = BKM ? frag_k_swz(cur + GT, wn * 64 + j * 16, ks, lane) : frag_m_swz(cur + GT, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  gemm_epilogue<TC, MODE>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep);
+  if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab);
 }
 
 // dst[i] (+)= sum_s slab[s][i]  (fixed order: deterministic)
@@ -365,6 +519,15 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, int S, int6
   hipLaunchKernelGGL((gemm_kernel<T, AKV, BKV, TC, MODEV>), GRID, dim3(NT), 0, s, M, N, K, a, lda, b, ldb, c, \
                      ldc, alpha, ep, kchunk, bslab)
 
+static bool rp_dma_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_GEMM_DMA");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
+
 template <typename T, typename TC>
 int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int ak, const void* B,
                   int64_t ldb, int bk, void* Cp, int64_t ldc, float alpha, const EpiDev& ep,
@@ -373,6 +536,31 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
   const T* a = (const T*)A;
   const T* b = (const T*)B;
   TC* c = (TC*)Cp;
+  if constexpr (std::is_same<T, bf16>::value) {
+    const bool full_k = K % 64 == 0 && (splits == 0 || kchunk % 64 == 0);
+    if (full_k && rp_dma_enabled()) {
+      const bf16* ab = (const bf16*)A;
+      const bf16* bb = (const bf16*)B;
+#define RP_DMA_LAUNCH(AKV, BKV, MODEV, GRID)                                                                       \
+  hipLaunchKernelGGL((gemm_bf16_dma_kernel<AKV, BKV, TC, MODEV>), GRID, dim3(NT), 0, s, M, N, K, ab, lda, bb, ldb, c, \
+                     ldc, alpha, ep, kchunk, bslab)
+      if (splits == 0) {
+        dim3 grid((unsigned)tiles);
+        if (ak && bk) RP_DMA_LAUNCH(true, true, 0, grid);
+        else if (ak && !bk) RP_DMA_LAUNCH(true, false, 0, grid);
+        else if (!ak && !bk) RP_DMA_LAUNCH(false, false, 0, grid);
+        else RP_DMA_LAUNCH(false, true, 0, grid);
+      } else {
+        dim3 grid((unsigned)tiles, (unsigned)splits);
+        if (ak && bk) RP_DMA_LAUNCH(true, true, 1, grid);
+        else if (ak && !bk) RP_DMA_LAUNCH(true, false, 1, grid);
+        else if (!ak && !bk) RP_DMA_LAUNCH(false, false, 1, grid);
+        else RP_DMA_LAUNCH(false, true, 1, grid);
+      }
+#undef RP_DMA_LAUNCH
+      return rp_check_launch("rp_gemm");
+    }
+  }
   if (splits == 0) {
     dim3 grid((unsigned)tiles);
     if (ak && bk) RP_GEMM_LAUNCH(true, true, 0, grid);

@@ -43,7 +43,7 @@ def close(a, b, atol, rtol=0.0, what=""):
 
 # ----------------------------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,N,Kd", [(256, 128, 64), (300, 136, 200), (17, 520, 2944), (1000, 1536, 512)])
+@pytest.mark.parametrize("M,N,Kd", [(256, 128, 64), (300, 136, 200), (17, 520, 2944), (1000, 1536, 512), (333, 200, 128)])
 def test_gemm_three_layouts(dev, dtype, M, N, Kd):
     x = rnd(M, Kd, dev=dev, seed=1).to(dtype)
     w = rnd(N, Kd, dev=dev, seed=2, scale=0.05).to(dtype)
@@ -272,7 +272,8 @@ def test_adam_matches_torch(dev):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("T,Nn,Kd", [(16384, 512, 512), (771, 2048, 512), (100, 256, 2944), (5000, 1536, 512)])
+@pytest.mark.parametrize("T,Nn,Kd", [(16384, 512, 512), (771, 2048, 512), (100, 256, 2944), (5000, 1536, 512),
+                                        (4096, 200, 136), (1024, 2048, 512)])
 def test_wgrad_splitk_with_bias(dev, dtype, T, Nn, Kd):
     dy = rnd(T, Nn, dev=dev, seed=1).to(dtype)
     x = rnd(T, Kd, dev=dev, seed=2).to(dtype)
