@@ -7,11 +7,15 @@ OBJ := $(patsubst $(CSRC)/%.hip,build/%.o,$(SRC))
 LIB := repurpose_amd/_native/librepurpose_amd.so
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Wall -Wno-unused-variable
 
+# attention: no NaN semantics needed (scores are finite or -inf), drops the canonicalising
+# v_max before every fmaxf of an MFMA result
+build/rp_attention.o: EXTRA := -fno-honor-nans
+
 all: $(LIB)
 
 build/%.o: $(CSRC)/%.hip $(CSRC)/rp_common.h include/rp_api.h
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(EXTRA) -c $< -o $@
 
 $(LIB): $(OBJ)
 	@mkdir -p $(dir $(LIB))

@@ -32,12 +32,27 @@ constexpr int HD = 64;   // head dim (dk) — the Repurpose config (512 / 8 head
 constexpr int NW = 4;    // waves per workgroup
 constexpr int NT = NW * 64;
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float RESCALE_LOG2 = 8.f;  // forward: deferred-rescale threshold (log2 units)
 
 template <typename T>
 struct AttnCfg {
-  static constexpr int ROWB = HD * (int)sizeof(T) + 16;  // padded LDS row (bytes)
-  static constexpr int CPR = HD * (int)sizeof(T) / 16;   // 16-byte chunks per row
+  // bf16 tiles: 128-byte rows, XOR-swizzled (see lds_off); fp32 parity tiles: 16-byte row padding
+  static constexpr int ROWB = std::is_same<T, bf16>::value ? HD * 2 : HD * 4 + 16;
+  static constexpr int CPR = HD * (int)sizeof(T) / 16;  // 16-byte chunks per row
 };
+
+// Byte offset of (row, byte-in-row) in an LDS tile.  bf16: the 32-byte pair of 16-byte chunks is
+// XORed with (row >> 1) & 3, which makes both access patterns conflict-free: ds_read_b128 row
+// fragments (16 lanes = 16 rows x 2 adjacent chunks cover all 16 bank quads) and
+// ds_read_b64_tr_b16 column fragments (8 consecutive rows x one 32-byte pair cover all 8 bank
+// octets).  The pair index (bits 5-6) changes, the chunk parity (bit 4) and byte (bits 0-3) stay.
+template <typename T>
+__device__ __forceinline__ int lds_off(int row, int byte) {
+  if constexpr (std::is_same<T, bf16>::value)
+    return row * 128 + (byte ^ (((row >> 1) & 3) << 5));
+  else
+    return row * AttnCfg<T>::ROWB + byte;
+}
 
 // keep-bit mask layout (the forward's register layout, so the forward and dQ kernels move one
 // 16-bit word per lane and key tile): [B*H][KT = ceil(T/64)][4 lane groups g][ldm = roundup(T,64)]
@@ -51,6 +66,15 @@ struct Stage {
   static constexpr int PER = ROWS * AttnCfg<T>::CPR / NT;
   uint4 r[PER];
   __device__ __forceinline__ void load(const T* __restrict__ base, int64_t ld, int row0, int nrows, int tid) {
+    if (row0 + ROWS <= nrows) {  // whole tile in range (uniform): no per-row predication
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int id = tid + NT * i;
+        const int row = id / AttnCfg<T>::CPR, c = id % AttnCfg<T>::CPR;
+        r[i] = *reinterpret_cast<const uint4*>(base + (int64_t)(row0 + row) * ld + c * (16 / (int)sizeof(T)));
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int id = tid + NT * i;
@@ -66,7 +90,7 @@ struct Stage {
     for (int i = 0; i < PER; ++i) {
       int id = tid + NT * i;
       int row = id / AttnCfg<T>::CPR, c = id % AttnCfg<T>::CPR;
-      *reinterpret_cast<uint4*>(lds + row * AttnCfg<T>::ROWB + c * 16) = r[i];
+      *reinterpret_cast<uint4*>(lds + lds_off<T>(row, c * 16)) = r[i];
     }
   }
 };
@@ -74,7 +98,7 @@ struct Stage {
 // ----- fragment helpers -------------------------------------------------------------------------
 // bf16 row fragment: lane holds X[r0 + (l&15)][k0 + 8*(l>>4) + j]   (MFMA 16x16x32 A/B operand)
 __device__ __forceinline__ bf16x8 row_frag_lds(const char* lds, int r0, int k0, int lane) {
-  return *reinterpret_cast<const bf16x8*>(lds + (r0 + (lane & 15)) * AttnCfg<bf16>::ROWB + (k0 + 8 * (lane >> 4)) * 2);
+  return *reinterpret_cast<const bf16x8*>(lds + lds_off<bf16>(r0 + (lane & 15), (k0 + 8 * (lane >> 4)) * 2));
 }
 __device__ __forceinline__ bf16x8 row_frag_gmem(const bf16* base, int64_t ld, int r0, int nrows, int k0, int lane) {
   int r = r0 + (lane & 15);
@@ -91,8 +115,8 @@ __device__ __forceinline__ bf16x8 row_frag_gmem(const bf16* base, int64_t ld, in
 // i.e. the k-slot order (g, j) <-> row R + (j<4 ? 4g+j : 16+4g+j-4) used by the accumulators.
 __device__ __forceinline__ bf16x8 col_frag_lds(const char* lds, int R, int c0, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const char* p0 = lds + (R + 4 * g + q) * AttnCfg<bf16>::ROWB + (c0 + 4 * p) * 2;
-  const char* p1 = p0 + 16 * AttnCfg<bf16>::ROWB;
+  const char* p0 = lds + lds_off<bf16>(R + 4 * g + q, (c0 + 4 * p) * 2);  // R % 16 == 0
+  const char* p1 = p0 + 16 * AttnCfg<bf16>::ROWB;                          // same swizzle 16 rows on
   bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
   bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p1);
   bf16x8 r;
@@ -120,14 +144,49 @@ __device__ __forceinline__ float ldsf(const char* lds, int r, int c) {
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// keep bits of 4 consecutive keys kb..kb+3 (kb even) of query q: one hash per key pair
-// (element (q, k): 16-bit half (k & 1) of rp_hash(seed_bh, q*T + (k & ~1)))
-__device__ __forceinline__ uint32_t keep_nibble(uint32_t seed_bh, uint32_t q, uint32_t T_, uint32_t kb,
-                                                uint32_t thr) {
-  const uint32_t h0 = rp_hash(seed_bh, q * T_ + kb);
-  const uint32_t h1 = rp_hash(seed_bh, q * T_ + kb + 2);
-  return ((h0 & 0xFFFFu) >= thr ? 1u : 0u) | ((h0 >> 16) >= thr ? 2u : 0u) | ((h1 & 0xFFFFu) >= thr ? 4u : 0u) |
-         ((h1 >> 16) >= thr ? 8u : 0u);
+// max / sum over the 4 lanes l, l^16, l^32, l^48 (one query of an S^T accumulator) with the gfx950
+// row-swap permutes (VALU, no LDS round trip like ds_bpermute)
+__device__ __forceinline__ float quad_max(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float quad_sum(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// Attention dropout stream (include/rp_api.h, rp_attn_fwd): for query q, key tile `tile` and lane
+// group g (keys 64*tile + 16*kt + 4*g + r, kt, r in 0..3) the state st = rp_hash(seed_bh,
+// (q*KT + tile)*4 + g) is advanced by xorshift32 eight times; word j covers keys
+// (kt = j>>1, r = 2*(j&1) + {0: low half, 1: high half}); a key is kept iff its half, read as a signed
+// 16-bit integer, is >= round(p*65536) - 32768 (probability 1 - p, exact to 2^-16).
+// Outputs dm[j] (0xFFFF in each dropped half: the AND-NOT mask of the packed bf16 P pair) and
+// returns the 16 keep bits, bit (kt*4 + r).  Full-rate VALU only: a saturating packed 16-bit
+// subtract + arithmetic shift per pair, no 32-bit multiplies beyond the one seeding hash.
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t drop_masks(uint32_t seed_bh, uint32_t q, uint32_t KT, uint32_t tile, uint32_t g,
+                                               uint32_t thr, uint32_t dm[8]) {
+  uint32_t st = rp_hash(seed_bh, (q * KT + tile) * 4u + g);
+  const short ts = (short)((int)thr - 32768);
+  const i16x2 t2 = {ts, ts};
+  uint32_t acc = 0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    st ^= st << 13;
+    st ^= st >> 17;
+    st ^= st << 5;
+    const i16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, st), t2);  // < 0 <=> dropped
+    const uint32_t m = __builtin_bit_cast(uint32_t, (i16x2)(d >> (short)15));
+    dm[j] = m;
+    // keep bit of the low half -> bit 4*(j>>1) + 2*(j&1); high half -> 16 + that + 1 (folded below)
+    const int b = 4 * (j >> 1) + 2 * (j & 1);
+    acc |= ~m & ((1u << b) | (1u << (16 + b + 1)));
+  }
+  return (acc & 0xFFFFu) | (acc >> 16);
 }
 
 // =================================================================================================
@@ -136,8 +195,8 @@ __device__ __forceinline__ uint32_t keep_nibble(uint32_t seed_bh, uint32_t q, ui
 constexpr int FW_QB = NW * 32;  // queries per workgroup
 constexpr int FW_KT = 64;       // keys per tile
 
-template <typename T>
-__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const T* __restrict__ qkv, const uint8_t* __restrict__ kvalid,
+template <typename T, bool DROP>
+__global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2) void attn_fwd_kernel(const T* __restrict__ qkv, const uint8_t* __restrict__ kvalid,
                                                         int B, int T_, int H, float scale, uint32_t drop_thresh,
                                                         float drop_scale, uint32_t seed, T* __restrict__ out,
                                                         float* __restrict__ lse, uint16_t* __restrict__ dmask) {
@@ -159,6 +218,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const T* __restrict__ q
   const int q0 = qb * FW_QB + w * 32;  // this wave's first query
   const uint32_t seed_bh = rp_hash(seed, (uint32_t)bh);
   const float c = scale * LOG2E;
+  const float rth = RESCALE_LOG2 / c;  // deferred-rescale threshold in score units
   const int KT = mask_kt(T_);
   const int64_t ldm = mask_ld(T_);
   uint16_t* mrow = dmask ? dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
@@ -190,21 +250,26 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const T* __restrict__ q
 
   Stage<T, FW_KT> sk, sv;
   const int nkt = (T_ + FW_KT - 1) / FW_KT;
-  auto stage_mask = [&](char* buf, int k0) {
+  // key-valid flags of a tile: loaded with the K/V prefetch (wave 0, one byte per lane), staged as
+  // an additive bias + a "no masked key" flag at the LDS write
+  auto load_valid = [&](int k0) -> bool {
+    const int k = k0 + lane;
+    return w == 0 && k < T_ && kvalid[(int64_t)b * T_ + k];
+  };
+  auto stage_mask = [&](char* buf, bool ok) {
     float* kb = reinterpret_cast<float*>(buf + 2 * TILE);
-    if (tid < FW_KT) {  // exactly wave 0
-      const int k = k0 + tid;
-      const bool ok = k < T_ && kvalid[(int64_t)b * T_ + k];
-      kb[tid] = ok ? 0.f : -INFINITY;
+    if (w == 0) {
+      kb[lane] = ok ? 0.f : -INFINITY;
       const unsigned long long bal = __ballot(ok);
-      if (tid == 0) *reinterpret_cast<int*>(buf + 2 * TILE + FW_KT * 4) = bal == ~0ull;
+      if (lane == 0) *reinterpret_cast<int*>(buf + 2 * TILE + FW_KT * 4) = bal == ~0ull;
     }
   };
   sk.load(Kg, ld, 0, T_, tid);
   sv.load(Vg, ld, 0, T_, tid);
+  bool kvn = load_valid(0);
   sk.store(lds, tid);
   sv.store(lds + TILE, tid);
-  stage_mask(lds, 0);
+  stage_mask(lds, kvn);
   __syncthreads();
 
   for (int kt_i = 0; kt_i < nkt; ++kt_i) {
@@ -215,6 +280,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const T* __restrict__ q
     if (more) {
       sk.load(Kg, ld, k0 + FW_KT, T_, tid);
       sv.load(Vg, ld, k0 + FW_KT, T_, tid);
+      kvn = load_valid(k0 + FW_KT);
     }
     const char* Kl = cur;
     const char* Vl = cur + TILE;
@@ -247,6 +313,9 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const T* __restrict__ q
         }
     }
     // ---- mask (only tiles with masked keys) + column max ----
+    // Deferred rescale: the running reference m only moves when the tile max exceeds it by more
+    // than RESCALE_LOG2 (P <= 2^8 meanwhile, exact in fp32/bf16 range); l and O share the
+    // reference, so out = O / l is unchanged and the lse uses the same m.
     float mnew[2];
     bool grow = false;
 #pragma unroll
@@ -257,66 +326,84 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const T* __restrict__ q
 #pragma unroll
           for (int r = 0; r < 4; ++r) s[kt][qt][r] += kbias[kt * 16 + 4 * g + r];
       }
-      float mx = s[0][qt][0];
+      float mx = s[0][qt][0];  // chain -> v_max3
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][qt][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      mnew[qt] = fmaxf(m[qt], mx);
-      grow |= mnew[qt] > m[qt];
+      mx = quad_max(mx);
+      mnew[qt] = mx;
+      grow |= mx > m[qt] + rth;  // no NaN anywhere: m = -inf -> grows iff mx finite
     }
-    if (__any(grow)) {  // rescale only when some row max grew (wave-uniform branch)
+    if (__any(grow)) {  // wave-uniform branch, per-lane update
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        const float mref = mnew[qt] == -INFINITY ? 0.f : mnew[qt];
-        const float alpha = exp2f((m[qt] - mref) * c);  // m = -inf -> 0
+        const bool gq = mnew[qt] > m[qt] + rth;
+        const float alpha = gq ? rp_exp2((m[qt] - mnew[qt]) * c) : 1.f;  // m = -inf -> 0
         lp[qt] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
-        m[qt] = mnew[qt];
+        m[qt] = gq ? mnew[qt] : m[qt];
       }
     }
-    // ---- P = exp2(S*c - m*c); per-lane partial row sums; dropout bits ----
+    // ---- P = exp2(S*c - m*c); per-lane partial row sums (before dropout), tree order ----
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const float mc = (m[qt] == -INFINITY ? 0.f : m[qt]) * c;
-      const int q = q0 + qt * 16 + i;
-      uint32_t word = 0;
+      float t4[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(fmaf(s[kt][qt][r], c, -mc));
-          lp[qt] += p;
-          s[kt][qt][r] = p;
-        }
-        if (drop_thresh) {
-          const uint32_t nib =
-              keep_nibble(seed_bh, (uint32_t)q, (uint32_t)T_, (uint32_t)(k0 + kt * 16 + 4 * g), drop_thresh);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s[kt][qt][r] = ((nib >> r) & 1u) ? s[kt][qt][r] : 0.f;
-          word |= nib << (4 * kt);
-        }
+        for (int r = 0; r < 4; ++r) s[kt][qt][r] = rp_exp2(fmaf(s[kt][qt][r], c, -mc));
+        t4[kt] = (s[kt][qt][0] + s[kt][qt][1]) + (s[kt][qt][2] + s[kt][qt][3]);
       }
-      if (drop_thresh && q < T_) mrow[((int64_t)kt_i * 4 + g) * ldm + q] = (uint16_t)word;
+      lp[qt] += (t4[0] + t4[1]) + (t4[2] + t4[3]);
+    }
+    // ---- dropout: 8 drop masks per (query, tile) from one xorshift stream; keep bits stored ----
+    uint32_t dm[2][8];
+    if constexpr (DROP) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int q = q0 + qt * 16 + i;
+        const uint32_t word = drop_masks(seed_bh, (uint32_t)q, (uint32_t)KT, (uint32_t)kt_i, (uint32_t)g, drop_thresh, dm[qt]);
+        if (q < T_) mrow[((int64_t)kt_i * 4 + g) * ldm + q] = (uint16_t)word;
+      }
     }
     // ---- O^T[dk][q] += V^T P^T ----
     if constexpr (BF) {
+      bf16x8 pf[2][2];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 pf[2];
+      for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) pf[qt] = pack8(s[2 * ks][qt], s[2 * ks + 1][qt]);
+        for (int ks = 0; ks < 2; ++ks) {
+          pf[qt][ks] = pack8(s[2 * ks][qt], s[2 * ks + 1][qt]);
+          if constexpr (DROP) {
+            uint4 u = __builtin_bit_cast(uint4, pf[qt][ks]);
+            u.x &= ~dm[qt][4 * ks + 0];
+            u.y &= ~dm[qt][4 * ks + 1];
+            u.z &= ~dm[qt][4 * ks + 2];
+            u.w &= ~dm[qt][4 * ks + 3];
+            pf[qt][ks] = __builtin_bit_cast(bf16x8, u);
+          }
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
           bf16x8 vf = col_frag_lds(Vl, ks * 32, dt * 16, lane);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) o[qt][dt] = mfma_bf16(vf, pf[qt], o[qt][dt]);
+          for (int qt = 0; qt < 2; ++qt) o[qt][dt] = mfma_bf16(vf, pf[qt][ks], o[qt][dt]);
         }
-      }
     } else {
+      if constexpr (DROP) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              s[kt][qt][r] = ((dm[qt][2 * kt + (r >> 1)] >> (16 * (r & 1))) & 1u) ? 0.f : s[kt][qt][r];
+      }
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -331,7 +418,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const T* __restrict__ q
     if (more) {
       sk.store(nxt, tid);
       sv.store(nxt + TILE, tid);
-      stage_mask(nxt, k0 + FW_KT);
+      stage_mask(nxt, kvn);
     }
     __syncthreads();
   }
@@ -340,9 +427,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const T* __restrict__ q
   const int64_t ldo = (int64_t)H * HD;
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    float l = lp[qt];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    const float l = quad_sum(lp[qt]);
     const int q = q0 + qt * 16 + i;
     if (q >= T_) continue;
     const float inv = drop_scale / l;
@@ -386,7 +471,7 @@ __global__ void attn_delta_kernel(const T* __restrict__ out, const T* __restrict
 constexpr int KV_KB = NW * 32;
 constexpr int KV_QT = 64;
 
-template <typename T>
+template <typename T, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                            const float* __restrict__ lse, const float* __restrict__ delta,
                                                            const uint8_t* __restrict__ kvalid, int B, int T_, int H,
@@ -415,6 +500,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
   const float* del_bh = delta + (int64_t)bh * T_;
   const int kw0 = kb * KV_KB + w * 32;
   const float c = scale * LOG2E;
+  const float inv_ds = DROP ? 1.f / drop_scale : 1.f;
   const int KT = mask_kt(T_);
   const int64_t ldm = mask_ld(T_);
 
@@ -440,12 +526,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
       }
     }
   }
-  bool kok[2];
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
-    const int k = kw0 + kt * 16 + i;
-    kok[kt] = k < T_ && kvalid[(int64_t)b * T_ + k];
-  }
 
   f32x4 dk[2][4], dv[2][4];
 #pragma unroll
@@ -458,7 +538,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
   // keep-bit words of this workgroup's 2 key tiles x 4 groups x 64 queries: thread t < 64 moves
   // 16 bytes (row = tile*4 + g, 8 queries)
   auto load_mask = [&](int qs0) {
-    if (use_drop && tid < 64) {
+    if (DROP && tid < 64) {
       const int r = tid >> 3, cch = tid & 7;
       const int tile = kb * (KV_KB / 64) + (r >> 2);
       if (tile < KT)
@@ -467,22 +547,31 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
         mreg = make_uint4(0u, 0u, 0u, 0u);
     }
   };
-  auto stage_rows = [&](char* buf, int qs0) {
+  // per-query lse / delta of a tile: loaded with the Q/dO prefetch (wave 0), staged at the LDS write
+  float lse_r = 0.f, del_r = 0.f;
+  auto load_rows = [&](int qs0) {
+    if (tid < KV_QT) {
+      const int q = qs0 + tid;
+      lse_r = q < T_ ? lse_bh[q] * LOG2E : INFINITY;  // +inf -> P = 0 for padded rows
+      del_r = q < T_ ? -del_bh[q] * inv_ds : 0.f;     // -delta/ds: the dP accumulators' start
+    }
+  };
+  auto stage_rows = [&](char* buf) {
     float* lb = reinterpret_cast<float*>(buf + 2 * TILE);
     if (tid < KV_QT) {
-      int q = qs0 + tid;
-      lb[tid] = q < T_ ? lse_bh[q] * LOG2E : INFINITY;  // +inf -> P = 0 for padded rows
-      lb[KV_QT + tid] = q < T_ ? del_bh[q] : 0.f;
+      lb[tid] = lse_r;
+      lb[KV_QT + tid] = del_r;
     }
-    if (use_drop && tid < 64) *reinterpret_cast<uint4*>(buf + 2 * TILE + 2 * KV_QT * 4 + tid * 16) = mreg;
+    if (DROP && tid < 64) *reinterpret_cast<uint4*>(buf + 2 * TILE + 2 * KV_QT * 4 + tid * 16) = mreg;
   };
   const int nqt = (T_ + KV_QT - 1) / KV_QT;
   sq.load(Qg, ld, 0, T_, tid);
   sdo.load(dOg, ldo, 0, T_, tid);
   load_mask(0);
+  load_rows(0);
   sq.store(lds, tid);
   sdo.store(lds + TILE, tid);
-  stage_rows(lds, 0);
+  stage_rows(lds);
   __syncthreads();
 
   for (int it = 0; it < nqt; ++it) {
@@ -494,6 +583,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
       sq.load(Qg, ld, qs0 + KV_QT, T_, tid);
       sdo.load(dOg, ldo, qs0 + KV_QT, T_, tid);
       load_mask(qs0 + KV_QT);
+      load_rows(qs0 + KV_QT);
     }
     const char* Ql = cur;
     const char* dOl = cur + TILE;
@@ -505,11 +595,17 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       // S[q][key], dP[q][key]: C-layout row q = (2hf+qq)*16 + 4g + r, col key = kt*16 + i
-      f32x4 s[2][2], dp[2][2];
+      // dP starts at -delta/ds (row constant as the initial accumulator): dS = p*ds*acc
+      f32x4 s[2][2], dp[2][2], ndq[2];
 #pragma unroll
-      for (int qq = 0; qq < 2; ++qq)
+      for (int qq = 0; qq < 2; ++qq) {
+        ndq[qq] = *reinterpret_cast<const f32x4*>(drow + (2 * hf + qq) * 16 + 4 * g);
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) s[qq][kt] = dp[qq][kt] = zero4();
+        for (int kt = 0; kt < 2; ++kt) {
+          s[qq][kt] = zero4();
+          dp[qq][kt] = ndq[qq];
+        }
+      }
       if constexpr (BF) {
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
@@ -537,14 +633,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
             }
           }
       }
-      // P (dropped, for dV) -> s ; dS (for dK) -> dp
+      // P (dropped, for dV) -> s ; dS (for dK) -> dp.  Masked keys are not masked here: their P / dS
+      // only reach their own dK / dV rows, which the epilogue writes as zeros.
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
         const int qrow = (2 * hf + qq) * 16 + 4 * g;
         const float4 lq4 = *reinterpret_cast<const float4*>(lrow + qrow);
-        const float4 dq4 = *reinterpret_cast<const float4*>(drow + qrow);
         const float lq[4] = {lq4.x, lq4.y, lq4.z, lq4.w};
-        const float dq[4] = {dq4.x, dq4.y, dq4.z, dq4.w};
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
           // this lane's key: ko = key % 64 -> word row (tile half, group (ko%16)/4), bit (ko/16)*4 + ko%4
@@ -552,20 +647,20 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
           const int mrow_l = ((w * 32 + kt * 16) >> 6) * 4 + ((ko & 15) >> 2);
           const int bit = (ko >> 4) * 4 + (ko & 3);
           uint2 bits = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-          if (use_drop) bits = *reinterpret_cast<const uint2*>(mw + mrow_l * KV_QT + qrow);
+          if constexpr (DROP) bits = *reinterpret_cast<const uint2*>(mw + mrow_l * KV_QT + qrow);
           const uint32_t wd[4] = {bits.x & 0xFFFFu, bits.x >> 16, bits.y & 0xFFFFu, bits.y >> 16};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = kok[kt] ? exp2f(fmaf(s[qq][kt][r], c, -lq[r])) : 0.f;
-            float gp = dp[qq][kt][r];
-            float pd = p;
-            if (use_drop) {
+            const float p = rp_exp2(fmaf(s[qq][kt][r], c, -lq[r]));
+            if constexpr (DROP) {  // dS = p*(keep*ds*dP - delta) = p*ds*(keep ? acc : -delta/ds)
               const bool keep = (wd[r] >> bit) & 1u;
-              pd = keep ? p * drop_scale : 0.f;
-              gp = keep ? gp * drop_scale : 0.f;
+              const float pds = p * drop_scale;
+              s[qq][kt][r] = keep ? pds : 0.f;
+              dp[qq][kt][r] = pds * (keep ? dp[qq][kt][r] : ndq[qq][r]);
+            } else {
+              s[qq][kt][r] = p;
+              dp[qq][kt][r] = p * dp[qq][kt][r];
             }
-            s[qq][kt][r] = pd;
-            dp[qq][kt][r] = p * (gp - dq[r]);
           }
         }
       }
@@ -607,11 +702,11 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
     if (more) {
       sq.store(nxt, tid);
       sdo.store(nxt + TILE, tid);
-      stage_rows(nxt, qs0 + KV_QT);
+      stage_rows(nxt);
     }
     __syncthreads();
   }
-  // store: dk[kt][dt][r] = dK[key = kw0 + kt*16 + 4g + r][dk = dt*16 + i]
+  // store: dk[kt][dt][r] = dK[key = kw0 + kt*16 + 4g + r][dk = dt*16 + i]; masked keys -> 0
   T* dK = dqkv + (int64_t)b * T_ * ld + (int64_t)H * HD + h * HD;
   T* dV = dqkv + (int64_t)b * T_ * ld + 2LL * H * HD + h * HD;
 #pragma unroll
@@ -620,10 +715,11 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
     for (int r = 0; r < 4; ++r) {
       const int key = kw0 + kt * 16 + 4 * g + r;
       if (key >= T_) continue;
+      const bool ok = kvalid[(int64_t)b * T_ + key] != 0;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        rp_st(dK + (int64_t)key * ld + dt * 16 + i, dk[kt][dt][r] * scale);
-        rp_st(dV + (int64_t)key * ld + dt * 16 + i, dv[kt][dt][r]);
+        rp_st(dK + (int64_t)key * ld + dt * 16 + i, ok ? dk[kt][dt][r] * scale : 0.f);
+        rp_st(dV + (int64_t)key * ld + dt * 16 + i, ok ? dv[kt][dt][r] : 0.f);
       }
     }
 }
@@ -631,7 +727,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
 // =================================================================================================
 // backward: dQ per 128-query block (4 waves x 32 queries), sweep over 64-key tiles
 // =================================================================================================
-template <typename T>
+template <typename T, bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                                           const uint8_t* __restrict__ kvalid, int B, int T_, int H,
@@ -668,7 +764,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + qt * 16 + i;
     lq[qt] = q < T_ ? lse[(int64_t)bh * T_ + q] * LOG2E : INFINITY;
-    dq[qt] = q < T_ ? delta[(int64_t)bh * T_ + q] : 0.f;
+    dq[qt] = q < T_ ? -delta[(int64_t)bh * T_ + q] * (DROP ? 1.f / drop_scale : 1.f) : 0.f;  // -delta/ds
     if constexpr (BF) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -691,19 +787,21 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
     for (int dt = 0; dt < 4; ++dt) dqa[qt][dt] = zero4();
 
   Stage<T, FW_KT> sk, sv;
-  auto stage_mask = [&](char* buf, int k0) {
+  auto load_valid = [&](int k0) -> bool {
+    const int k = k0 + lane;
+    return w == 0 && k < T_ && kvalid[(int64_t)b * T_ + k];
+  };
+  auto stage_mask = [&](char* buf, bool ok) {
     float* kbm = reinterpret_cast<float*>(buf + 2 * TILE);
-    if (tid < FW_KT) {
-      int k = k0 + tid;
-      kbm[tid] = (k < T_ && kvalid[(int64_t)b * T_ + k]) ? 1.f : 0.f;
-    }
+    if (w == 0) kbm[lane] = ok ? 0.f : -INFINITY;  // key bias: the S^T accumulators' start
   };
   const int nkt = (T_ + FW_KT - 1) / FW_KT;
   sk.load(Kg, ld, 0, T_, tid);
   sv.load(Vg, ld, 0, T_, tid);
+  bool kvn = load_valid(0);
   sk.store(lds, tid);
   sv.store(lds + TILE, tid);
-  stage_mask(lds, 0);
+  stage_mask(lds, kvn);
   __syncthreads();
 
   for (int it = 0; it < nkt; ++it) {
@@ -713,7 +811,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
     const int k0 = it * FW_KT;
     // keep-bit word of this lane's queries for the tile (same register layout as the forward)
     uint32_t kwd[2] = {0u, 0u};
-    if (use_drop) {
+    if constexpr (DROP) {
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         const int q = q0 + qt * 16 + i;
@@ -723,17 +821,25 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
     if (more) {
       sk.load(Kg, ld, k0 + FW_KT, T_, tid);
       sv.load(Vg, ld, k0 + FW_KT, T_, tid);
+      kvn = load_valid(k0 + FW_KT);
     }
     const char* Kl = cur;
     const char* Vl = cur + TILE;
-    const float* kok = reinterpret_cast<const float*>(cur + 2 * TILE);
+    const float* kbias = reinterpret_cast<const float*>(cur + 2 * TILE);
 
-    // S^T[key][q] = K Q^T, dP^T[key][q] = V dO^T : row key = kt*16 + 4g + r, col q = qt*16 + i
+    // S^T[key][q] = K Q^T, dP^T[key][q] = V dO^T : row key = kt*16 + 4g + r, col q = qt*16 + i.
+    // Row constants as the initial accumulators: S^T starts at the key bias (0 / -inf: masked keys
+    // give P = 0 with no select), dP^T at -delta/ds.
     f32x4 s[4][2], dp[4][2];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int kt = 0; kt < 4; ++kt) {
+      const f32x4 kb4 = *reinterpret_cast<const f32x4*>(kbias + kt * 16 + 4 * g);
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) s[kt][qt] = dp[kt][qt] = zero4();
+      for (int qt = 0; qt < 2; ++qt) {
+        s[kt][qt] = kb4;
+        dp[kt][qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
+      }
+    }
     if constexpr (BF) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
@@ -761,19 +867,20 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
           }
         }
     }
-    // dS^T = P^T (gP^T - delta)
+    // dS^T = P^T (keep*ds*dP^T - delta) = P^T*ds*(keep ? acc : -delta/ds)
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      const float4 ok4 = *reinterpret_cast<const float4*>(kok + kt * 16 + 4 * g);
-      const float okr[4] = {ok4.x, ok4.y, ok4.z, ok4.w};
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = okr[r] != 0.f ? exp2f(fmaf(s[kt][qt][r], c, -lq[qt])) : 0.f;
-          float gp = dp[kt][qt][r];
-          if (use_drop) gp = ((kwd[qt] >> (4 * kt + r)) & 1u) ? gp * drop_scale : 0.f;
-          s[kt][qt][r] = p * (gp - dq[qt]);
+          const float p = rp_exp2(fmaf(s[kt][qt][r], c, -lq[qt]));
+          if constexpr (DROP) {
+            const bool keep = (kwd[qt] >> (4 * kt + r)) & 1u;
+            s[kt][qt][r] = (p * drop_scale) * (keep ? dp[kt][qt][r] : dq[qt]);
+          } else {
+            s[kt][qt][r] = p * dp[kt][qt][r];
+          }
         }
     }
     // dQ[q][dk] += dS K : A = dS (q on row = lane i, key slots), B = K columns (tr read)
@@ -805,7 +912,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
     if (more) {
       sk.store(nxt, tid);
       sv.store(nxt + TILE, tid);
-      stage_mask(nxt, k0 + FW_KT);
+      stage_mask(nxt, kvn);
     }
     __syncthreads();
   }
@@ -828,8 +935,12 @@ int launch_fwd(const void* qkv, const uint8_t* kv, int B, int T_, int H, float s
   const int nqb = (T_ + FW_QB - 1) / FW_QB;
   const uint32_t thr = rp_dropout_thresh(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  hipLaunchKernelGGL(attn_fwd_kernel<T>, dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv, kv, B, T_, H,
-                     scale, thr, ds, seed, (T*)out, lse, thr ? dmask : nullptr);
+  if (thr)
+    hipLaunchKernelGGL((attn_fwd_kernel<T, true>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv, kv, B,
+                       T_, H, scale, thr, ds, seed, (T*)out, lse, dmask);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<T, false>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv, kv, B,
+                       T_, H, scale, thr, ds, seed, (T*)out, lse, nullptr);
   return rp_check_launch("rp_attn_fwd");
 }
 
@@ -842,11 +953,18 @@ int launch_bwd(const void* qkv, const void* out, const void* dout, const float* 
   hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, (const T*)out,
                      (const T*)dout, B, T_, H, delta);
   const int nkb = (T_ + KV_KB - 1) / KV_KB;
-  hipLaunchKernelGGL(attn_bwd_kv_kernel<T>, dim3((unsigned)(nkb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                     (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
   const int nqb = (T_ + FW_QB - 1) / FW_QB;
-  hipLaunchKernelGGL(attn_bwd_q_kernel<T>, dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                     (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+  if (use) {
+    hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true>), dim3((unsigned)(nkb * B * H)), dim3(NT), 0, s, (const T*)qkv,
+                       (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+    hipLaunchKernelGGL((attn_bwd_q_kernel<T, true>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv,
+                       (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false>), dim3((unsigned)(nkb * B * H)), dim3(NT), 0, s, (const T*)qkv,
+                       (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+    hipLaunchKernelGGL((attn_bwd_q_kernel<T, false>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv,
+                       (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+  }
   return rp_check_launch("rp_attn_bwd");
 }
 

@@ -66,6 +66,10 @@ static inline uint32_t rp_dropout_thresh(float p) {
 // ----------------------------------------------------------------------------------------------
 // element load/store helpers (fp32 math everywhere)
 // ----------------------------------------------------------------------------------------------
+// 2^x as the bare v_exp_f32 (no denormal-range fix-up: results below 2^-126 flush to 0, which
+// softmax weights tolerate; exp2f() adds ~6 VALU per call for that fix-up)
+__device__ __forceinline__ float rp_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ float rp_ld(const float* p) { return *p; }
 __device__ __forceinline__ float rp_ld(const bf16* p) { return (float)(*p); }
 __device__ __forceinline__ void rp_st(float* p, float v) { *p = v; }
