@@ -167,7 +167,6 @@ __device__ __forceinline__ float quad_sum(float v) {
 // Outputs dm[j] (0xFFFF in each dropped half: the AND-NOT mask of the packed bf16 P pair) and
 // returns the 16 keep bits, bit (kt*4 + r).  Full-rate VALU only: a saturating packed 16-bit
 // subtract + arithmetic shift per pair, no 32-bit multiplies beyond the one seeding hash.
-typedef short i16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t drop_masks(uint32_t seed_bh, uint32_t q, uint32_t KT, uint32_t tile, uint32_t g,
                                                uint32_t thr, uint32_t dm[8]) {
   uint32_t st = rp_hash(seed_bh, (q * KT + tile) * 4u + g);

@@ -52,8 +52,44 @@ __device__ __forceinline__ uint32_t rp_hash(uint32_t seed, uint32_t idx) {
   return h;
 }
 
-__device__ __forceinline__ bool rp_keep(uint32_t seed, uint32_t idx, uint32_t thresh16) {
-  return (rp_hash(seed, idx) & 0xFFFFu) >= thresh16;
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+// Element dropout (GEMM / LayerNorm epilogues), per aligned group of 8 elements (index idx ->
+// group idx >> 3, slot e = idx & 7): w0 = rp_hash(seed, group), w(j+1) = xorshift32(w(j));
+// slot e reads the 16-bit half (e & 1) of w(e >> 1) as int16 and is kept iff it is
+// >= thresh16 - 32768 (probability 1 - p to 2^-16).  Returns the 8 keep bits (bit e).
+// One hash + 3 shift-xor steps per 8 elements; the keep test is a saturating packed 16-bit
+// subtract + arithmetic shift per pair (no 32-bit multiply per element).
+__device__ __forceinline__ uint32_t rp_keep8(uint32_t seed, uint32_t group, uint32_t thresh16) {
+  uint32_t w = rp_hash(seed, group);
+  const short ts = (short)((int)thresh16 - 32768);
+  const i16x2 t2 = {ts, ts};
+  uint32_t acc = 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j) {
+      w ^= w << 13;
+      w ^= w >> 17;
+      w ^= w << 5;
+    }
+    const i16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w), t2);  // < 0: dropped
+    const uint32_t m = __builtin_bit_cast(uint32_t, (i16x2)(d >> (short)15));
+    acc |= ~m & ((1u << (2 * j)) | (1u << (16 + 2 * j + 1)));
+  }
+  return (acc & 0xFFFFu) | (acc >> 16);
+}
+
+// keep bits of VPT consecutive elements starting at idx0 (idx0 % VPT == 0, VPT a power of two)
+template <int VPT>
+__device__ __forceinline__ uint32_t rp_keep_bits(uint32_t seed, uint32_t idx0, uint32_t thresh16) {
+  if constexpr (VPT >= 8) {
+    uint32_t b = 0u;
+#pragma unroll
+    for (int g = 0; g < VPT / 8; ++g) b |= rp_keep8(seed, (idx0 >> 3) + g, thresh16) << (8 * g);
+    return b;
+  } else {
+    return (rp_keep8(seed, idx0 >> 3, thresh16) >> (idx0 & 7)) & ((1u << VPT) - 1u);
+  }
 }
 
 static inline uint32_t rp_dropout_thresh(float p) {

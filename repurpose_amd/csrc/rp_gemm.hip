@@ -232,9 +232,9 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* ld
         for (int e = 0; e < OV; ++e) v[e] = fmaxf(v[e], 0.f);
       }
       if (ep.drop_thresh) {
-        const uint32_t base = (uint32_t)(m * N + n);
+        const uint32_t kb = rp_keep_bits<OV>(ep.drop_seed, (uint32_t)(m * N + n), ep.drop_thresh);
 #pragma unroll
-        for (int e = 0; e < OV; ++e) v[e] = rp_keep(ep.drop_seed, base + e, ep.drop_thresh) ? v[e] * ep.drop_scale : 0.f;
+        for (int e = 0; e < OV; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * ep.drop_scale : 0.f;
       }
       if (ep.gate) {
         if (ep.gate_bf16) {

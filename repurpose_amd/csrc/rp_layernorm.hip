@@ -122,13 +122,13 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_fwd_kernel(int64_t rows, LnF
   if (a.pe) load_row<VPT>(pe, a.pe, RP_F32, (row % a.pe_period) * D + c0);
   load_row<VPT>(gm, a.gamma, RP_F32, c0);
   load_row<VPT>(bt, a.beta, RP_F32, c0);
+  const uint32_t kb = a.drop_thresh ? rp_keep_bits<VPT>(a.drop_seed, (uint32_t)(row * D + c0), a.drop_thresh) : 0u;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     float y = (v[i] - mean) * rstd * gm[i] + bt[i];
     if (a.pe) y += pe[i];
     if (a.relu) y = fmaxf(y, 0.f);
-    if (a.drop_thresh)
-      y = rp_keep(a.drop_seed, (uint32_t)(row * D + c0 + i), a.drop_thresh) ? y * a.drop_scale : 0.f;
+    if (a.drop_thresh) y = ((kb >> i) & 1u) ? y * a.drop_scale : 0.f;
     v[i] = y;
   }
   if (a.out_f32) store_row<VPT>(v, a.out_f32, RP_F32, row * a.ld_out_f32 + c0);
@@ -171,9 +171,9 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_bwd_kernel(int64_t rows, LnB
     load_row<VPT>(g, a.dy, a.dy_dtype, row * a.lddy + c0);
     load_row<VPT>(x, a.x, a.x_dtype, row * a.ldx + c0);
     if (a.drop_thresh) {
+      const uint32_t kb = rp_keep_bits<VPT>(a.drop_seed, (uint32_t)(row * D + c0), a.drop_thresh);
 #pragma unroll
-      for (int i = 0; i < VPT; ++i)
-        g[i] = rp_keep(a.drop_seed, (uint32_t)(row * D + c0 + i), a.drop_thresh) ? g[i] * a.drop_scale : 0.f;
+      for (int i = 0; i < VPT; ++i) g[i] = ((kb >> i) & 1u) ? g[i] * a.drop_scale : 0.f;
     }
     if (a.y) {
       float yv[VPT];
@@ -206,9 +206,9 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_bwd_kernel(int64_t rows, LnB
     if (a.dx) store_row<VPT>(dx, a.dx, RP_F32, row * a.lddx + c0);
     if (a.dx_lp) {
       if (a.lp_thresh) {
+        const uint32_t kb = rp_keep_bits<VPT>(a.lp_seed, (uint32_t)(row * D + c0), a.lp_thresh);
 #pragma unroll
-        for (int i = 0; i < VPT; ++i)
-          dx[i] = rp_keep(a.lp_seed, (uint32_t)(row * D + c0 + i), a.lp_thresh) ? dx[i] * a.lp_scale : 0.f;
+        for (int i = 0; i < VPT; ++i) dx[i] = ((kb >> i) & 1u) ? dx[i] * a.lp_scale : 0.f;
       }
       store_row<VPT>(dx, a.dx_lp, a.dx_lp_dtype, row * a.lddx_lp + c0);
     }

@@ -22,9 +22,26 @@ def rp_hash(seed, idx):
     return h
 
 
+def xorshift32(w):
+    w = (w ^ (w << 13)) & M32
+    w = w ^ (w >> 17)
+    return (w ^ (w << 5)) & M32
+
+
 def keep_mask(seed, idx, p):
+    """GEMM / LayerNorm element dropout (csrc/rp_common.h rp_keep8): per aligned group of 8
+    elements one rp_hash + xorshift32 stream; 16-bit halves read as int16."""
     thr = int(p * 65536 + 0.5)
-    return (rp_hash(seed, idx) & 0xFFFF) >= thr
+    w0 = rp_hash(seed, idx >> 3)
+    words = [w0]
+    for _ in range(3):
+        words.append(xorshift32(words[-1]))
+    W = torch.stack(words, -1)
+    e = idx & 7
+    w = torch.gather(W, -1, (e >> 1).unsqueeze(-1)).squeeze(-1)
+    half = torch.where((e & 1) == 1, w >> 16, w & 0xFFFF)
+    sgn = torch.where(half >= 32768, half - 65536, half)
+    return sgn >= thr - 32768
 
 
 def rnd(*shape, dev, scale=1.0, seed=0):
