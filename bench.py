@@ -45,6 +45,14 @@ def flops_per_timestep(T, L=16, d=512, dff=2048, din=2944):
     return lin + attn + inp + fm + cls + reg
 
 
+# Algorithmic FLOPs per launch of the timed attention kernels (B sequences, H heads, T, dk):
+#   attn_fwd       S = QK^T and O = PV                         4*B*H*T^2*dk
+#   attn_bwd_dkdv  dV = P^T dO, dP = dO V^T, dK = dS^T Q        6*B*H*T^2*dk  (its S recompute excluded)
+#   attn_bwd_dq    dQ = dS K                                    2*B*H*T^2*dk  (its S, dP recompute excluded)
+# (together the SURVEY §8d attention count: 4*T*d forward + 8*T*d backward per token and layer)
+KERNEL_FLOPS = {"attn_fwd": 4.0, "attn_bwd_dkdv": 6.0, "attn_bwd_dq": 2.0}
+
+
 def synth_batch(B, T, dev, seed):
     g = torch.Generator(device="cpu").manual_seed(seed)
     v = torch.randn(B, T, 512, generator=g)
@@ -112,7 +120,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--roofline-kernel", default="attn_fwd")
+    ap.add_argument("--roofline-kernel", default="attn_bwd_dkdv", choices=list(KERNEL_FLOPS))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,7 +156,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    K.timer_start(args.roofline_kernel)
+    K.timer_start(*KERNEL_FLOPS)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -168,15 +176,19 @@ def main():
     if rank == 0:
         fpt = flops_per_timestep(T)
         H, dk = 8, 64
-        if args.roofline_kernel == "attn_fwd":
-            kflops = 4.0 * B * H * T * T * dk
-        else:
-            kflops = float("nan")
-        achieved = kflops / (kern_ms * 1e-3) / 1e12 if kern_ms else None
-        roof = {"kernel": args.roofline_kernel, "bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
-                "unit": "TFLOP/s", "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": None,
-                "avg_launch_ms": kern_ms, "flops_per_launch": kflops,
-                "step_tflops": fpt * value / world / 1e12, "step_frac": fpt * value / world / 1e12 / PEAK_BF16_TFLOPS}
+
+        def roofline(name):
+            ms = kern_ms.get(name)
+            kflops = KERNEL_FLOPS[name] * B * H * T * T * dk
+            ach = kflops / (ms * 1e-3) / 1e12 if ms else None
+            return {"kernel": name, "bound": "mfma", "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": (ach / PEAK_BF16_TFLOPS) if ach else None, "traffic": None, "avg_launch_ms": ms,
+                    "flops_per_launch": kflops}
+
+        roof = roofline(args.roofline_kernel)
+        roof["step_tflops"] = fpt * value / world / 1e12
+        roof["step_frac"] = roof["step_tflops"] / PEAK_BF16_TFLOPS
+        roof["other_kernels"] = [roofline(n) for n in KERNEL_FLOPS if n != args.roofline_kernel]
         res = {"metric": "feature-timesteps/sec (fwd+bwd) tri-modal T=2048", "value": value,
                "unit": "feature-timesteps/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",

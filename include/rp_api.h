@@ -184,10 +184,21 @@ int64_t rp_attn_dropmask_elems(int B, int T, int H);
 int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk,
                 float scale, float dropout_p, uint32_t seed, void* out, float* lse, uint16_t* dropmask,
                 void* stream);
-/* Backward; dqkv: [B*T, 3*H*dk] (fully overwritten); delta_ws: [B, H, T] fp32 workspace. */
+/* Backward; dqkv: [B*T, 3*H*dk] (fully overwritten); delta_ws: [B, H, T] fp32 workspace.
+ * = rp_attn_bwd_delta (delta = rowsum(dout * out)), then rp_attn_bwd_dkdv (dK, dV columns of dqkv,
+ * one workgroup per 128-key block) and rp_attn_bwd_dq (dQ columns, one per 128-query block); the
+ * three phases are also exported separately (per-kernel timing; same arguments). */
 int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
                 const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                 const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream);
+int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, int B, int T, int H, int dk, float* delta_ws,
+                      void* stream);
+int rp_attn_bwd_dkdv(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
+                     const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
+                     const uint16_t* dropmask, void* dqkv, void* stream);
+int rp_attn_bwd_dq(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
+                   const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
+                   const uint16_t* dropmask, void* dqkv, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Focal loss (alpha, gamma) on n frames.  mask may be NULL (all ones).

@@ -943,28 +943,58 @@ int launch_fwd(const void* qkv, const uint8_t* kv, int B, int T_, int H, float s
   return rp_check_launch("rp_attn_fwd");
 }
 
+// phases: bit 0 = delta pre-pass, bit 1 = dK/dV kernel, bit 2 = dQ kernel
 template <typename T>
-int launch_bwd(const void* qkv, const void* out, const void* dout, const float* lse, const uint8_t* kv, int B, int T_,
-               int H, float scale, float p, const uint16_t* dmask, void* dqkv, float* delta, hipStream_t s) {
+int launch_bwd(int phases, const void* qkv, const void* out, const void* dout, const float* lse, const uint8_t* kv,
+               int B, int T_, int H, float scale, float p, const uint16_t* dmask, void* dqkv, float* delta,
+               hipStream_t s) {
   const int use = rp_dropout_thresh(p) != 0;
   const float dsc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const int64_t rows = (int64_t)B * T_;
-  hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, (const T*)out,
-                     (const T*)dout, B, T_, H, delta);
+  if (phases & 1)
+    hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, (const T*)out,
+                       (const T*)dout, B, T_, H, delta);
   const int nkb = (T_ + KV_KB - 1) / KV_KB;
   const int nqb = (T_ + FW_QB - 1) / FW_QB;
-  if (use) {
-    hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true>), dim3((unsigned)(nkb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                       (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
-    hipLaunchKernelGGL((attn_bwd_q_kernel<T, true>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                       (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
-  } else {
-    hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false>), dim3((unsigned)(nkb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                       (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
-    hipLaunchKernelGGL((attn_bwd_q_kernel<T, false>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                       (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+  if (phases & 2) {
+    if (use)
+      hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true>), dim3((unsigned)(nkb * B * H)), dim3(NT), 0, s, (const T*)qkv,
+                         (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+    else
+      hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false>), dim3((unsigned)(nkb * B * H)), dim3(NT), 0, s, (const T*)qkv,
+                         (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+  }
+  if (phases & 4) {
+    if (use)
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv,
+                         (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+    else
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv,
+                         (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
   }
   return rp_check_launch("rp_attn_bwd");
+}
+
+int attn_bwd_entry(int phases, int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
+                   const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
+                   const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
+  RP_REQUIRE(dk == HD, "rp_attn_bwd: head dim %d unsupported (64)", dk);
+  RP_REQUIRE(B >= 0 && T >= 0 && H > 0, "rp_attn_bwd: bad shape");
+  if (B == 0 || T == 0) return RP_OK;
+  RP_REQUIRE(qkv && dout && lse && key_valid && dqkv && delta_ws && (out || !(phases & 1)), "rp_attn_bwd: null pointer");
+  RP_REQUIRE(rp_aligned16(qkv) && rp_aligned16(dout) && rp_aligned16(dqkv), "rp_attn_bwd: 16-byte alignment required");
+  RP_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "rp_attn_bwd: dropout_p out of range");
+  RP_REQUIRE(rp_dropout_thresh(dropout_p) == 0 || (dropmask && rp_aligned16(dropmask)),
+             "rp_attn_bwd: dropout needs the forward's dropmask");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RP_BF16)
+    return launch_bwd<bf16>(phases, qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p, dropmask, dqkv,
+                            delta_ws, s);
+  if (dtype == RP_F32)
+    return launch_bwd<float>(phases, qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p, dropmask, dqkv,
+                             delta_ws, s);
+  rp_set_error("rp_attn_bwd: bad dtype");
+  return RP_ERR_ARG;
 }
 
 }  // namespace
@@ -995,19 +1025,41 @@ extern "C" int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid,
 extern "C" int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
                            const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                            const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
-  RP_REQUIRE(dk == HD, "rp_attn_bwd: head dim %d unsupported (64)", dk);
-  RP_REQUIRE(B >= 0 && T >= 0 && H > 0, "rp_attn_bwd: bad shape");
+  return attn_bwd_entry(7, dtype, qkv, out, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
+                        delta_ws, stream);
+}
+
+extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, int B, int T, int H, int dk,
+                                 float* delta_ws, void* stream) {
+  RP_REQUIRE(dk == HD, "rp_attn_bwd_delta: head dim %d unsupported (64)", dk);
+  RP_REQUIRE(B >= 0 && T >= 0 && H > 0, "rp_attn_bwd_delta: bad shape");
   if (B == 0 || T == 0) return RP_OK;
-  RP_REQUIRE(qkv && out && dout && lse && key_valid && dqkv && delta_ws, "rp_attn_bwd: null pointer");
-  RP_REQUIRE(rp_aligned16(qkv) && rp_aligned16(dout) && rp_aligned16(dqkv), "rp_attn_bwd: 16-byte alignment required");
-  RP_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "rp_attn_bwd: dropout_p out of range");
-  RP_REQUIRE(rp_dropout_thresh(dropout_p) == 0 || (dropmask && rp_aligned16(dropmask)),
-             "rp_attn_bwd: dropout needs the forward's dropmask");
+  RP_REQUIRE(out && dout && delta_ws, "rp_attn_bwd_delta: null pointer");
   hipStream_t s = (hipStream_t)stream;
+  const int64_t rows = (int64_t)B * T;
   if (dtype == RP_BF16)
-    return launch_bwd<bf16>(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p, dropmask, dqkv, delta_ws, s);
-  if (dtype == RP_F32)
-    return launch_bwd<float>(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p, dropmask, dqkv, delta_ws, s);
-  rp_set_error("rp_attn_bwd: bad dtype");
-  return RP_ERR_ARG;
+    hipLaunchKernelGGL(attn_delta_kernel<bf16>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, (const bf16*)out,
+                       (const bf16*)dout, B, T, H, delta_ws);
+  else if (dtype == RP_F32)
+    hipLaunchKernelGGL(attn_delta_kernel<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, (const float*)out,
+                       (const float*)dout, B, T, H, delta_ws);
+  else {
+    rp_set_error("rp_attn_bwd_delta: bad dtype");
+    return RP_ERR_ARG;
+  }
+  return rp_check_launch("rp_attn_bwd_delta");
+}
+
+extern "C" int rp_attn_bwd_dkdv(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
+                                const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
+                                const uint16_t* dropmask, void* dqkv, void* stream) {
+  return attn_bwd_entry(2, dtype, qkv, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
+                        (float*)delta_ws, stream);
+}
+
+extern "C" int rp_attn_bwd_dq(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
+                              const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
+                              const uint16_t* dropmask, void* dqkv, void* stream) {
+  return attn_bwd_entry(4, dtype, qkv, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
+                        (float*)delta_ws, stream);
 }

@@ -13,38 +13,36 @@ from . import _native as N
 _DT = {torch.float32: N.RP_F32, torch.bfloat16: N.RP_BF16}
 
 # Live per-kernel timing with HIP events recorded on the launch stream (bench.py roofline).
-_timer = {"name": None, "ev": []}
+_timer = {"names": (), "ev": {}}
 
 
-def timer_start(name):
-    _timer["name"] = name
-    _timer["ev"] = []
+def timer_start(*names):
+    _timer["names"] = tuple(names)
+    _timer["ev"] = {n: [] for n in names}
 
 
 def timer_stop():
-    """Average duration (ms) of the timed kernel's launches since timer_start, or None."""
+    """{name: average duration (ms) of that kernel's launches since timer_start, or None}."""
     ev = _timer["ev"]
-    _timer["name"] = None
-    _timer["ev"] = []
-    if not ev:
-        return None
+    _timer["names"] = ()
+    _timer["ev"] = {}
     torch.cuda.synchronize()
-    return sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    return {n: (sum(a.elapsed_time(b) for a, b in v) / len(v) if v else None) for n, v in ev.items()}
 
 
 def _tick(name):
-    if _timer["name"] != name:
+    if name not in _timer["names"]:
         return None
     e = torch.cuda.Event(enable_timing=True)
     e.record()
-    return e
+    return (name, e)
 
 
-def _tock(e0):
-    if e0 is not None:
+def _tock(t0):
+    if t0 is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        _timer["ev"].append((e0, e1))
+        _timer["ev"][t0[0]].append((t0[1], e1))
 
 
 def _p(t):
@@ -231,9 +229,17 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
     dk = qkv.shape[1] // (3 * H)
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
+    st, dt = _stream(qkv), _dt(qkv)
     e0 = _tick("attn_bwd")
-    N.call("rp_attn_bwd", _dt(qkv), _p(qkv), _p(out), _p(dout), _p(lse), _p(key_valid), B, T, H, dk,
-           float(scale), float(dropout_p), _p(dropmask), _p(dqkv), _p(delta), _stream(qkv))
+    N.call("rp_attn_bwd_delta", dt, _p(out), _p(dout), B, T, H, dk, _p(delta), st)
+    e1 = _tick("attn_bwd_dkdv")
+    N.call("rp_attn_bwd_dkdv", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
+           float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
+    _tock(e1)
+    e2 = _tick("attn_bwd_dq")
+    N.call("rp_attn_bwd_dq", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
+           float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
+    _tock(e2)
     _tock(e0)
     return dqkv
 
