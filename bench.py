@@ -182,9 +182,17 @@ def main():
             kflops = KERNEL_FLOPS[name] * B * H * T * T * dk
             ach = kflops / (ms * 1e-3) / 1e12 if ms else None
             return {"kernel": name, "bound": "mfma", "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": (ach / PEAK_BF16_TFLOPS) if ach else None, "traffic": None, "avg_launch_ms": ms,
+                    "frac": (ach / PEAK_BF16_TFLOPS) if ach else None, "traffic": traffic.get(name),
+                    "traffic_unit": "bytes/launch (rocprofv3 PMC)", "avg_launch_ms": ms,
                     "flops_per_launch": kflops}
 
+        # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+        # (scripts/pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE doubled per the gfx950 correction)
+        try:
+            with open(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")) as f:
+                traffic = {k: v["hbm_bytes"] for k, v in json.load(f).items()}
+        except (OSError, ValueError, KeyError):
+            traffic = {}
         roof = roofline(args.roofline_kernel)
         roof["step_tflops"] = fpt * value / world / 1e12
         roof["step_frac"] = roof["step_tflops"] / PEAK_BF16_TFLOPS
