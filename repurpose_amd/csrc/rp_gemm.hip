@@ -496,22 +496,40 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
   if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab);
 }
 
-// dst[i] (+)= sum_s slab[s][i]  (fixed order: deterministic)
-__global__ void splitk_reduce_kernel(const float* __restrict__ slab, int S, int64_t n, float* __restrict__ dst,
-                                     int accumulate) {
-  const int64_t n4 = n / 4;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 acc = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s = 0; s < S; ++s) {
-      float4 q = reinterpret_cast<const float4*>(slab + (int64_t)s * n)[i];
-      acc.x += q.x; acc.y += q.y; acc.z += q.z; acc.w += q.w;
-    }
-    reinterpret_cast<float4*>(dst)[i] = acc;
+// dst[i] (+)= sum_s slab[s][i] in fixed slab order (deterministic), for the weight slabs (n
+// elements) and, in the same launch, the bias slabs (n2 elements, blocks past nb1).  Four slab
+// loads in flight per step.
+__device__ __forceinline__ void splitk_sum4(const float* __restrict__ slab, int S, int64_t n, int64_t i,
+                                            float* __restrict__ dst, int accumulate) {
+  float4 acc = accumulate ? reinterpret_cast<const float4*>(dst)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* p = reinterpret_cast<const float4*>(slab) + i;
+  const int64_t st = n / 4;
+  int s = 0;
+  for (; s + 4 <= S; s += 4) {
+    const float4 a = p[(int64_t)s * st], b = p[(int64_t)(s + 1) * st], c = p[(int64_t)(s + 2) * st],
+                 d = p[(int64_t)(s + 3) * st];
+    acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
+    acc.x += c.x; acc.y += c.y; acc.z += c.z; acc.w += c.w;
+    acc.x += d.x; acc.y += d.y; acc.z += d.z; acc.w += d.w;
   }
-  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float acc = accumulate ? dst[i] : 0.f;
-    for (int s = 0; s < S; ++s) acc += slab[(int64_t)s * n + i];
-    dst[i] = acc;
+  for (; s < S; ++s) {
+    const float4 a = p[(int64_t)s * st];
+    acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+  }
+  reinterpret_cast<float4*>(dst)[i] = acc;
+}
+
+__global__ void splitk_reduce_kernel(const float* __restrict__ slab, int S, int64_t n, float* __restrict__ dst,
+                                     const float* __restrict__ slab2, int64_t n2, float* __restrict__ dst2,
+                                     int nb1, int accumulate) {
+  // n, n2 are multiples of 4 (M, N multiples of 8)
+  if ((int)blockIdx.x < nb1) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += (int64_t)nb1 * blockDim.x)
+      splitk_sum4(slab, S, n, i, dst, accumulate);
+  } else {
+    const int64_t i = (int64_t)(blockIdx.x - nb1) * blockDim.x + threadIdx.x;
+    if (i < n2 / 4) splitk_sum4(slab2, S, n2, i, dst2, accumulate);
   }
 }
 
@@ -685,13 +703,11 @@ extern "C" int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const v
     rc = launch_gemm_t<float, float>(M, N, K, dY, ldy, 0, X, ldx, 0, slab, N, 1.f, e, s, splits, kchunk, bslab);
   if (rc) return rc;
   const int64_t n = M * N;
-  unsigned g = (unsigned)((n / 4 + 255) / 256);
+  int64_t g = (n / 4 + 255) / 256;
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, s, slab, splits, n, dW, accumulate);
-  if (db) {
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((M / 4 + 255) / 256 + 1)), dim3(256), 0, s, bslab, splits, M,
-                       db, accumulate);
-  }
+  const int64_t g2 = db ? (M / 4 + 255) / 256 : 0;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(g + g2)), dim3(256), 0, s, slab, splits, n, dW, bslab, M, db,
+                     (int)g, accumulate);
   return rp_check_launch("rp_gemm_wgrad");
 }
