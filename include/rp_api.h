@@ -181,6 +181,49 @@ int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ldx,
  * rp_attn_dropmask_elems() words), the backward reads them back.  dropmask may be NULL when
  * p == 0. */
 int64_t rp_attn_dropmask_elems(int B, int T, int H);
+
+/* General multi-head attention (self or cross): q rows [B*Tq] with stride ldq, k / v rows [B*Tk]
+ * with strides ldk / ldv (head h = columns h*dk .. h*dk+dk-1 of a row, any row stride that is a
+ * multiple of 8 elements), key_valid [B, Tk] (0 -> the key is masked with -inf for every query:
+ * torch key_padding_mask semantics; models/transformer.py's masked_fill(-1e9) is identical unless
+ * a sequence has no valid key at all).  out [B*Tq, ldo]; lse [B, H, Tq] fp32.  Backward: dout
+ * [B*Tq, lddo]; dq [B*Tq, lddq], dk / dv [B*Tk, lddk / lddv] are fully overwritten; delta_ws
+ * [B, H, Tq] fp32.  Dropout keep bits (forward -> backward) as for rp_attn_fwd with T -> (Tq, Tk):
+ * rp_mha_dropmask_elems(B, Tq, Tk, H) uint16 words [B*H][ceil(Tk/64)][4][roundup(Tq,64)].
+ * Replaces models/transformer.py:37-81 MultiHeadAttention's score/softmax/PV core (self attention
+ * of EncoderLayer :84-102, cross attention of CrossAttentionEncoderLayer :105-130 and
+ * CrossSelfEncoderLayer :133-176). */
+typedef struct rp_mha_args {
+  const void* q;
+  int64_t ldq;
+  const void* k;
+  int64_t ldk;
+  const void* v;
+  int64_t ldv;
+  const uint8_t* key_valid;
+  int B, Tq, Tk, H, head_dim;
+  float scale;
+  float dropout_p;
+  uint32_t seed;
+  void* out;
+  int64_t ldo;
+  float* lse;
+  uint16_t* dropmask;
+  const void* dout;
+  int64_t lddo;
+  void* dq;
+  int64_t lddq;
+  void* dk;
+  int64_t lddk;
+  void* dv;
+  int64_t lddv;
+  float* delta_ws;
+} rp_mha_args;
+
+int64_t rp_mha_dropmask_elems(int B, int Tq, int Tk, int H);
+int rp_mha_fwd(int dtype, const rp_mha_args* args, void* stream);
+/* phases: 1 = delta pre-pass, 2 = dK/dV, 4 = dQ (7 = all, in that order) */
+int rp_mha_bwd(int dtype, const rp_mha_args* args, int phases, void* stream);
 int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk,
                 float scale, float dropout_p, uint32_t seed, void* out, float* lse, uint16_t* dropmask,
                 void* stream);

@@ -42,6 +42,14 @@ class LnBwdArgs(ctypes.Structure):
                 ("dx_lp_seed", c_u32), ("dgamma_part", c_vp), ("dbeta_part", c_vp)]
 
 
+class MhaArgs(ctypes.Structure):
+    _fields_ = [("q", c_vp), ("ldq", c_i64), ("k", c_vp), ("ldk", c_i64), ("v", c_vp), ("ldv", c_i64),
+                ("key_valid", c_vp), ("B", c_i), ("Tq", c_i), ("Tk", c_i), ("H", c_i), ("head_dim", c_i),
+                ("scale", c_f), ("dropout_p", c_f), ("seed", c_u32), ("out", c_vp), ("ldo", c_i64), ("lse", c_vp),
+                ("dropmask", c_vp), ("dout", c_vp), ("lddo", c_i64), ("dq", c_vp), ("lddq", c_i64), ("dk", c_vp),
+                ("lddk", c_i64), ("dv", c_vp), ("lddv", c_i64), ("delta_ws", c_vp)]
+
+
 # name -> (restype, argtypes); mirrors include/rp_api.h one to one
 _SIGNATURES = {
     "rp_version": (c_i, []),
@@ -64,6 +72,9 @@ _SIGNATURES = {
     "rp_attn_bwd_delta": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_vp, c_vp]),
     "rp_attn_bwd_dkdv": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp]),
     "rp_attn_bwd_dq": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp]),
+    "rp_mha_dropmask_elems": (c_i64, [c_i, c_i, c_i, c_i]),
+    "rp_mha_fwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_vp]),
+    "rp_mha_bwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_i, c_vp]),
     "rp_focal_fwd_sum": (c_i, [c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_vp]),
     "rp_focal_elementwise": (c_i, [c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_vp]),
     "rp_focal_bwd": (c_i, [c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_i, c_vp, c_vp]),

@@ -60,6 +60,25 @@ __device__ __forceinline__ int lds_off(int row, int byte) {
 __host__ __device__ inline int64_t mask_ld(int T) { return ((int64_t)T + 63) / 64 * 64; }
 __host__ __device__ inline int mask_kt(int T) { return (T + 63) / 64; }
 
+// ----- problem description (device side of rp_mha_args) ------------------------------------------
+// q [B*Tq rows, ldq], k / v [B*Tk rows, ldk / ldv]: head h at columns h*64..h*64+63 of each row;
+// out / dout [B*Tq rows, ldo / lddo]; dq [B*Tq, lddq], dk / dv [B*Tk, lddk / lddv];
+// lse / delta [B, H, Tq] fp32; key_valid [B, Tk]; dropout keep bits over (Tq, Tk) (see mask_ld).
+struct MhaDev {
+  const void* q; const void* k; const void* v;
+  int64_t ldq, ldk, ldv;
+  const uint8_t* kvalid;
+  int B, Tq, Tk, H;
+  float scale;
+  uint32_t drop_thresh; float drop_scale; uint32_t seed;
+  void* out; int64_t ldo;
+  float* lse;
+  uint16_t* dmask;
+  const void* dout; int64_t lddo;
+  float* delta;
+  void* dq; int64_t lddq; void* dk; int64_t lddk; void* dv; int64_t lddv;
+};
+
 // ----- global [rows][64] (row stride ld elements) <-> LDS [rows][ROWB] staging ------------------
 template <typename T, int ROWS>
 struct Stage {
@@ -195,32 +214,34 @@ constexpr int FW_QB = NW * 32;  // queries per workgroup
 constexpr int FW_KT = 64;       // keys per tile
 
 template <typename T, bool DROP>
-__global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2) void attn_fwd_kernel(const T* __restrict__ qkv, const uint8_t* __restrict__ kvalid,
-                                                        int B, int T_, int H, float scale, uint32_t drop_thresh,
-                                                        float drop_scale, uint32_t seed, T* __restrict__ out,
-                                                        float* __restrict__ lse, uint16_t* __restrict__ dmask) {
+__global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2) void attn_fwd_kernel(MhaDev a) {
   using C = AttnCfg<T>;
   constexpr int TILE = FW_KT * C::ROWB;
   constexpr int BUF = 2 * TILE + FW_KT * 4 + 16;
   __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, i = lane & 15;
-  const int nqb = (T_ + FW_QB - 1) / FW_QB;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const uint8_t* __restrict__ kvalid = a.kvalid;
+  const float scale = a.scale;
+  const uint32_t drop_thresh = a.drop_thresh;
+  const float drop_scale = a.drop_scale;
+  float* __restrict__ lse = a.lse;
+  const int nqb = (Tq + FW_QB - 1) / FW_QB;
   const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
   const int bh = L / nqb, qb = L % nqb;
   const int b = bh / H, h = bh % H;
-  const int64_t ld = 3LL * H * HD;
-  const T* seq = qkv + (int64_t)b * T_ * ld;
-  const T* Qg = seq + h * HD;
-  const T* Kg = seq + (int64_t)H * HD + h * HD;
-  const T* Vg = seq + 2LL * H * HD + h * HD;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv;
+  const T* Qg = (const T*)a.q + (int64_t)b * Tq * ldq + h * HD;
+  const T* Kg = (const T*)a.k + (int64_t)b * Tk * ldk + h * HD;
+  const T* Vg = (const T*)a.v + (int64_t)b * Tk * ldv + h * HD;
   const int q0 = qb * FW_QB + w * 32;  // this wave's first query
-  const uint32_t seed_bh = rp_hash(seed, (uint32_t)bh);
+  const uint32_t seed_bh = rp_hash(a.seed, (uint32_t)bh);
   const float c = scale * LOG2E;
   const float rth = RESCALE_LOG2 / c;  // deferred-rescale threshold in score units
-  const int KT = mask_kt(T_);
-  const int64_t ldm = mask_ld(T_);
-  uint16_t* mrow = dmask ? dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
+  uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
 
   // Q^T operand (B operand of S^T = K Q^T): lane holds Q[q0 + qt*16 + i][dk slots]
   constexpr bool BF = std::is_same<T, bf16>::value;
@@ -230,13 +251,13 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) qf[qt][s] = row_frag_gmem((const bf16*)Qg, ld, q0 + qt * 16, T_, s * 32, lane);
+      for (int s = 0; s < 2; ++s) qf[qt][s] = row_frag_gmem((const bf16*)Qg, ldq, q0 + qt * 16, Tq, s * 32, lane);
   } else {
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       int q = q0 + qt * 16 + i;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) qs[qt][s] = q < T_ ? (float)Qg[(int64_t)q * ld + 4 * s + g] : 0.f;
+      for (int s = 0; s < 16; ++s) qs[qt][s] = q < Tq ? (float)Qg[(int64_t)q * ldq + 4 * s + g] : 0.f;
     }
   }
 
@@ -248,12 +269,12 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   float m[2] = {-INFINITY, -INFINITY}, lp[2] = {0.f, 0.f};
 
   Stage<T, FW_KT> sk, sv;
-  const int nkt = (T_ + FW_KT - 1) / FW_KT;
+  const int nkt = (Tk + FW_KT - 1) / FW_KT;
   // key-valid flags of a tile: loaded with the K/V prefetch (wave 0, one byte per lane), staged as
   // an additive bias + a "no masked key" flag at the LDS write
   auto load_valid = [&](int k0) -> bool {
     const int k = k0 + lane;
-    return w == 0 && k < T_ && kvalid[(int64_t)b * T_ + k];
+    return w == 0 && k < Tk && kvalid[(int64_t)b * Tk + k];
   };
   auto stage_mask = [&](char* buf, bool ok) {
     float* kb = reinterpret_cast<float*>(buf + 2 * TILE);
@@ -263,8 +284,8 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
       if (lane == 0) *reinterpret_cast<int*>(buf + 2 * TILE + FW_KT * 4) = bal == ~0ull;
     }
   };
-  sk.load(Kg, ld, 0, T_, tid);
-  sv.load(Vg, ld, 0, T_, tid);
+  sk.load(Kg, ldk, 0, Tk, tid);
+  sv.load(Vg, ldv, 0, Tk, tid);
   bool kvn = load_valid(0);
   sk.store(lds, tid);
   sv.store(lds + TILE, tid);
@@ -277,8 +298,8 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     const bool more = kt_i + 1 < nkt;
     const int k0 = kt_i * FW_KT;
     if (more) {
-      sk.load(Kg, ld, k0 + FW_KT, T_, tid);
-      sv.load(Vg, ld, k0 + FW_KT, T_, tid);
+      sk.load(Kg, ldk, k0 + FW_KT, Tk, tid);
+      sv.load(Vg, ldv, k0 + FW_KT, Tk, tid);
       kvn = load_valid(k0 + FW_KT);
     }
     const char* Kl = cur;
@@ -365,7 +386,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
       for (int qt = 0; qt < 2; ++qt) {
         const int q = q0 + qt * 16 + i;
         const uint32_t word = drop_masks(seed_bh, (uint32_t)q, (uint32_t)KT, (uint32_t)kt_i, (uint32_t)g, drop_thresh, dm[qt]);
-        if (q < T_) mrow[((int64_t)kt_i * 4 + g) * ldm + q] = (uint16_t)word;
+        if (q < Tq) mrow[((int64_t)kt_i * 4 + g) * ldm + q] = (uint16_t)word;
       }
     }
     // ---- O^T[dk][q] += V^T P^T ----
@@ -423,19 +444,20 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   }
 
   // ---- epilogue: O[q][dk] = O^T / l ; lse ----
-  const int64_t ldo = (int64_t)H * HD;
+  const int64_t ldo = a.ldo;
+  T* __restrict__ out = (T*)a.out;
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const float l = quad_sum(lp[qt]);
     const int q = q0 + qt * 16 + i;
-    if (q >= T_) continue;
+    if (q >= Tq) continue;
     const float inv = drop_scale / l;
-    T* orow = out + ((int64_t)b * T_ + q) * ldo + h * HD;
+    T* orow = out + ((int64_t)b * Tq + q) * ldo + h * HD;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) rp_st(orow + dt * 16 + 4 * g + r, o[qt][dt][r] * inv);
-    if (g == 0) lse[(int64_t)bh * T_ + q] = m[qt] * scale + logf(l);
+    if (g == 0) lse[(int64_t)bh * Tq + q] = m[qt] * scale + logf(l);
   }
 }
 
@@ -443,23 +465,24 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 // backward pre-pass: delta[bh][q] = sum_d dO[q][d] * O[q][d]
 // =================================================================================================
 template <typename T>
-__global__ void attn_delta_kernel(const T* __restrict__ out, const T* __restrict__ dout, int B, int T_, int H,
-                                  float* __restrict__ delta) {
-  // one wave per (b, t) row of H*64 elements; 8 lanes per head
+__global__ void attn_delta_kernel(MhaDev a) {
+  // one wave per (b, t) query row; 8 lanes per head
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (int64_t)B * T_) return;
-  const int D = H * HD;
+  if (row >= (int64_t)a.B * a.Tq) return;
+  const int D = a.H * HD;
+  const T* o = (const T*)a.out + row * a.ldo;
+  const T* d = (const T*)a.dout + row * a.lddo;
   for (int e = lane * 8; e < D; e += 512) {
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += rp_ld(out + row * D + e + j) * rp_ld(dout + row * D + e + j);
+    for (int j = 0; j < 8; ++j) s += rp_ld(o + e + j) * rp_ld(d + e + j);
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
     if ((lane & 7) == 0) {
-      const int b = (int)(row / T_), t = (int)(row % T_);
-      delta[((int64_t)b * H + e / HD) * T_ + t] = s;
+      const int b = (int)(row / a.Tq), t = (int)(row % a.Tq);
+      a.delta[((int64_t)b * a.H + e / HD) * a.Tq + t] = s;
     }
   }
 }
@@ -471,11 +494,7 @@ constexpr int KV_KB = NW * 32;
 constexpr int KV_QT = 64;
 
 template <typename T, bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
-                                                           const float* __restrict__ lse, const float* __restrict__ delta,
-                                                           const uint8_t* __restrict__ kvalid, int B, int T_, int H,
-                                                           float scale, int use_drop, float drop_scale,
-                                                           const uint16_t* __restrict__ dmask, T* __restrict__ dqkv) {
+__global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   using C = AttnCfg<T>;
   constexpr bool BF = std::is_same<T, bf16>::value;
   constexpr int TILE = KV_QT * C::ROWB;
@@ -484,24 +503,26 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
   __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, i = lane & 15;
-  const int nkb = (T_ + KV_KB - 1) / KV_KB;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const uint8_t* __restrict__ kvalid = a.kvalid;
+  const float scale = a.scale, drop_scale = a.drop_scale;
+  const uint16_t* __restrict__ dmask = a.dmask;
+  const int nkb = (Tk + KV_KB - 1) / KV_KB;
   const int L = rp_xcd_remap(blockIdx.x, nkb * B * H);
   const int bh = L / nkb, kb = L % nkb;
   const int b = bh / H, h = bh % H;
-  const int64_t ld = 3LL * H * HD;
-  const int64_t ldo = (int64_t)H * HD;
-  const T* seq = qkv + (int64_t)b * T_ * ld;
-  const T* Qg = seq + h * HD;
-  const T* Kg = seq + (int64_t)H * HD + h * HD;
-  const T* Vg = seq + 2LL * H * HD + h * HD;
-  const T* dOg = dout + (int64_t)b * T_ * ldo + h * HD;
-  const float* lse_bh = lse + (int64_t)bh * T_;
-  const float* del_bh = delta + (int64_t)bh * T_;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
+  const T* Qg = (const T*)a.q + (int64_t)b * Tq * ldq + h * HD;
+  const T* Kg = (const T*)a.k + (int64_t)b * Tk * ldk + h * HD;
+  const T* Vg = (const T*)a.v + (int64_t)b * Tk * ldv + h * HD;
+  const T* dOg = (const T*)a.dout + (int64_t)b * Tq * lddo + h * HD;
+  const float* lse_bh = a.lse + (int64_t)bh * Tq;
+  const float* del_bh = a.delta + (int64_t)bh * Tq;
   const int kw0 = kb * KV_KB + w * 32;
   const float c = scale * LOG2E;
   const float inv_ds = DROP ? 1.f / drop_scale : 1.f;
-  const int KT = mask_kt(T_);
-  const int64_t ldm = mask_ld(T_);
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
 
   // K, V as B operands of S = Q K^T and dP = dO V^T: lane holds X[kw0 + kt*16 + i][dk slots]
   bf16x8 kf[2][2], vf[2][2];
@@ -511,8 +532,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        kf[kt][s] = row_frag_gmem((const bf16*)Kg, ld, kw0 + kt * 16, T_, s * 32, lane);
-        vf[kt][s] = row_frag_gmem((const bf16*)Vg, ld, kw0 + kt * 16, T_, s * 32, lane);
+        kf[kt][s] = row_frag_gmem((const bf16*)Kg, ldk, kw0 + kt * 16, Tk, s * 32, lane);
+        vf[kt][s] = row_frag_gmem((const bf16*)Vg, ldv, kw0 + kt * 16, Tk, s * 32, lane);
       }
   } else {
 #pragma unroll
@@ -520,8 +541,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
       const int k = kw0 + kt * 16 + i;
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        ks_[kt][s] = k < T_ ? (float)Kg[(int64_t)k * ld + 4 * s + g] : 0.f;
-        vs_[kt][s] = k < T_ ? (float)Vg[(int64_t)k * ld + 4 * s + g] : 0.f;
+        ks_[kt][s] = k < Tk ? (float)Kg[(int64_t)k * ldk + 4 * s + g] : 0.f;
+        vs_[kt][s] = k < Tk ? (float)Vg[(int64_t)k * ldv + 4 * s + g] : 0.f;
       }
     }
   }
@@ -551,8 +572,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
   auto load_rows = [&](int qs0) {
     if (tid < KV_QT) {
       const int q = qs0 + tid;
-      lse_r = q < T_ ? lse_bh[q] * LOG2E : INFINITY;  // +inf -> P = 0 for padded rows
-      del_r = q < T_ ? -del_bh[q] * inv_ds : 0.f;     // -delta/ds: the dP accumulators' start
+      lse_r = q < Tq ? lse_bh[q] * LOG2E : INFINITY;  // +inf -> P = 0 for padded rows
+      del_r = q < Tq ? -del_bh[q] * inv_ds : 0.f;     // -delta/ds: the dP accumulators' start
     }
   };
   auto stage_rows = [&](char* buf) {
@@ -563,9 +584,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
     }
     if (DROP && tid < 64) *reinterpret_cast<uint4*>(buf + 2 * TILE + 2 * KV_QT * 4 + tid * 16) = mreg;
   };
-  const int nqt = (T_ + KV_QT - 1) / KV_QT;
-  sq.load(Qg, ld, 0, T_, tid);
-  sdo.load(dOg, ldo, 0, T_, tid);
+  const int nqt = (Tq + KV_QT - 1) / KV_QT;
+  sq.load(Qg, ldq, 0, Tq, tid);
+  sdo.load(dOg, lddo, 0, Tq, tid);
   load_mask(0);
   load_rows(0);
   sq.store(lds, tid);
@@ -579,8 +600,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
     const bool more = it + 1 < nqt;
     const int qs0 = it * KV_QT;
     if (more) {
-      sq.load(Qg, ld, qs0 + KV_QT, T_, tid);
-      sdo.load(dOg, ldo, qs0 + KV_QT, T_, tid);
+      sq.load(Qg, ldq, qs0 + KV_QT, Tq, tid);
+      sdo.load(dOg, lddo, qs0 + KV_QT, Tq, tid);
       load_mask(qs0 + KV_QT);
       load_rows(qs0 + KV_QT);
     }
@@ -706,19 +727,19 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
     __syncthreads();
   }
   // store: dk[kt][dt][r] = dK[key = kw0 + kt*16 + 4g + r][dk = dt*16 + i]; masked keys -> 0
-  T* dK = dqkv + (int64_t)b * T_ * ld + (int64_t)H * HD + h * HD;
-  T* dV = dqkv + (int64_t)b * T_ * ld + 2LL * H * HD + h * HD;
+  T* dK = (T*)a.dk + (int64_t)b * Tk * a.lddk + h * HD;
+  T* dV = (T*)a.dv + (int64_t)b * Tk * a.lddv + h * HD;
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = kw0 + kt * 16 + 4 * g + r;
-      if (key >= T_) continue;
-      const bool ok = kvalid[(int64_t)b * T_ + key] != 0;
+      if (key >= Tk) continue;
+      const bool ok = kvalid[(int64_t)b * Tk + key] != 0;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        rp_st(dK + (int64_t)key * ld + dt * 16 + i, ok ? dk[kt][dt][r] * scale : 0.f);
-        rp_st(dV + (int64_t)key * ld + dt * 16 + i, ok ? dv[kt][dt][r] : 0.f);
+        rp_st(dK + (int64_t)key * a.lddk + dt * 16 + i, ok ? dk[kt][dt][r] * scale : 0.f);
+        rp_st(dV + (int64_t)key * a.lddv + dt * 16 + i, ok ? dv[kt][dt][r] : 0.f);
       }
     }
 }
@@ -727,11 +748,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(const T* __restrict_
 // backward: dQ per 128-query block (4 waves x 32 queries), sweep over 64-key tiles
 // =================================================================================================
 template <typename T, bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
-                                                          const float* __restrict__ lse, const float* __restrict__ delta,
-                                                          const uint8_t* __restrict__ kvalid, int B, int T_, int H,
-                                                          float scale, int use_drop, float drop_scale,
-                                                          const uint16_t* __restrict__ dmask, T* __restrict__ dqkv) {
+__global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
   using C = AttnCfg<T>;
   constexpr bool BF = std::is_same<T, bf16>::value;
   constexpr int TILE = FW_KT * C::ROWB;
@@ -739,22 +756,25 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
   __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, i = lane & 15;
-  const int nqb = (T_ + FW_QB - 1) / FW_QB;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const uint8_t* __restrict__ kvalid = a.kvalid;
+  const float scale = a.scale, drop_scale = a.drop_scale;
+  const float* __restrict__ lse = a.lse;
+  const float* __restrict__ delta = a.delta;
+  const int nqb = (Tq + FW_QB - 1) / FW_QB;
   const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
   const int bh = L / nqb, qb = L % nqb;
   const int b = bh / H, h = bh % H;
-  const int64_t ld = 3LL * H * HD;
-  const int64_t ldo = (int64_t)H * HD;
-  const T* seq = qkv + (int64_t)b * T_ * ld;
-  const T* Qg = seq + h * HD;
-  const T* Kg = seq + (int64_t)H * HD + h * HD;
-  const T* Vg = seq + 2LL * H * HD + h * HD;
-  const T* dOg = dout + (int64_t)b * T_ * ldo + h * HD;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
+  const T* Qg = (const T*)a.q + (int64_t)b * Tq * ldq + h * HD;
+  const T* Kg = (const T*)a.k + (int64_t)b * Tk * ldk + h * HD;
+  const T* Vg = (const T*)a.v + (int64_t)b * Tk * ldv + h * HD;
+  const T* dOg = (const T*)a.dout + (int64_t)b * Tq * lddo + h * HD;
   const int q0 = qb * FW_QB + w * 32;
   const float c = scale * LOG2E;
-  const int KT = mask_kt(T_);
-  const int64_t ldm = mask_ld(T_);
-  const uint16_t* mrow = dmask ? dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
+  const uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
 
   bf16x8 qf[2][2], df[2][2];
   float qs[2][16], dsv[2][16];
@@ -762,19 +782,19 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + qt * 16 + i;
-    lq[qt] = q < T_ ? lse[(int64_t)bh * T_ + q] * LOG2E : INFINITY;
-    dq[qt] = q < T_ ? -delta[(int64_t)bh * T_ + q] * (DROP ? 1.f / drop_scale : 1.f) : 0.f;  // -delta/ds
+    lq[qt] = q < Tq ? lse[(int64_t)bh * Tq + q] * LOG2E : INFINITY;
+    dq[qt] = q < Tq ? -delta[(int64_t)bh * Tq + q] * (DROP ? 1.f / drop_scale : 1.f) : 0.f;  // -delta/ds
     if constexpr (BF) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        qf[qt][s] = row_frag_gmem((const bf16*)Qg, ld, q0 + qt * 16, T_, s * 32, lane);
-        df[qt][s] = row_frag_gmem((const bf16*)dOg, ldo, q0 + qt * 16, T_, s * 32, lane);
+        qf[qt][s] = row_frag_gmem((const bf16*)Qg, ldq, q0 + qt * 16, Tq, s * 32, lane);
+        df[qt][s] = row_frag_gmem((const bf16*)dOg, lddo, q0 + qt * 16, Tq, s * 32, lane);
       }
     } else {
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        qs[qt][s] = q < T_ ? (float)Qg[(int64_t)q * ld + 4 * s + g] : 0.f;
-        dsv[qt][s] = q < T_ ? (float)dOg[(int64_t)q * ldo + 4 * s + g] : 0.f;
+        qs[qt][s] = q < Tq ? (float)Qg[(int64_t)q * ldq + 4 * s + g] : 0.f;
+        dsv[qt][s] = q < Tq ? (float)dOg[(int64_t)q * lddo + 4 * s + g] : 0.f;
       }
     }
   }
@@ -788,15 +808,15 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
   Stage<T, FW_KT> sk, sv;
   auto load_valid = [&](int k0) -> bool {
     const int k = k0 + lane;
-    return w == 0 && k < T_ && kvalid[(int64_t)b * T_ + k];
+    return w == 0 && k < Tk && kvalid[(int64_t)b * Tk + k];
   };
   auto stage_mask = [&](char* buf, bool ok) {
     float* kbm = reinterpret_cast<float*>(buf + 2 * TILE);
     if (w == 0) kbm[lane] = ok ? 0.f : -INFINITY;  // key bias: the S^T accumulators' start
   };
-  const int nkt = (T_ + FW_KT - 1) / FW_KT;
-  sk.load(Kg, ld, 0, T_, tid);
-  sv.load(Vg, ld, 0, T_, tid);
+  const int nkt = (Tk + FW_KT - 1) / FW_KT;
+  sk.load(Kg, ldk, 0, Tk, tid);
+  sv.load(Vg, ldv, 0, Tk, tid);
   bool kvn = load_valid(0);
   sk.store(lds, tid);
   sv.store(lds + TILE, tid);
@@ -814,12 +834,12 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         const int q = q0 + qt * 16 + i;
-        kwd[qt] = q < T_ ? (uint32_t)mrow[((int64_t)it * 4 + g) * ldm + q] : 0u;
+        kwd[qt] = q < Tq ? (uint32_t)mrow[((int64_t)it * 4 + g) * ldm + q] : 0u;
       }
     }
     if (more) {
-      sk.load(Kg, ld, k0 + FW_KT, T_, tid);
-      sv.load(Vg, ld, k0 + FW_KT, T_, tid);
+      sk.load(Kg, ldk, k0 + FW_KT, Tk, tid);
+      sv.load(Vg, ldv, k0 + FW_KT, Tk, tid);
       kvn = load_valid(k0 + FW_KT);
     }
     const char* Kl = cur;
@@ -916,117 +936,179 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(const T* __restrict__
     __syncthreads();
   }
   // store: dqa[qt][dt][r] = dQ[q = q0 + qt*16 + 4g + r][dk = dt*16 + i]
-  T* dQ = dqkv + (int64_t)b * T_ * ld + h * HD;
+  T* dQ = (T*)a.dq + (int64_t)b * Tq * a.lddq + h * HD;
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int q = q0 + qt * 16 + 4 * g + r;
-      if (q >= T_) continue;
+      if (q >= Tq) continue;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) rp_st(dQ + (int64_t)q * ld + dt * 16 + i, dqa[qt][dt][r] * scale);
+      for (int dt = 0; dt < 4; ++dt) rp_st(dQ + (int64_t)q * a.lddq + dt * 16 + i, dqa[qt][dt][r] * scale);
     }
 }
 
 template <typename T>
-int launch_fwd(const void* qkv, const uint8_t* kv, int B, int T_, int H, float scale, float p, uint32_t seed,
-               void* out, float* lse, uint16_t* dmask, hipStream_t s) {
-  const int nqb = (T_ + FW_QB - 1) / FW_QB;
-  const uint32_t thr = rp_dropout_thresh(p);
-  const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  if (thr)
-    hipLaunchKernelGGL((attn_fwd_kernel<T, true>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv, kv, B,
-                       T_, H, scale, thr, ds, seed, (T*)out, lse, dmask);
+int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
+  const int nqb = (a.Tq + FW_QB - 1) / FW_QB;
+  const dim3 grid((unsigned)(nqb * a.B * a.H));
+  if (a.drop_thresh)
+    hipLaunchKernelGGL((attn_fwd_kernel<T, true>), grid, dim3(NT), 0, s, a);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<T, false>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv, kv, B,
-                       T_, H, scale, thr, ds, seed, (T*)out, lse, nullptr);
-  return rp_check_launch("rp_attn_fwd");
+    hipLaunchKernelGGL((attn_fwd_kernel<T, false>), grid, dim3(NT), 0, s, a);
+  return rp_check_launch("rp_mha_fwd");
 }
 
 // phases: bit 0 = delta pre-pass, bit 1 = dK/dV kernel, bit 2 = dQ kernel
 template <typename T>
-int launch_bwd(int phases, const void* qkv, const void* out, const void* dout, const float* lse, const uint8_t* kv,
-               int B, int T_, int H, float scale, float p, const uint16_t* dmask, void* dqkv, float* delta,
-               hipStream_t s) {
-  const int use = rp_dropout_thresh(p) != 0;
-  const float dsc = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const int64_t rows = (int64_t)B * T_;
-  if (phases & 1)
-    hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, (const T*)out,
-                       (const T*)dout, B, T_, H, delta);
-  const int nkb = (T_ + KV_KB - 1) / KV_KB;
-  const int nqb = (T_ + FW_QB - 1) / FW_QB;
+int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
+  const int64_t rows = (int64_t)a.B * a.Tq;
+  if (phases & 1) hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
+  const int nkb = (a.Tk + KV_KB - 1) / KV_KB;
+  const int nqb = (a.Tq + FW_QB - 1) / FW_QB;
   if (phases & 2) {
-    if (use)
-      hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true>), dim3((unsigned)(nkb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                         (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+    const dim3 grid((unsigned)(nkb * a.B * a.H));
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true>), grid, dim3(NT), 0, s, a);
     else
-      hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false>), dim3((unsigned)(nkb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                         (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+      hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false>), grid, dim3(NT), 0, s, a);
   }
   if (phases & 4) {
-    if (use)
-      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                         (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+    const dim3 grid((unsigned)(nqb * a.B * a.H));
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true>), grid, dim3(NT), 0, s, a);
     else
-      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false>), dim3((unsigned)(nqb * B * H)), dim3(NT), 0, s, (const T*)qkv,
-                         (const T*)dout, lse, delta, kv, B, T_, H, scale, use, dsc, dmask, (T*)dqkv);
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false>), grid, dim3(NT), 0, s, a);
   }
-  return rp_check_launch("rp_attn_bwd");
+  return rp_check_launch("rp_mha_bwd");
 }
 
-int attn_bwd_entry(int phases, int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
-                   const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
-                   const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
-  RP_REQUIRE(dk == HD, "rp_attn_bwd: head dim %d unsupported (64)", dk);
-  RP_REQUIRE(B >= 0 && T >= 0 && H > 0, "rp_attn_bwd: bad shape");
-  if (B == 0 || T == 0) return RP_OK;
-  RP_REQUIRE(qkv && dout && lse && key_valid && dqkv && delta_ws && (out || !(phases & 1)), "rp_attn_bwd: null pointer");
-  RP_REQUIRE(rp_aligned16(qkv) && rp_aligned16(dout) && rp_aligned16(dqkv), "rp_attn_bwd: 16-byte alignment required");
-  RP_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "rp_attn_bwd: dropout_p out of range");
-  RP_REQUIRE(rp_dropout_thresh(dropout_p) == 0 || (dropmask && rp_aligned16(dropmask)),
-             "rp_attn_bwd: dropout needs the forward's dropmask");
+int launch_mha_bwd_dtype(int dtype, int phases, const MhaDev& a, hipStream_t s) {
+  return dtype == RP_BF16 ? launch_mha_bwd<bf16>(phases, a, s) : launch_mha_bwd<float>(phases, a, s);
+}
+
+// host validation of rp_mha_args -> MhaDev; phases 0 = forward
+int make_dev(const char* fn, int dtype, const rp_mha_args* p, int phases, MhaDev& a) {
+  RP_REQUIRE(p, "%s: null args", fn);
+  RP_REQUIRE(dtype == RP_BF16 || dtype == RP_F32, "%s: bad dtype %d", fn, dtype);
+  RP_REQUIRE(p->head_dim == HD, "%s: head dim %d unsupported (64)", fn, p->head_dim);
+  RP_REQUIRE(p->B >= 0 && p->Tq >= 0 && p->Tk >= 0 && p->H > 0, "%s: bad shape", fn);
+  RP_REQUIRE(p->dropout_p >= 0.f && p->dropout_p < 1.f, "%s: dropout_p out of range", fn);
+  RP_REQUIRE((int64_t)p->Tq * p->Tk < (int64_t)UINT32_MAX, "%s: Tq*Tk too large", fn);
+  const int64_t w = (int64_t)p->H * HD;
+  RP_REQUIRE(p->ldq >= w && p->ldk >= w && p->ldv >= w && p->ldq % 8 == 0 && p->ldk % 8 == 0 && p->ldv % 8 == 0,
+             "%s: q/k/v leading dims must be >= H*dk and multiples of 8", fn);
+  RP_REQUIRE(p->q && p->k && p->v && p->key_valid && p->lse, "%s: null pointer", fn);
+  RP_REQUIRE(rp_aligned16(p->q) && rp_aligned16(p->k) && rp_aligned16(p->v), "%s: 16-byte alignment required", fn);
+  const uint32_t thr = rp_dropout_thresh(p->dropout_p);
+  RP_REQUIRE(thr == 0 || (p->dropmask && rp_aligned16(p->dropmask)), "%s: dropout needs the dropmask buffer", fn);
+  a = MhaDev{};
+  a.q = p->q; a.k = p->k; a.v = p->v; a.ldq = p->ldq; a.ldk = p->ldk; a.ldv = p->ldv;
+  a.kvalid = p->key_valid; a.B = p->B; a.Tq = p->Tq; a.Tk = p->Tk; a.H = p->H; a.scale = p->scale;
+  a.drop_thresh = thr; a.drop_scale = p->dropout_p > 0.f ? 1.f / (1.f - p->dropout_p) : 1.f; a.seed = p->seed;
+  a.out = p->out; a.ldo = p->ldo; a.lse = p->lse; a.dmask = thr ? p->dropmask : nullptr;
+  a.dout = p->dout; a.lddo = p->lddo; a.delta = p->delta_ws;
+  a.dq = p->dq; a.lddq = p->lddq; a.dk = p->dk; a.lddk = p->lddk; a.dv = p->dv; a.lddv = p->lddv;
+  if (phases == 0 || (phases & 1)) {
+    RP_REQUIRE(p->out && p->ldo >= w && p->ldo % 8 == 0 && rp_aligned16(p->out), "%s: bad out / ldo", fn);
+  }
+  if (phases) {
+    RP_REQUIRE(p->dout && p->lddo >= w && p->lddo % 8 == 0 && rp_aligned16(p->dout), "%s: bad dout / lddo", fn);
+    RP_REQUIRE(p->delta_ws, "%s: null delta workspace", fn);
+  }
+  if (phases & 2) {
+    RP_REQUIRE(p->dk && p->dv && p->lddk >= w && p->lddv >= w && rp_aligned16(p->dk) && rp_aligned16(p->dv),
+               "%s: bad dk / dv", fn);
+  }
+  if (phases & 4) RP_REQUIRE(p->dq && p->lddq >= w && rp_aligned16(p->dq), "%s: bad dq", fn);
+  return RP_OK;
+}
+
+int mha_fwd_entry(int dtype, const rp_mha_args* p, void* stream) {
+  MhaDev a;
+  const int rc = make_dev("rp_mha_fwd", dtype, p, 0, a);
+  if (rc) return rc;
+  if (a.B == 0 || a.Tq == 0) return RP_OK;
+  RP_REQUIRE(a.Tk > 0, "rp_mha_fwd: no keys");
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == RP_BF16)
-    return launch_bwd<bf16>(phases, qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p, dropmask, dqkv,
-                            delta_ws, s);
-  if (dtype == RP_F32)
-    return launch_bwd<float>(phases, qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p, dropmask, dqkv,
-                             delta_ws, s);
-  rp_set_error("rp_attn_bwd: bad dtype");
-  return RP_ERR_ARG;
+  return dtype == RP_BF16 ? launch_mha_fwd<bf16>(a, s) : launch_mha_fwd<float>(a, s);
+}
+
+int mha_bwd_entry(int dtype, const rp_mha_args* p, int phases, void* stream) {
+  RP_REQUIRE(phases >= 1 && phases <= 7, "rp_mha_bwd: phases must be in 1..7");
+  MhaDev a;
+  const int rc = make_dev("rp_mha_bwd", dtype, p, phases, a);
+  if (rc) return rc;
+  if (a.B == 0 || a.Tq == 0 || a.Tk == 0) return RP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == RP_BF16 ? launch_mha_bwd<bf16>(phases, a, s) : launch_mha_bwd<float>(phases, a, s);
+}
+
+// packed self-attention (qkv [B*T, 3*H*dk]) -> general description
+rp_mha_args packed(const void* qkv, const uint8_t* kv, int B, int T, int H, int dk, float scale, float p, uint32_t seed,
+                   const void* out, float* lse, const uint16_t* dmask, const void* dout, void* dqkv, float* delta) {
+  rp_mha_args a{};
+  const int64_t ld = 3LL * H * dk, lo = (int64_t)H * dk;
+  a.q = qkv; a.k = qkv; a.v = qkv; a.ldq = a.ldk = a.ldv = ld;
+  a.key_valid = kv; a.B = B; a.Tq = T; a.Tk = T; a.H = H; a.head_dim = dk; a.scale = scale; a.dropout_p = p; a.seed = seed;
+  a.out = const_cast<void*>(out); a.ldo = lo; a.lse = lse; a.dropmask = const_cast<uint16_t*>(dmask);
+  a.dout = dout; a.lddo = lo; a.delta_ws = delta;
+  a.dq = dqkv; a.dk = dqkv; a.dv = dqkv; a.lddq = a.lddk = a.lddv = ld;
+  return a;
+}
+// byte offsets of the K and V column blocks of a packed row
+void packed_offsets(rp_mha_args& a, int dtype) {
+  const int64_t es = dtype == RP_BF16 ? 2 : 4;
+  const int64_t off = (int64_t)a.H * a.head_dim * es;
+  a.k = (const char*)a.q + off;
+  a.v = (const char*)a.q + 2 * off;
+  if (a.dq) {
+    a.dk = (char*)a.dq + off;
+    a.dv = (char*)a.dq + 2 * off;
+  }
 }
 
 }  // namespace
 
-extern "C" int64_t rp_attn_dropmask_elems(int B, int T, int H) {
-  if (B <= 0 || T <= 0 || H <= 0) return 0;
-  return (int64_t)B * H * mask_kt(T) * 4 * mask_ld(T);
+extern "C" int64_t rp_attn_dropmask_elems(int B, int T, int H) { return rp_mha_dropmask_elems(B, T, T, H); }
+
+extern "C" int64_t rp_mha_dropmask_elems(int B, int Tq, int Tk, int H) {
+  if (B <= 0 || Tq <= 0 || Tk <= 0 || H <= 0) return 0;
+  return (int64_t)B * H * mask_kt(Tk) * 4 * mask_ld(Tq);
+}
+
+extern "C" int rp_mha_fwd(int dtype, const rp_mha_args* args, void* stream) { return mha_fwd_entry(dtype, args, stream); }
+
+extern "C" int rp_mha_bwd(int dtype, const rp_mha_args* args, int phases, void* stream) {
+  return mha_bwd_entry(dtype, args, phases, stream);
 }
 
 extern "C" int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
                            float dropout_p, uint32_t seed, void* out, float* lse, uint16_t* dropmask, void* stream) {
   RP_REQUIRE(dk == HD, "rp_attn_fwd: head dim %d unsupported (64)", dk);
-  RP_REQUIRE(B >= 0 && T >= 0 && H > 0, "rp_attn_fwd: bad shape");
-  if (B == 0 || T == 0) return RP_OK;
-  RP_REQUIRE(qkv && key_valid && out && lse, "rp_attn_fwd: null pointer");
-  RP_REQUIRE(rp_aligned16(qkv) && rp_aligned16(out), "rp_attn_fwd: 16-byte alignment required");
-  RP_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "rp_attn_fwd: dropout_p out of range");
-  RP_REQUIRE((int64_t)T * T < (int64_t)UINT32_MAX, "rp_attn_fwd: T too large");
-  RP_REQUIRE(rp_dropout_thresh(dropout_p) == 0 || (dropmask && rp_aligned16(dropmask)),
-             "rp_attn_fwd: dropout needs a 16-byte aligned dropmask buffer (rp_attn_dropmask_elems)");
-  hipStream_t s = (hipStream_t)stream;
-  if (dtype == RP_BF16) return launch_fwd<bf16>(qkv, key_valid, B, T, H, scale, dropout_p, seed, out, lse, dropmask, s);
-  if (dtype == RP_F32) return launch_fwd<float>(qkv, key_valid, B, T, H, scale, dropout_p, seed, out, lse, dropmask, s);
-  rp_set_error("rp_attn_fwd: bad dtype");
-  return RP_ERR_ARG;
+  RP_REQUIRE(qkv, "rp_attn_fwd: null qkv");
+  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, seed, out, lse, dropmask, nullptr, nullptr,
+                         nullptr);
+  packed_offsets(a, dtype);
+  return mha_fwd_entry(dtype, &a, stream);
+}
+
+static int attn_bwd_packed(int phases, int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
+                           const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
+                           const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
+  RP_REQUIRE(dk == HD, "rp_attn_bwd: head dim %d unsupported (64)", dk);
+  RP_REQUIRE(qkv && dqkv, "rp_attn_bwd: null qkv / dqkv");
+  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, 0, out, const_cast<float*>(lse), dropmask, dout,
+                         dqkv, delta_ws);
+  packed_offsets(a, dtype);
+  return mha_bwd_entry(dtype, &a, phases, stream);
 }
 
 extern "C" int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
                            const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                            const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
-  return attn_bwd_entry(7, dtype, qkv, out, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
-                        delta_ws, stream);
+  return attn_bwd_packed(7, dtype, qkv, out, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
+                         delta_ws, stream);
 }
 
 extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, int B, int T, int H, int dk,
@@ -1035,31 +1117,23 @@ extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, i
   RP_REQUIRE(B >= 0 && T >= 0 && H > 0, "rp_attn_bwd_delta: bad shape");
   if (B == 0 || T == 0) return RP_OK;
   RP_REQUIRE(out && dout && delta_ws, "rp_attn_bwd_delta: null pointer");
-  hipStream_t s = (hipStream_t)stream;
-  const int64_t rows = (int64_t)B * T;
-  if (dtype == RP_BF16)
-    hipLaunchKernelGGL(attn_delta_kernel<bf16>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, (const bf16*)out,
-                       (const bf16*)dout, B, T, H, delta_ws);
-  else if (dtype == RP_F32)
-    hipLaunchKernelGGL(attn_delta_kernel<float>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, (const float*)out,
-                       (const float*)dout, B, T, H, delta_ws);
-  else {
-    rp_set_error("rp_attn_bwd_delta: bad dtype");
-    return RP_ERR_ARG;
-  }
-  return rp_check_launch("rp_attn_bwd_delta");
+  RP_REQUIRE(dtype == RP_BF16 || dtype == RP_F32, "rp_attn_bwd_delta: bad dtype");
+  MhaDev a{};
+  a.B = B; a.Tq = T; a.Tk = T; a.H = H; a.out = const_cast<void*>(out); a.ldo = (int64_t)H * HD; a.dout = dout;
+  a.lddo = (int64_t)H * HD; a.delta = delta_ws;
+  return launch_mha_bwd_dtype(dtype, 1, a, (hipStream_t)stream);
 }
 
 extern "C" int rp_attn_bwd_dkdv(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
                                 const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                                 const uint16_t* dropmask, void* dqkv, void* stream) {
-  return attn_bwd_entry(2, dtype, qkv, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
-                        (float*)delta_ws, stream);
+  return attn_bwd_packed(2, dtype, qkv, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
+                         const_cast<float*>(delta_ws), stream);
 }
 
 extern "C" int rp_attn_bwd_dq(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
                               const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                               const uint16_t* dropmask, void* dqkv, void* stream) {
-  return attn_bwd_entry(4, dtype, qkv, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
-                        (float*)delta_ws, stream);
+  return attn_bwd_packed(4, dtype, qkv, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
+                         const_cast<float*>(delta_ws), stream);
 }

@@ -244,6 +244,70 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
     return dqkv
 
 
+def _rows(t, H, dk):
+    """(data pointer, row stride) of a [rows, >= H*dk] activation view with unit column stride."""
+    if t.dim() != 2 or t.stride(1) != 1 or t.shape[1] < H * dk:
+        raise ValueError("mha: operands are [rows, H*dk] views with unit column stride")
+    return t.data_ptr(), t.stride(0)
+
+
+def mha_fwd(q, k, v, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, seed=0):
+    """General (self / cross) attention core.  q [B*Tq, >=H*dk], k/v [B*Tk, >=H*dk] row views (any row
+    stride), key_valid [B, Tk] uint8.  -> (out [B*Tq, H*dk], lse [B, H, Tq], dropmask or None)."""
+    _gpu(q, k, v, key_valid)
+    _contig(key_valid)
+    if not (q.dtype == k.dtype == v.dtype):
+        raise TypeError("mha_fwd: q, k, v must share a dtype")
+    dk = 64
+    out = torch.empty(B * Tq, H * dk, device=q.device, dtype=q.dtype)
+    lse = torch.empty(B, H, Tq, device=q.device, dtype=torch.float32)
+    mask = None
+    if dropout_p > 0:
+        mask = torch.empty(N.load().rp_mha_dropmask_elems(B, Tq, Tk, H), device=q.device, dtype=torch.int16)
+    a = N.MhaArgs()
+    a.q, a.ldq = _rows(q, H, dk)
+    a.k, a.ldk = _rows(k, H, dk)
+    a.v, a.ldv = _rows(v, H, dk)
+    a.key_valid = key_valid.data_ptr()
+    a.B, a.Tq, a.Tk, a.H, a.head_dim = B, Tq, Tk, H, dk
+    a.scale, a.dropout_p, a.seed = float(scale), float(dropout_p), int(seed) & 0xFFFFFFFF
+    a.out, a.ldo = out.data_ptr(), out.stride(0)
+    a.lse = lse.data_ptr()
+    a.dropmask = mask.data_ptr() if mask is not None else None
+    N.call("rp_mha_fwd", _dt(q), ctypes.byref(a), _stream(q))
+    return out, lse, mask
+
+
+def mha_bwd(q, k, v, out, dout, lse, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, dropmask=None):
+    """-> (dq [B*Tq, H*dk], dk [B*Tk, H*dk], dv [B*Tk, H*dk]) for mha_fwd's inputs."""
+    _gpu(q, k, v, out, dout, lse, key_valid, dropmask)
+    _contig(out, dout, lse, key_valid)
+    if dropout_p > 0 and dropmask is None:
+        raise ValueError("mha_bwd: dropout needs the forward's dropmask")
+    dk = 64
+    dq = torch.empty(B * Tq, H * dk, device=q.device, dtype=q.dtype)
+    dkk = torch.empty(B * Tk, H * dk, device=q.device, dtype=q.dtype)
+    dv = torch.empty(B * Tk, H * dk, device=q.device, dtype=q.dtype)
+    delta = torch.empty(B, H, Tq, device=q.device, dtype=torch.float32)
+    a = N.MhaArgs()
+    a.q, a.ldq = _rows(q, H, dk)
+    a.k, a.ldk = _rows(k, H, dk)
+    a.v, a.ldv = _rows(v, H, dk)
+    a.key_valid = key_valid.data_ptr()
+    a.B, a.Tq, a.Tk, a.H, a.head_dim = B, Tq, Tk, H, dk
+    a.scale, a.dropout_p = float(scale), float(dropout_p)
+    a.out, a.ldo = out.data_ptr(), out.stride(0)
+    a.lse = lse.data_ptr()
+    a.dropmask = dropmask.data_ptr() if dropmask is not None else None
+    a.dout, a.lddo = dout.data_ptr(), dout.stride(0)
+    a.dq, a.lddq = dq.data_ptr(), dq.stride(0)
+    a.dk, a.lddk = dkk.data_ptr(), dkk.stride(0)
+    a.dv, a.lddv = dv.data_ptr(), dv.stride(0)
+    a.delta_ws = delta.data_ptr()
+    N.call("rp_mha_bwd", _dt(q), ctypes.byref(a), 7, _stream(q))
+    return dq, dkk, dv
+
+
 # ------------------------------------------------------------------------------------- focal loss
 def focal_fwd_sum(x, t, mask=None, alpha=0.7, gamma=2.0):
     _gpu(x, t, mask)

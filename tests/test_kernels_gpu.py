@@ -225,6 +225,44 @@ def test_attention_fwd_bwd(dev, dtype, T, p):
     close(dqkv, gref, atol=btol, rtol=btol, what="attn bwd")
 
 
+def mha_ref(q, k, v, kv, B, Tq, Tk, H, scale):
+    """torch restatement of the general attention core (fp64): softmax(scale*QK^T + key mask) V."""
+    dk = 64
+    qh = q[:, :H * dk].reshape(B, Tq, H, dk).permute(0, 2, 1, 3)
+    kh = k[:, :H * dk].reshape(B, Tk, H, dk).permute(0, 2, 1, 3)
+    vh = v[:, :H * dk].reshape(B, Tk, H, dk).permute(0, 2, 1, 3)
+    s = (qh @ kh.transpose(-1, -2)) * scale
+    s = s.masked_fill(~kv.bool().view(B, 1, 1, Tk), float("-inf"))
+    o = torch.softmax(s, -1) @ vh
+    return o.permute(0, 2, 1, 3).reshape(B * Tq, H * dk)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Tq,Tk", [(100, 37), (64, 256), (130, 129)])
+def test_mha_cross_strided(dev, dtype, Tq, Tk):
+    """Cross attention (Tq != Tk) on strided row views (q from a wider buffer, k/v interleaved
+    columns of one [B*Tk, 2*H*dk] buffer), key padding on the context."""
+    B, H, dk = 2, 4, 64
+    qbuf = rnd(B * Tq, H * dk + 64, dev=dev, seed=Tq).to(dtype)
+    kvbuf = rnd(B * Tk, 2 * H * dk, dev=dev, seed=Tk + 7).to(dtype)
+    q, k, v = qbuf[:, 32:32 + H * dk], kvbuf[:, :H * dk], kvbuf[:, H * dk:]
+    lens = torch.tensor([Tk, max(1, Tk // 3)], device=dev)
+    kv = (torch.arange(Tk, device=dev)[None] < lens[:, None]).to(torch.uint8)
+    scale = 0.125
+    o, lse, _ = K.mha_fwd(q, k, v, kv, B, Tq, Tk, H, scale)
+    qd, kd, vd = (t.double().requires_grad_(True) for t in (q, k, v))
+    ref = mha_ref(qd, kd, vd, kv, B, Tq, Tk, H, scale)
+    ftol = 2e-5 if dtype == torch.float32 else 2e-2
+    close(o, ref.detach(), atol=ftol, rtol=ftol, what="mha fwd")
+    do = rnd(B * Tq, H * dk, dev=dev, seed=Tq + Tk).to(dtype)
+    dq, dkk, dv = K.mha_bwd(q, k, v, o, do, lse, kv, B, Tq, Tk, H, scale)
+    gq, gk, gv = torch.autograd.grad(ref, (qd, kd, vd), do.double())
+    btol = 1e-4 if dtype == torch.float32 else 6e-2
+    close(dq, gq, atol=btol, rtol=btol, what="mha dq")
+    close(dkk, gk, atol=btol, rtol=btol, what="mha dk")
+    close(dv, gv, atol=btol, rtol=btol, what="mha dv")
+
+
 def test_attention_lse(dev):
     B, H, T = 1, 8, 96
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=3)
