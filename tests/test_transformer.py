@@ -1,0 +1,105 @@
+"""repurpose_amd.transformer (drop-in for models/transformer.py) against the CPU restatement in
+oracle/transformer_oracle.py: structure on CPU; forward and gradients on the GPU (fp32)."""
+import pytest
+import torch
+
+from oracle import transformer_oracle as O
+from repurpose_amd import transformer as R
+
+D, H, DFF = 128, 2, 256  # head dim 64, as the kernels implement
+
+CASES = {
+    "MultiHeadAttention": lambda m: m.MultiHeadAttention(D, H),
+    "MLP": lambda m: m.MLP(96, DFF, D),
+    "EncoderLayer": lambda m: m.EncoderLayer(D, H, DFF),
+    "CrossAttentionEncoderLayer": lambda m: m.CrossAttentionEncoderLayer(D, H, DFF),
+    "CrossSelfEncoderLayer": lambda m: m.CrossSelfEncoderLayer(D, H, DFF),
+    "UniModalEncoder": lambda m: m.UniModalEncoder(96, D, 2, H, DFF),
+}
+
+
+def build(name, seed=0):
+    torch.manual_seed(seed)
+    ref = CASES[name](O)
+    torch.manual_seed(seed)
+    ours = CASES[name](R)
+    return ref, ours
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_state_dict_and_init_match(name):
+    ref, ours = build(name)
+    a, b = ref.state_dict(), ours.state_dict()
+    assert list(a) == list(b)
+    for k in a:
+        assert a[k].shape == b[k].shape, k
+        assert torch.equal(a[k], b[k]), k  # same construction order -> same seeded init
+
+
+def test_positional_encoding_keeps_batch_index_quirk():
+    pe = R.PositionalEncoding(16, max_len=50)
+    x = torch.zeros(3, 7, 16)
+    y = pe(x)
+    for b in range(3):  # sample b gets pe[b] at every timestep (seq-first table on batch-first input)
+        assert torch.equal(y[b], pe.pe[b].expand(7, 16))
+
+
+def _inputs(name, dev, B=2, T=70, Tc=45):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, T, 96 if name in ("MLP", "UniModalEncoder") else D, generator=g)
+    ctx = torch.randn(B, T if name == "CrossSelfEncoderLayer" else Tc, D, generator=g)
+    lens = torch.tensor([T, T - 23])
+    mask = (torch.arange(T)[None] < lens[:, None]).unsqueeze(1)          # [B, 1, T]
+    clens = torch.tensor([ctx.shape[1], ctx.shape[1] - 11])
+    cmask = (torch.arange(ctx.shape[1])[None] < clens[:, None]).unsqueeze(1)
+    return x, ctx, mask, cmask
+
+
+def _call(name, m, x, ctx, mask, cmask):
+    if name == "MultiHeadAttention":
+        return m(x, ctx, ctx * 0.5 + 1.0, cmask)  # distinct q, k, v sources
+    if name == "MLP":
+        return m(x)
+    if name == "EncoderLayer":
+        return m(x, mask)
+    if name == "CrossAttentionEncoderLayer":
+        return m(x, ctx, cmask)
+    if name == "CrossSelfEncoderLayer":
+        return m(x, ctx, mask)
+    return m(x, mask)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(CASES))
+def test_forward_backward_parity(dev, name):
+    ref, ours = build(name)
+    ours = ours.to(dev)
+    x, ctx, mask, cmask = _inputs(name, dev)
+    xr, cr = x.clone().requires_grad_(True), ctx.clone().requires_grad_(True)
+    yr = _call(name, ref, xr, cr, mask, cmask)
+    xo, co = x.to(dev).requires_grad_(True), ctx.to(dev).requires_grad_(True)
+    yo = _call(name, ours, xo, co, mask.to(dev), cmask.to(dev))
+    err = (yo.detach().cpu() - yr.detach()).abs().max().item()
+    assert err < 1e-3 * max(1.0, yr.abs().max().item()), f"{name} forward max|err| {err:.3e}"
+    w = torch.randn(yr.shape, generator=torch.Generator().manual_seed(9))
+    (yr * w).sum().backward()
+    (yo * w.to(dev)).sum().backward()
+    pairs = [("x", xr.grad, xo.grad)]
+    if name in ("MultiHeadAttention", "CrossAttentionEncoderLayer", "CrossSelfEncoderLayer"):
+        pairs.append(("context", cr.grad, co.grad))
+    pairs += [(n, p.grad, q.grad) for (n, p), q in zip(ref.named_parameters(), ours.parameters())]
+    # denominators floored at 1% of the largest reference gradient: some gradients are exactly zero in
+    # exact arithmetic (e.g. the key-projection bias: softmax is shift-invariant) and only rounding noise
+    gmax = max(a.abs().max().item() for _, a, _ in pairs)
+    for n, a, b in pairs:
+        assert b is not None, n
+        rel = (b.cpu() - a).abs().max().item() / max(a.abs().max().item(), 1e-2 * gmax)
+        assert rel < 2e-3, f"{name} grad {n}: rel err {rel:.3e}"
+
+
+@pytest.mark.gpu
+def test_per_query_mask_rejected(dev):
+    m = R.MultiHeadAttention(D, H).to(dev)
+    x = torch.randn(2, 8, D, device=dev)
+    with pytest.raises(NotImplementedError):
+        m(x, x, x, torch.ones(2, 8, 8, device=dev))
