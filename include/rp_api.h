@@ -23,6 +23,9 @@
  *   rp_adam_step          torch.optim.Adam(lr, weight_decay) step  main.py:190-191,369
  *   rp_infer_select       inference_single_video                 models/MMCTransformer.py:181-229
  *   rp_softnms            soft_nms_intervals_cpu                 models/softnms.py:3-38
+ *   rp_mha_fwd/bwd        models/transformer.py:37-81 MultiHeadAttention core (self / cross)
+ *   rp_tiou_hits          calculate_tiou (batched)               utils/metrics.py:82-111
+ *   rp_diou_fwd/bwd       ctr_diou_loss_1d                       models/losses.py:56-116
  *   (gradient all-reduce over RCCL is issued by the host layer through torch.distributed,
  *    replacing utils/distributed.py:396-433 DDP; no collective lives in this library)
  */
@@ -285,6 +288,23 @@ int rp_infer_select(const float* logits, const uint8_t* mask, const float* offse
 int rp_softnms(const float* scores, const float* segs, const int* count, int B, int cap,
                float sigma, float thresh, const int* max_seg, int* keep, int* keep_count,
                float* final_scores, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Evaluation metric (utils/metrics.py:82-111 calculate_tiou, batched): pred [V][P][2] fp32 segments
+ * (start, end), pred_count[V] valid rows; ref [V][R][2] fp64 reference segments, ref_count[V];
+ * thresholds[n_thr] (1..32).  hits[V][n_thr] = number of predictions whose best IoU over the
+ * video's references (0 when it has none) is >= the threshold; IoU in double exactly as the
+ * reference's Python floats.  precision = hits / pred_count (0 if pred_count == 0). */
+int rp_tiou_hits(const float* pred, const int* pred_count, int P, const double* ref, const int* ref_count, int R,
+                 const double* thresholds, int n_thr, int V, int* hits, void* stream);
+
+/* 1-D distance-IoU loss (models/losses.py:56-116 ctr_diou_loss_1d) on n (left, right) offset pairs.
+ * reduction 0: out[n] per element; 1: *out = mean; 2: *out = sum (single deterministic pass).
+ * Backward: dpred / dgt (either may be NULL) = grad_scale * grad_out (per element if per_elem, else
+ * the device scalar grad_out[0]) * d loss / d offsets (torch's tie / clamp subgradients). */
+int rp_diou_fwd(const float* pred, const float* gt, int64_t n, float eps, int reduction, float* out, void* stream);
+int rp_diou_bwd(const float* pred, const float* gt, int64_t n, float eps, const float* grad_out, int per_elem,
+                float grad_scale, float* dpred, float* dgt, void* stream);
 
 #ifdef __cplusplus
 }

@@ -75,6 +75,9 @@ _SIGNATURES = {
     "rp_mha_dropmask_elems": (c_i64, [c_i, c_i, c_i, c_i]),
     "rp_mha_fwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_vp]),
     "rp_mha_bwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_i, c_vp]),
+    "rp_tiou_hits": (c_i, [c_vp, c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_i, c_i, c_vp, c_vp]),
+    "rp_diou_fwd": (c_i, [c_vp, c_vp, c_i64, c_f, c_i, c_vp, c_vp]),
+    "rp_diou_bwd": (c_i, [c_vp, c_vp, c_i64, c_f, c_vp, c_i, c_f, c_vp, c_vp, c_vp]),
     "rp_focal_fwd_sum": (c_i, [c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_vp]),
     "rp_focal_elementwise": (c_i, [c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_vp]),
     "rp_focal_bwd": (c_i, [c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_i, c_vp, c_vp]),

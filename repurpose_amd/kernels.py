@@ -399,3 +399,37 @@ def softnms(scores, segs, count, sigma, thresh, max_seg, want_final_scores=False
     N.call("rp_softnms", _p(scores), _p(segs), _p(count), B, cap, float(sigma), float(thresh), _p(max_seg),
            _p(keep), _p(keep_count), _p(final), _stream(scores))
     return keep, keep_count, final
+
+
+# ------------------------------------------------------------------------------------- metric, DIoU
+def tiou_hits(pred, pred_count, ref, ref_count, thresholds):
+    """pred [V, P, 2] fp32, ref [V, R, 2] fp64, counts [V] int32, thresholds fp64 [n] -> hits [V, n] int32."""
+    _gpu(pred, pred_count, ref, ref_count, thresholds)
+    _contig(pred, pred_count, ref, ref_count, thresholds)
+    V, P = pred.shape[0], pred.shape[1]
+    R = ref.shape[1]
+    hits = torch.empty(V, thresholds.numel(), device=pred.device, dtype=torch.int32)
+    N.call("rp_tiou_hits", _p(pred), _p(pred_count), P, _p(ref), _p(ref_count), R, _p(thresholds),
+           thresholds.numel(), V, _p(hits), _stream(pred))
+    return hits
+
+
+def diou_fwd(pred, gt, eps, reduction):
+    """pred, gt [n, 2] fp32 contiguous; reduction 0 none / 1 mean / 2 sum."""
+    _gpu(pred, gt)
+    _contig(pred, gt)
+    n = pred.shape[0]
+    out = torch.empty(n if reduction == 0 else (), device=pred.device, dtype=torch.float32)
+    N.call("rp_diou_fwd", _p(pred), _p(gt), n, float(eps), int(reduction), _p(out), _stream(pred))
+    return out
+
+
+def diou_bwd(pred, gt, eps, grad_out, per_elem, grad_scale, want_pred=True, want_gt=False):
+    _gpu(pred, gt, grad_out)
+    _contig(pred, gt, grad_out)
+    n = pred.shape[0]
+    dp = torch.empty_like(pred) if want_pred else None
+    dg = torch.empty_like(gt) if want_gt else None
+    N.call("rp_diou_bwd", _p(pred), _p(gt), n, float(eps), _p(grad_out), int(per_elem), float(grad_scale),
+           _p(dp), _p(dg), _stream(pred))
+    return dp, dg

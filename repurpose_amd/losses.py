@@ -6,8 +6,8 @@
   ``MMCTransformer.losses`` (reference ``models/MMCTransformer.py:159-179``): one kernel computes
   ``sum(mask * focal)`` with a deterministic single-block reduction; the backward kernel writes
   ``dL/dlogit`` directly (no [B,T,1] intermediate).
-* ``ctr_diou_loss_1d`` — reference ``:56-116``; never called by the reference trainer,
-  kept for API completeness on torch tensor ops (rank-4 "next" item in SURVEY §8f).
+* ``ctr_diou_loss_1d`` — reference ``:56-116``; never called by the reference trainer (SURVEY §0.2);
+  fused forward / backward kernels rp_diou_fwd / rp_diou_bwd.
 """
 import torch
 
@@ -79,22 +79,38 @@ def sigmoid_focal_loss(inputs, targets, alpha: float = 0.7, gamma: float = 2.0, 
     raise ValueError(f"invalid reduction {reduction!r}")
 
 
+class _CtrDiou(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, g, reduction, eps):
+        shape = a.shape
+        a2, g2 = a.reshape(-1, 2).contiguous(), g.reshape(-1, 2).contiguous()
+        red = {"none": 0, "mean": 1, "sum": 2}[reduction]
+        out = K.diou_fwd(a2, g2, eps, red)
+        ctx.save_for_backward(a2, g2)
+        ctx.red, ctx.eps, ctx.shape = red, eps, shape
+        return out.view(shape[:-1]) if red == 0 else out
+
+    @staticmethod
+    def backward(ctx, gout):
+        a2, g2 = ctx.saved_tensors
+        n = a2.shape[0]
+        per_elem = ctx.red == 0
+        scale = (1.0 / n if n > 0 else 0.0) if ctx.red == 1 else 1.0
+        go = gout.contiguous().float().reshape(-1) if per_elem else gout.float().reshape(1)
+        dp, dg = K.diou_bwd(a2, g2, ctx.eps, go, per_elem, scale, want_pred=ctx.needs_input_grad[0],
+                            want_gt=ctx.needs_input_grad[1])
+        return (dp.view(ctx.shape) if dp is not None else None,
+                dg.view(ctx.shape) if dg is not None else None, None, None)
+
+
 def ctr_diou_loss_1d(input_offsets, target_offsets, reduction: str = "none", eps: float = 1e-8):
-    """Reference ``models/losses.py:56-116`` (1-D distance-IoU on [B, T, 2] offsets)."""
+    """Reference ``models/losses.py:56-116`` (1-D distance-IoU on [..., 2] (left, right) offsets),
+    forward and backward in the HIP kernels rp_diou_fwd / rp_diou_bwd.  Like the reference it asserts
+    non-negative offsets (a device-to-host check)."""
     a = input_offsets.float()
     g = target_offsets.float()
     assert (a >= 0.0).all(), "predicted offsets must be non-negative"
     assert (g >= 0.0).all(), "GT offsets must be non-negative"
-    lp, rp = a[:, :, 0], a[:, :, 1]
-    lg, rg = g[:, :, 0], g[:, :, 1]
-    inter = torch.min(lp, lg) + torch.min(rp, rg)
-    union = (lp + rp) + (lg + rg) - inter
-    iou = inter / union.clamp(min=eps)
-    enclose = torch.max(lp, lg) + torch.max(rp, rg)
-    rho = 0.5 * (rp - lp - rg + lg)
-    loss = 1.0 - iou + torch.square(rho / enclose.clamp(min=eps))
-    if reduction == "mean":
-        return loss.mean() if loss.numel() > 0 else 0.0 * loss.sum()
-    if reduction == "sum":
-        return loss.sum()
-    return loss
+    if reduction not in ("none", "mean", "sum"):
+        raise ValueError(f"ctr_diou_loss_1d: unknown reduction {reduction!r}")
+    return _CtrDiou.apply(a, g, reduction, float(eps))

@@ -1,11 +1,20 @@
-"""Evaluation metric of the trainer (reference ``utils/metrics.py``), host side.
+"""Evaluation metric of the trainer (reference ``utils/metrics.py``).
 
 ``calculate_tiou`` (``:82-111``) is the "AtIoU" the trainer reports (``main.py:685-703``):
 precision of predicted segments at each tIoU threshold, averaged over thresholds and videos.
+The per-video host function keeps the reference's signature; ``evaluate_tiou`` scores a whole
+batch of videos in one HIP launch (rp_tiou_hits, IoU in double like the reference's Python floats)
+and, under torch.distributed, gathers every rank's per-video precisions so the full split is
+scored (the reference scores only rank 0's shard).
 ``calculate_ap`` / ``calculate_recall`` (``:1-80``) are unused by the reference trainer and are
-restated for API completeness.  These are O(#pred x #gt) per video on tens of segments — host
-work, off the hot path (SURVEY §8f rank 3 lists a GPU version as a later item).
+restated for API completeness.
 """
+import torch
+import torch.distributed as dist
+
+from . import kernels as K
+
+THRESHOLDS = (0.5, 0.6, 0.7, 0.8, 0.9)  # main.py:685
 
 
 def _seg_iou(a, b):
@@ -52,3 +61,51 @@ def calculate_recall(segments, labels):
     if pos == 0:
         return 0.0
     return sum(1 for p, l in zip(pred, labels) if p == 1 and l == 1) / pos
+
+
+def tiou_precision_batched(gt_segments, pred_segments, tiou_thresholds=THRESHOLDS, device=None):
+    """Per-video calculate_tiou for a batch on the GPU.
+
+    gt_segments: list (videos) of lists of (start, end); pred_segments: list of [P_v, 2] tensors or
+    lists.  Returns a float64 tensor [V, n_thresholds] of precisions (0 for a video with no
+    predictions), equal to calculate_tiou(gt, pred, thresholds)[th] for every video and threshold."""
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    V = len(gt_segments)
+    preds = [torch.as_tensor(p, dtype=torch.float32).reshape(-1, 2) for p in pred_segments]
+    P = max([p.shape[0] for p in preds] + [1])
+    R = max([len(g) for g in gt_segments] + [1])
+    pred = torch.zeros(V, P, 2, dtype=torch.float32)
+    ref = torch.zeros(V, R, 2, dtype=torch.float64)
+    npred = torch.tensor([p.shape[0] for p in preds], dtype=torch.int32)
+    nref = torch.tensor([len(g) for g in gt_segments], dtype=torch.int32)
+    for v in range(V):
+        if preds[v].shape[0]:
+            pred[v, :preds[v].shape[0]] = preds[v].cpu()
+        if len(gt_segments[v]):
+            ref[v, :len(gt_segments[v])] = torch.as_tensor(gt_segments[v], dtype=torch.float64).reshape(-1, 2)
+    thr = torch.tensor(list(tiou_thresholds), dtype=torch.float64)
+    hits = K.tiou_hits(pred.to(dev), npred.to(dev), ref.to(dev), nref.to(dev), thr.to(dev)).double()
+    n = npred.to(dev).double().unsqueeze(1)
+    return torch.where(n > 0, hits / n.clamp(min=1), torch.zeros_like(hits))
+
+
+def evaluate_tiou(gt_segments, pred_segments, tiou_thresholds=THRESHOLDS, gather=True):
+    """main.py:685-703 aggregation: tIoU[th] = mean over videos, AtIoU = mean over thresholds.
+    With torch.distributed initialised (and gather=True) the per-video precisions of all ranks are
+    gathered first.  Returns (tIoU dict, AtIoU, number of videos scored)."""
+    prec = tiou_precision_batched(gt_segments, pred_segments, tiou_thresholds)
+    if gather and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        n = torch.tensor([prec.shape[0]], device=prec.device, dtype=torch.int64)
+        sizes = [torch.zeros_like(n) for _ in range(dist.get_world_size())]
+        dist.all_gather(sizes, n)
+        cap = int(max(s.item() for s in sizes))
+        pad = torch.zeros(cap, prec.shape[1], device=prec.device, dtype=prec.dtype)
+        pad[:prec.shape[0]] = prec
+        parts = [torch.zeros_like(pad) for _ in sizes]
+        dist.all_gather(parts, pad)
+        prec = torch.cat([p[:int(s.item())] for p, s in zip(parts, sizes)], 0)
+    if prec.shape[0] == 0:
+        raise ZeroDivisionError("evaluate_tiou: no videos (the reference divides by len(total_tIoU))")
+    mean = prec.mean(0).cpu().tolist()
+    tiou = {th: m for th, m in zip(tiou_thresholds, mean)}
+    return tiou, sum(tiou.values()) / len(tiou), prec.shape[0]
