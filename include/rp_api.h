@@ -25,6 +25,7 @@
  *   rp_softnms            soft_nms_intervals_cpu                 models/softnms.py:3-38
  *   rp_mha_fwd/bwd        models/transformer.py:37-81 MultiHeadAttention core (self / cross)
  *   rp_tiou_hits          calculate_tiou (batched)               utils/metrics.py:82-111
+ *   rp_pad_rows           collate_fn / preprocessing padding     dataset/RepurposeClip.py:449-533
  *   rp_diou_fwd/bwd       ctr_diou_loss_1d                       models/losses.py:56-116
  *   (gradient all-reduce over RCCL is issued by the host layer through torch.distributed,
  *    replacing utils/distributed.py:396-433 DDP; no collective lives in this library)
@@ -45,7 +46,7 @@ extern "C" {
  *   w((idx & 7) >> 1) as int16 and is kept iff they are >= round(p*65536) - 32768;
  *   kept values are scaled by 1/(1-p).  rp_hash: repurpose_amd/csrc/rp_common.h. */
 enum { RP_OK = 0, RP_ERR_ARG = 1, RP_ERR_LAUNCH = 2 };
-enum { RP_F32 = 0, RP_BF16 = 1 };
+enum { RP_F32 = 0, RP_BF16 = 1, RP_F16 = 2, RP_F64 = 3, RP_I64 = 4 };  /* F16/F64/I64: rp_pad_rows sources */
 
 int rp_version(void);
 /* Copies the last error message of the calling thread into buf (NUL-terminated). */
@@ -288,6 +289,14 @@ int rp_infer_select(const float* logits, const uint8_t* mask, const float* offse
 int rp_softnms(const float* scores, const float* segs, const int* count, int B, int cap,
                float sigma, float thresh, const int* max_seg, int* keep, int* keep_count,
                float* final_scores, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Batch collation on the device (dataset/RepurposeClip.py:449-533 preprocessing): the rows of B
+ * ragged sequences, concatenated in src ([sum len_b, D], dtype RP_F16 / RP_F32 / RP_F64 / RP_I64),
+ * row_offsets[B+1] their prefix sums; dst fp32 [B, T, D] = padded batch (pad where t >= len_b),
+ * converted like torch's copy (fp64 -> fp32 round to nearest even). */
+int rp_pad_rows(const void* src, int src_dtype, const int64_t* row_offsets, int B, int T, int D, float pad, float* dst,
+                void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Evaluation metric (utils/metrics.py:82-111 calculate_tiou, batched): pred [V][P][2] fp32 segments

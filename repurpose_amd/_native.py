@@ -11,7 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REPURPOSE_AMD_LIB", os.path.join(_HERE, "_native", "librepurpose_amd.so"))
 
 RP_OK, RP_ERR_ARG, RP_ERR_LAUNCH = 0, 1, 2
-RP_F32, RP_BF16 = 0, 1
+RP_F32, RP_BF16, RP_F16, RP_F64, RP_I64 = 0, 1, 2, 3, 4
 
 c_i64 = ctypes.c_int64
 c_vp = ctypes.c_void_p
@@ -75,6 +75,7 @@ _SIGNATURES = {
     "rp_mha_dropmask_elems": (c_i64, [c_i, c_i, c_i, c_i]),
     "rp_mha_fwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_vp]),
     "rp_mha_bwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_i, c_vp]),
+    "rp_pad_rows": (c_i, [c_vp, c_i, c_vp, c_i, c_i, c_i, c_f, c_vp, c_vp]),
     "rp_tiou_hits": (c_i, [c_vp, c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_i, c_i, c_vp, c_vp]),
     "rp_diou_fwd": (c_i, [c_vp, c_vp, c_i64, c_f, c_i, c_vp, c_vp]),
     "rp_diou_bwd": (c_i, [c_vp, c_vp, c_i64, c_f, c_vp, c_i, c_f, c_vp, c_vp, c_vp]),

@@ -203,6 +203,25 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 
 }  // namespace
 
+// ---------------------------------------------------------------- ragged -> padded batch -----------
+// dst[b][t][d] = t < len_b ? (float)src[(offs[b] + t) * D + d] : pad   (len_b = offs[b+1] - offs[b])
+// torch's copy conversion: fp16 -> fp32 exact, fp64 -> fp32 round-to-nearest-even, int64 -> fp32.
+template <typename S>
+__device__ __forceinline__ float to_f32(S v) { return (float)v; }
+
+template <typename S>
+__global__ void pad_rows_kernel(const S* __restrict__ src, const int64_t* __restrict__ offs, int B, int T, int D,
+                                float pad, float* __restrict__ dst) {
+  const int64_t n = (int64_t)B * T * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bt = i / D;
+    const int d = (int)(i - bt * D);
+    const int b = (int)(bt / T), t = (int)(bt - (int64_t)b * T);
+    const int64_t o = offs[b], len = offs[b + 1] - o;
+    dst[i] = t < len ? to_f32(src[(o + t) * D + d]) : pad;
+  }
+}
+
 extern "C" int rp_concat_rows(const float* v, int dv, const float* a, int da, const float* t, int dt, int64_t rows,
                               void* out, int out_dtype, void* stream) {
   RP_REQUIRE(dv >= 0 && da >= 0 && dt >= 0 && rows >= 0, "rp_concat_rows: negative size");
@@ -328,4 +347,23 @@ extern "C" int rp_adam_step(float* p, const float* g, float* m, float* v, int64_
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr_bc1, beta1,
                      beta2, eps, weight_decay, sqrt_bc2, (bf16*)p_lp);
   return rp_check_launch("rp_adam_step");
+}
+
+extern "C" int rp_pad_rows(const void* src, int src_dtype, const int64_t* row_offsets, int B, int T, int D, float pad,
+                           float* dst, void* stream) {
+  RP_REQUIRE(B >= 0 && T >= 0 && D > 0, "rp_pad_rows: bad shape");
+  if (B == 0 || T == 0) return RP_OK;
+  RP_REQUIRE(row_offsets && dst, "rp_pad_rows: null pointer");
+  const int64_t n = (int64_t)B * T * D;
+  int64_t g = (n + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipStream_t s = (hipStream_t)stream;
+  switch (src_dtype) {
+    case RP_F32: hipLaunchKernelGGL(pad_rows_kernel<float>, dim3((unsigned)g), dim3(256), 0, s, (const float*)src, row_offsets, B, T, D, pad, dst); break;
+    case RP_F16: hipLaunchKernelGGL(pad_rows_kernel<_Float16>, dim3((unsigned)g), dim3(256), 0, s, (const _Float16*)src, row_offsets, B, T, D, pad, dst); break;
+    case RP_F64: hipLaunchKernelGGL(pad_rows_kernel<double>, dim3((unsigned)g), dim3(256), 0, s, (const double*)src, row_offsets, B, T, D, pad, dst); break;
+    case RP_I64: hipLaunchKernelGGL(pad_rows_kernel<int64_t>, dim3((unsigned)g), dim3(256), 0, s, (const int64_t*)src, row_offsets, B, T, D, pad, dst); break;
+    default: rp_set_error("rp_pad_rows: bad src dtype %d", src_dtype); return RP_ERR_ARG;
+  }
+  return rp_check_launch("rp_pad_rows");
 }

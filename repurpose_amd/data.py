@@ -1,0 +1,162 @@
+"""Batch collation for the Repurpose trainer: drop-ins for
+``dataset/RepurposeClip.py`` ``preprocessing`` (:449-533), ``collate_fn`` (:536-567) and
+``collate_fn_test`` (:997-1030), plus a device-side path.
+
+Reference semantics kept exactly (fp32 outputs, ``padding_val`` fill, masks from the VISUAL lengths
+only — SURVEY hazard 9: text may be shorter and is then zero inside the valid region — and the
+same ValueErrors).
+
+Device path: the DataLoader workers only concatenate each modality's ragged rows into one array
+(``collate_ragged`` -> ``RaggedBatch``; no per-item padding loops, no torch.full of the padded
+batch on the host); the main process then moves the concatenated rows through pinned memory in one
+copy per modality and pads / converts on the GPU with ``rp_pad_rows`` (fp16 CLIP, fp32 PANNs, fp64
+text rows as stored in the .npy files).  ``RaggedBatch.to_device`` returns the same dict as
+``collate_fn`` with the tensors already on the device.
+
+``load_features`` reads the feature files with ``numpy.load(allow_pickle=False, mmap_mode='r')``
+(the reference uses allow_pickle=True).
+"""
+import ctypes
+from dataclasses import dataclass, field
+from typing import List
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import kernels as K
+
+_NP_DT = {np.dtype(np.float16): N.RP_F16, np.dtype(np.float32): N.RP_F32, np.dtype(np.float64): N.RP_F64,
+          np.dtype(np.int64): N.RP_I64}
+
+
+def load_features(path):
+    """[seq_len, dim] feature array of one video (memory-mapped, no pickle)."""
+    return np.load(path, mmap_mode="r", allow_pickle=False)
+
+
+# ----------------------------------------------------------------------------- host drop-ins
+@torch.no_grad()
+def preprocessing(vis_feats, aud_feats, text_feats, labels, segments, padding_val=0.0):
+    """dataset/RepurposeClip.py:449-533: pad the per-video tensors to the longest VISUAL sequence."""
+    lens = torch.as_tensor([v.shape[0] for v in vis_feats])
+    T = int(lens.max().item()) if len(vis_feats) else 0
+    if T == 0:
+        raise ValueError("All sequences in the batch have zero length")
+
+    def pad(seqs, tail):
+        out = torch.full((len(seqs), T) + tail, padding_val)
+        for i, s in enumerate(seqs):
+            if s.shape[0] > 0:
+                out[i, :s.shape[0], ...] = s
+        return out
+
+    v = pad(vis_feats, (vis_feats[0].shape[1],))
+    a = pad(aud_feats, (aud_feats[0].shape[1],))
+    t = pad(text_feats, (text_feats[0].shape[1],))
+    lab = pad(labels, ())
+    if len(segments) == 0:
+        raise ValueError("No segments provided to preprocessing function")
+    if all(s.shape[0] == 0 for s in segments):
+        raise ValueError("All segments in the batch have zero length")
+    seg_dim = next(s.shape[1] if s.dim() > 1 else 1 for s in segments if s.shape[0] > 0)
+    seg = torch.full((len(segments), T, seg_dim), padding_val)
+    for i, s in enumerate(segments):
+        if s.shape[0] > 0:
+            s = s.unsqueeze(1) if s.dim() == 1 else s
+            if s.shape[1] != seg_dim:
+                continue  # the reference logs a warning and skips the item
+            seg[i, :s.shape[0], ...] = s
+    masks = (torch.arange(T).expand(len(lens), T) < lens.unsqueeze(1)).unsqueeze(1)
+    return v, a, t, masks, lab, seg
+
+
+def _items(batch):
+    vis = [torch.tensor(np.asarray(it["feats"]["visual"])) for it in batch]
+    aud = [torch.tensor(np.asarray(it["feats"]["audio"])) for it in batch]
+    txt = [torch.tensor(np.asarray(it["feats"]["text"])) for it in batch]
+    lab = [torch.tensor(it["labels"]) for it in batch]
+    seg = [torch.tensor(it["segments"]) for it in batch]
+    return vis, aud, txt, lab, seg
+
+
+def collate_fn(batch):
+    """dataset/RepurposeClip.py:536-567."""
+    v, a, t, m, lab, seg = preprocessing(*_items(batch))
+    return {"video_id": [it["video_id"] for it in batch], "duration": [it["duration"] for it in batch],
+            "visual_feats": v, "audio_feats": a, "text_feats": t, "masks": m, "labels": lab, "segments": seg}
+
+
+def collate_fn_test(batch):
+    """dataset/RepurposeClip.py:997-1030 (adds the reference segments used by the metric)."""
+    out = collate_fn(batch)
+    out["gt_segments"] = [it["gt_segments"] for it in batch]
+    return out
+
+
+# ----------------------------------------------------------------------------- device path
+@dataclass
+class RaggedBatch:
+    """One modality per entry: rows of all videos concatenated + prefix offsets (int64 [B+1])."""
+    video_id: list
+    duration: list
+    rows: dict                      # name -> np.ndarray [sum len, D] (labels: [sum len, 1])
+    offsets: dict                   # name -> np.ndarray int64 [B+1]
+    extra: dict = field(default_factory=dict)
+
+    def to_device(self, device, padding_val=0.0):
+        """collate_fn's dict with every tensor on ``device``: one pinned H2D copy per modality, then
+        rp_pad_rows pads and converts on the GPU."""
+        if not torch.device(device).type == "cuda":
+            raise RuntimeError("RaggedBatch.to_device: the device path needs a ROCm device (use collate_fn on CPU)")
+        B = len(self.video_id)
+        vlens = np.diff(self.offsets["visual"])
+        T = int(vlens.max()) if B else 0
+        if T == 0:
+            raise ValueError("All sequences in the batch have zero length")
+        if int(np.diff(self.offsets["segments"]).max()) == 0:
+            raise ValueError("All segments in the batch have zero length")
+        out = {"video_id": self.video_id, "duration": self.duration}
+        names = {"visual": "visual_feats", "audio": "audio_feats", "text": "text_feats", "labels": "labels",
+                 "segments": "segments"}
+        for name, key in names.items():
+            rows = np.ascontiguousarray(self.rows[name])
+            offs = self.offsets[name]
+            if np.any(np.diff(offs) > T):
+                raise ValueError(f"{name}: a sequence is longer than the visual padding length {T}")
+            D = rows.shape[1] if rows.ndim > 1 else 1
+            src = torch.from_numpy(rows).pin_memory().to(device, non_blocking=True)
+            off = torch.from_numpy(offs.astype(np.int64)).pin_memory().to(device, non_blocking=True)
+            dst = torch.empty(B, T, D, device=device, dtype=torch.float32)
+            N.call("rp_pad_rows", ctypes.c_void_p(src.data_ptr()), _NP_DT[rows.dtype], ctypes.c_void_p(off.data_ptr()),
+                   B, T, D, float(padding_val), ctypes.c_void_p(dst.data_ptr()), K._stream(dst))
+            out[key] = dst.view(B, T) if name == "labels" else dst
+        lens_dev = torch.from_numpy(vlens.astype(np.int64)).to(device, non_blocking=True)
+        out["masks"] = (torch.arange(T, device=device)[None] < lens_dev[:, None]).unsqueeze(1)
+        out.update(self.extra)
+        return out
+
+
+def collate_ragged(batch, test=False):
+    """Worker-side collate: concatenation only (no padding, no torch tensors)."""
+    def cat(arrs, D=None):
+        arrs = [np.asarray(a) for a in arrs]
+        lens = [a.shape[0] for a in arrs]
+        offs = np.zeros(len(arrs) + 1, dtype=np.int64)
+        offs[1:] = np.cumsum(lens)
+        dt = np.result_type(*[a.dtype for a in arrs])
+        dt = np.dtype(np.float32) if dt not in _NP_DT else dt
+        shape = (int(offs[-1]),) + (arrs[0].shape[1:] if arrs[0].ndim > 1 else (1,))
+        rows = np.empty(shape, dtype=dt)
+        for a, o, n in zip(arrs, offs[:-1], lens):
+            if n:
+                rows[o:o + n] = a.reshape(n, -1)
+        return rows, offs
+
+    rows, offs = {}, {}
+    for name in ("visual", "audio", "text"):
+        rows[name], offs[name] = cat([it["feats"][name] for it in batch])
+    rows["labels"], offs["labels"] = cat([np.asarray(it["labels"], dtype=np.int64 if np.asarray(it["labels"]).dtype.kind in "iub" else np.float32) for it in batch])
+    rows["segments"], offs["segments"] = cat([np.asarray(it["segments"], dtype=np.float32).reshape(-1, 2) for it in batch])
+    extra = {"gt_segments": [it["gt_segments"] for it in batch]} if test else {}
+    return RaggedBatch([it["video_id"] for it in batch], [it["duration"] for it in batch], rows, offs, extra)
