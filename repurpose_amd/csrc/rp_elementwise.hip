@@ -75,6 +75,70 @@ __global__ void colsum_pass1(const T* __restrict__ X, int64_t rows, int64_t cols
   ws[(int64_t)blockIdx.x * cols + c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
+// single pass for short inputs (rows <= CS1_MAX_ROWS): a block owns 64 columns (16 float4 chunks)
+// and 64 row groups; each thread sums its rows in order, the groups are added in order through LDS
+constexpr int CS1_MAX_ROWS = 2048;
+template <typename T>
+__global__ __launch_bounds__(1024) void colsum_onepass(const T* __restrict__ X, int64_t rows, int64_t cols,
+                                                       int64_t ldx, const float* __restrict__ w,
+                                                       float* __restrict__ out, int accumulate) {
+  const int ch = threadIdx.x & 15, rg = threadIdx.x >> 4;  // 16 column chunks x 64 row groups
+  const int64_t c = (int64_t)blockIdx.x * 64 + ch * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < cols) {
+    const bool vec = std::is_same<T, float>::value && c + 3 < cols && (ldx & 3) == 0;
+    // rows rg, rg + 64, ... in order, eight loads in flight per step
+    for (int64_t r0 = rg; r0 < rows; r0 += 64 * 8) {
+      float4 v[8];
+      float wr[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t r = r0 + 64 * u;
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        wr[u] = 0.f;
+        if (r < rows) {
+          const T* p = X + r * ldx + c;
+          wr[u] = w ? w[r] : 1.f;
+          if (vec) {
+            v[u] = *reinterpret_cast<const float4*>(p);
+          } else {
+            v[u].x = rp_ld(p);
+            v[u].y = c + 1 < cols ? rp_ld(p + 1) : 0.f;
+            v[u].z = c + 2 < cols ? rp_ld(p + 2) : 0.f;
+            v[u].w = c + 3 < cols ? rp_ld(p + 3) : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s.x += wr[u] * v[u].x; s.y += wr[u] * v[u].y; s.z += wr[u] * v[u].z; s.w += wr[u] * v[u].w;
+      }
+    }
+  }
+  __shared__ float4 red[64][16];
+  red[rg][ch] = s;
+  __syncthreads();
+  // fixed-shape tree over the 64 row groups (deterministic)
+#pragma unroll
+  for (int h = 32; h >= 1; h >>= 1) {
+    if (rg < h) {
+      const float4 q = red[rg + h][ch];
+      float4 t = red[rg][ch];
+      t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
+      red[rg][ch] = t;
+    }
+    __syncthreads();
+  }
+  if (rg == 0 && c < cols) {
+    const float4 t = red[0][ch];
+    // explicit stores: a dynamically indexed local array would live in scratch
+    out[c] = accumulate ? out[c] + t.x : t.x;
+    if (c + 1 < cols) out[c + 1] = accumulate ? out[c + 1] + t.y : t.y;
+    if (c + 2 < cols) out[c + 2] = accumulate ? out[c + 2] + t.z : t.z;
+    if (c + 3 < cols) out[c + 3] = accumulate ? out[c + 3] + t.w : t.w;
+  }
+}
+
 __global__ void colsum_pass2(const float* __restrict__ ws, int64_t nrb, int64_t cols, float* __restrict__ out,
                              int accumulate) {
   const int64_t c = (int64_t)blockIdx.x * CS_THREADS + threadIdx.x;
@@ -259,6 +323,16 @@ extern "C" int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, i
   if (cols == 0) return RP_OK;
   RP_REQUIRE(out && workspace, "rp_colsum: null output/workspace");
   hipStream_t s = (hipStream_t)stream;
+  if (rows > 0 && rows <= CS1_MAX_ROWS) {
+    RP_REQUIRE(X, "rp_colsum: null X");
+    const dim3 g((unsigned)((cols + 63) / 64));
+    if (dtype == RP_BF16)
+      hipLaunchKernelGGL(colsum_onepass<bf16>, g, dim3(1024), 0, s, (const bf16*)X, rows, cols, ldx, w, out, accumulate);
+    else
+      hipLaunchKernelGGL(colsum_onepass<float>, g, dim3(1024), 0, s, (const float*)X, rows, cols, ldx, w, out,
+                         accumulate);
+    return rp_check_launch("rp_colsum");
+  }
   const int64_t nrb = (rows + CS_ROWS - 1) / CS_ROWS;
   if (nrb > 0) {
     RP_REQUIRE(X, "rp_colsum: null X");

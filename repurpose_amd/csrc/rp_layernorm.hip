@@ -7,8 +7,9 @@
 
 namespace {
 
-constexpr int LN_WAVES = 4;          // rows handled concurrently per block
-constexpr int LN_ROWS_PER_BLOCK = 64;  // backward: rows per block (partials granularity)
+constexpr int LN_WAVES = 4;            // forward: rows handled concurrently per block
+constexpr int LNB_WAVES = 8;           // backward: waves per block
+constexpr int LN_ROWS_PER_BLOCK = 32;  // backward: rows per block (partials granularity), 4 per wave
 
 template <int VPT>
 __device__ __forceinline__ void load_row(float (&v)[VPT], const void* base, int dtype, int64_t off) {
@@ -153,7 +154,7 @@ struct LnBwdDev {
 };
 
 template <int VPT>
-__global__ __launch_bounds__(64 * LN_WAVES) void ln_bwd_kernel(int64_t rows, LnBwdDev a) {
+__global__ __launch_bounds__(64 * LNB_WAVES) void ln_bwd_kernel(int64_t rows, LnBwdDev a) {
   constexpr int D = VPT * 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c0 = lane * VPT;
@@ -164,12 +165,13 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_bwd_kernel(int64_t rows, LnB
   load_row<VPT>(gam, a.gamma, RP_F32, c0);
 
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK;
-  for (int rr = w; rr < LN_ROWS_PER_BLOCK; rr += LN_WAVES) {
+  for (int rr = w; rr < LN_ROWS_PER_BLOCK; rr += LNB_WAVES) {
     const int64_t row = rbeg + rr;
     if (row >= rows) break;
-    float g[VPT], x[VPT];
+    float g[VPT], x[VPT], r[VPT];
     load_row<VPT>(g, a.dy, a.dy_dtype, row * a.lddy + c0);
     load_row<VPT>(x, a.x, a.x_dtype, row * a.ldx + c0);
+    if (a.dres) load_row<VPT>(r, a.dres, RP_F32, row * a.lddres + c0);  // issued with the other loads
     if (a.drop_thresh) {
       const uint32_t kb = rp_keep_bits<VPT>(a.drop_seed, (uint32_t)(row * D + c0), a.drop_thresh);
 #pragma unroll
@@ -198,8 +200,6 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_bwd_kernel(int64_t rows, LnB
 #pragma unroll
     for (int i = 0; i < VPT; ++i) dx[i] = rs * (g[i] * gam[i] - s1 - x[i] * s2);
     if (a.dres) {
-      float r[VPT];
-      load_row<VPT>(r, a.dres, RP_F32, row * a.lddres + c0);
 #pragma unroll
       for (int i = 0; i < VPT; ++i) dx[i] += r[i];
     }
@@ -214,17 +214,17 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_bwd_kernel(int64_t rows, LnB
     }
   }
   // combine the waves' partial affine gradients through LDS, one partial row per block
-  __shared__ float red[2][LN_WAVES][D];
+  __shared__ float red[2][LNB_WAVES][D];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     red[0][w][c0 + i] = pg[i];
     red[1][w][c0 + i] = pb[i];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < D; c += 64 * LN_WAVES) {
+  for (int c = threadIdx.x; c < D; c += 64 * LNB_WAVES) {
     float sg = 0.f, sb = 0.f;
 #pragma unroll
-    for (int k = 0; k < LN_WAVES; ++k) {
+    for (int k = 0; k < LNB_WAVES; ++k) {
       sg += red[0][k][c];
       sb += red[1][k][c];
     }
@@ -294,6 +294,6 @@ extern "C" int rp_layernorm_bwd(int64_t rows, int64_t D, const rp_ln_bwd_args* p
   a.lp_scale = p->dx_lp_dropout_p > 0.f ? 1.f / (1.f - p->dx_lp_dropout_p) : 1.f;
   a.lp_seed = p->dx_lp_seed;
   a.dgamma_part = p->dgamma_part; a.dbeta_part = p->dbeta_part;
-  dim3 grid((unsigned)rp_layernorm_bwd_blocks(rows)), block(64 * LN_WAVES);
+  dim3 grid((unsigned)rp_layernorm_bwd_blocks(rows)), block(64 * LNB_WAVES);
   RP_LN_DISPATCH(ln_bwd_kernel, D, grid, block, (hipStream_t)stream, rows, a);
 }

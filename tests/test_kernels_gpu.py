@@ -310,6 +310,11 @@ def test_rowdot_colsum_concat_cast(dev):
     close(cs, (X.double() * w.double()[:, None]).sum(0), atol=1e-3, what="colsum")
     Xb = X.to(torch.bfloat16)
     close(K.colsum(Xb), Xb.double().sum(0), atol=1e-3, what="colsum bf16")
+    for r, c in ((5000, 96), (300, 250)):  # two-pass path; ragged last column chunk
+        Y = rnd(r, c, dev=dev, seed=r)
+        acc = rnd(c, dev=dev, seed=c)
+        close(K.colsum(Y, out=acc.clone(), accumulate=True), acc.double() + Y.double().sum(0), atol=2e-3,
+              what=f"colsum {r}x{c}")
     v = rnd(3, 5, 8, dev=dev, seed=7)
     a = rnd(3, 5, 16, dev=dev, seed=8)
     t = rnd(3, 5, 4, dev=dev, seed=9)
