@@ -342,8 +342,14 @@ extern "C" int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, i
     else
       hipLaunchKernelGGL(colsum_pass1<float>, g1, dim3(CS_THREADS), 0, s, (const float*)X, rows, cols, ldx, w, workspace);
   }
-  hipLaunchKernelGGL(colsum_pass2, dim3((unsigned)((cols + CS_THREADS - 1) / CS_THREADS)), dim3(CS_THREADS), 0, s,
-                     workspace, nrb, cols, out, accumulate);
+  // second pass over the nrb partial rows with the single-pass kernel (nrb <= CS1_MAX_ROWS for any
+  // rows < CS1_MAX_ROWS * CS_ROWS; beyond that the serial pass)
+  if (nrb <= CS1_MAX_ROWS)
+    hipLaunchKernelGGL(colsum_onepass<float>, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, s, workspace, nrb, cols,
+                       cols, (const float*)nullptr, out, accumulate);
+  else
+    hipLaunchKernelGGL(colsum_pass2, dim3((unsigned)((cols + CS_THREADS - 1) / CS_THREADS)), dim3(CS_THREADS), 0, s,
+                       workspace, nrb, cols, out, accumulate);
   return rp_check_launch("rp_colsum");
 }
 

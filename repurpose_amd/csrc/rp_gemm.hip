@@ -604,7 +604,13 @@ void wgrad_plan(int64_t M, int64_t N, int64_t K, int bk, int& splits, int64_t& k
     return;
   }
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  int64_t sp = 512 / (tiles > 0 ? tiles : 1);
+  static int target = -1;  // workgroups to aim at (RP_WGRAD_BLOCKS overrides, for tuning)
+  if (target < 0) {
+    const char* e = getenv("RP_WGRAD_BLOCKS");
+    target = e ? atoi(e) : 512;
+    if (target < 1) target = 512;
+  }
+  int64_t sp = target / (tiles > 0 ? tiles : 1);
   const int64_t maxsp = K / (8 * bk);
   if (sp > maxsp) sp = maxsp;
   if (sp < 1) sp = 1;
