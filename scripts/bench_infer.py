@@ -1,0 +1,106 @@
+"""Inference-path benchmark (BASELINE.json config 5): a batch of 64 videos with val-like lengths
+(60 s .. 1801 s of 1-second features, padded to the longest), eval mode, ``MMCTransformer.inference_``
+end to end = forward + candidate selection (rp_infer_select) + batched Soft-NMS (rp_softnms).
+Prints one JSON line: videos/s on the GPU (fp32 parity mode and bf16), and the CPU restatement's
+``inference_`` (oracle, stock torch + numpy Soft-NMS) on a bounded sample of the same videos.
+
+    python scripts/bench_infer.py [--videos 64] [--reps 5] [--cpu-videos 4]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import MODEL_CFG  # noqa: E402
+
+CFG = {"pre_nms_topk": 1000, "pre_nms_thresh": 0.5, "duration_thresh": 10, "duration_thresh_max": 90,
+       "max_seg_per_min": 0.3, "nms_sigma": 0.5, "min_score": 0.01}
+
+
+def exercise_heads(model):
+    """Random-init heads put every probability near 0.5 and every offset near 0, so no candidate
+    would survive the 0.5 score / 10..90 s duration filters: shift the final cls bias so that
+    logits straddle 0 and the final reg bias to ~15 s per side (same edit on GPU model and oracle)."""
+    sd = model.state_dict()
+    with torch.no_grad():
+        sd["cls_head.7.bias"].fill_(0.02)
+        sd["reg_head.7.bias"].fill_(15.0)
+    model.load_state_dict(sd)
+    return model
+
+
+def make_batch(V, seed, dev):
+    g = torch.Generator().manual_seed(seed)
+    lens = torch.randint(60, 1802, (V,), generator=g)
+    T = int(lens.max())
+    v = torch.randn(V, T, 512, generator=g)
+    v = v / v.norm(dim=-1, keepdim=True)
+    a = torch.relu(torch.randn(V, T, 2048, generator=g))
+    t = torch.randn(V, T, 384, generator=g)
+    t = t / t.norm(dim=-1, keepdim=True)
+    mask = (torch.arange(T)[None] < lens[:, None]).unsqueeze(1)
+    b = {"visual_feats": v * mask.transpose(1, 2), "audio_feats": a * mask.transpose(1, 2),
+         "text_feats": t * mask.transpose(1, 2), "masks": mask, "labels": torch.zeros(V, T),
+         "segments": torch.zeros(V, T, 2)}
+    b = {k: x.to(dev) for k, x in b.items()}
+    b["video_id"] = [f"v{i}" for i in range(V)]
+    b["duration"] = [int(x) for x in lens]
+    return b
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--videos", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--cpu-videos", type=int, default=4)
+    args = ap.parse_args()
+    from repurpose_amd.MMCTransformer import MMCTransformer
+    dev = torch.device("cuda", 0)
+    res = {"metric": "inference videos/sec (config 5: forward + select + Soft-NMS)", "unit": "videos/sec",
+           "higher_is_better": True, "videos": args.videos, "data": "synthetic, val-like lengths 60..1801 s; random-init weights with shifted final head biases"}
+    batch = make_batch(args.videos, 7, dev)
+    for dt in ("fp32", "bf16"):
+        torch.manual_seed(1234)
+        m = exercise_heads(MMCTransformer(**MODEL_CFG, compute_dtype=dt)).to(dev).eval()
+        with torch.no_grad():
+            out = m.inference_(batch, CFG)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.reps):
+                out = m.inference_(batch, CFG)
+            torch.cuda.synchronize()
+        dt_s = (time.perf_counter() - t0) / args.reps
+        res[f"gpu_{dt}"] = {"value": args.videos / dt_s, "ms_per_batch": dt_s * 1e3,
+                            "proposals": int(sum(len(o["segments"]) for o in out))}
+        if dt == "fp32":
+            gpu_fp32_out = out
+    # CPU restatement on a bounded sample of the same videos
+    from oracle.mmct_oracle import MMCTransformer as Oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(1234)
+    om = exercise_heads(Oracle(**MODEL_CFG)).eval()
+    n = min(args.cpu_videos, args.videos)
+    cb = {k: (x[:n].cpu() if torch.is_tensor(x) else x[:n]) for k, x in batch.items()}
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        ref = om.inference_(cb, CFG)
+        cpu_s = time.perf_counter() - t0
+    # fp32 parity on the sampled videos: identical proposal frame indices (labels) after Soft-NMS
+    same = all(r["labels"].tolist() == g["labels"].cpu().tolist() for r, g in zip(ref, gpu_fp32_out[:n]))
+    res["fp32_parity_sample"] = {"videos": n, "identical_proposals": bool(same),
+                                 "proposals": int(sum(len(r["labels"]) for r in ref))}
+    res["cpu_baseline"] = {"value": n / cpu_s, "unit": "videos/sec", "cores": threads, "kind": "port",
+                           "sample": f"oracle inference_ (stock torch fp32 + numpy Soft-NMS) on {n} of the videos"}
+    res["value"] = res["gpu_bf16"]["value"]
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
