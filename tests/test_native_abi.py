@@ -52,5 +52,5 @@ def test_workspace_queries():
     lib = N.load()
     assert lib.rp_colsum_workspace(16384, 2048) == 256 * 2048
     assert lib.rp_gemm_wgrad_workspace(2048, 512, 16384) >= 2048 * 512 * 4
-    assert lib.rp_layernorm_bwd_blocks(16384) == 256
+    assert lib.rp_layernorm_bwd_blocks(16384) == 16384 // 32  # 32 rows per block (8 waves x 4 rows)
     assert lib.rp_layernorm_bwd_blocks(1) == 1
