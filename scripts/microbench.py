@@ -77,6 +77,30 @@ def main():
         t = timeit(lambda: K.layernorm_bwd(dy, x, mu, rs, gm, dres=dy, lp_dtype=bf, lp_dropout_p=0.1, dgamma=dg,
                                            dbeta=dg), a.reps)
         res.append(("ln bwd (+dres, lp out, dgamma/dbeta)", t, M * d * 18 / t / 1e6, "GB/s"))
+    if a.only in ("lib",):
+        # vendor-library yardsticks at the same shapes (hipBLASLt via torch.mm, torch SDPA): headroom only
+        for (n, k, name) in [(3 * d, d, "qkv"), (d, d, "out_proj"), (dff, d, "linear1"), (d, dff, "linear2")]:
+            x = torch.randn(M, k, generator=g).to(dev, bf)
+            w = (torch.randn(n, k, generator=g) * 0.02).to(dev, bf)
+            dy = torch.randn(M, n, generator=g).to(dev, bf)
+            fl = 2.0 * M * n * k
+            t = timeit(lambda: torch.mm(x, w.t()), a.reps)
+            res.append((f"torch.mm fwd {name}", t, fl / t / 1e9, "TFLOP/s"))
+            t = timeit(lambda: torch.mm(dy, w), a.reps)
+            res.append((f"torch.mm dgrad {name}", t, fl / t / 1e9, "TFLOP/s"))
+            t = timeit(lambda: torch.mm(dy.t(), x), a.reps)
+            res.append((f"torch.mm wgrad {name}", t, fl / t / 1e9, "TFLOP/s"))
+        q = torch.randn(B, H, T, 64, generator=g).to(dev, bf).requires_grad_()
+        kk = torch.randn(B, H, T, 64, generator=g).to(dev, bf).requires_grad_()
+        v = torch.randn(B, H, T, 64, generator=g).to(dev, bf).requires_grad_()
+        fl = 4.0 * B * H * T * T * 64
+        F = torch.nn.functional
+        t = timeit(lambda: F.scaled_dot_product_attention(q, kk, v), a.reps)
+        res.append(("torch sdpa fwd", t, fl / t / 1e9, "TFLOP/s"))
+        o = F.scaled_dot_product_attention(q, kk, v)
+        go = torch.randn_like(o)
+        t = timeit(lambda: torch.autograd.grad(F.scaled_dot_product_attention(q, kk, v), (q, kk, v), go), a.reps)
+        res.append(("torch sdpa fwd+bwd", t, 3 * fl / t / 1e9, "TFLOP/s"))
     for name, t, r, u in res:
         print(f"{name:48s} {t * 1e3:9.1f} us  {r:8.1f} {u}", flush=True)
 
