@@ -132,7 +132,8 @@ int rp_layernorm_fwd(int64_t rows, int64_t D, const rp_ln_fwd_args* a, void* str
  *   dx = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat));  dx += dres
  *   dx_f32 (if non-NULL) = dx;  dx_lp (if non-NULL) = dx * keep(dx_lp_seed)/(1-dx_lp_dropout_p)
  *   dgamma_part[blk, c] = sum over the block's rows of g*xhat;  dbeta_part[blk, c] = sum g
- * Partials have rp_layernorm_bwd_blocks(rows) rows; reduce them with rp_colsum. */
+ * Partials have rp_layernorm_bwd_blocks(rows) rows of row stride ld_part (0 = D); reduce them with
+ * rp_colsum (dgamma_part = P, dbeta_part = P + D, ld_part = 2D reduces both in one launch). */
 typedef struct rp_ln_bwd_args {
   const void* dy;
   int dy_dtype;
@@ -159,6 +160,7 @@ typedef struct rp_ln_bwd_args {
   uint32_t dx_lp_seed;
   float* dgamma_part;
   float* dbeta_part;
+  int64_t ld_part;
 } rp_ln_bwd_args;
 
 int64_t rp_layernorm_bwd_blocks(int64_t rows);
@@ -226,15 +228,17 @@ typedef struct rp_mha_args {
 
 int64_t rp_mha_dropmask_elems(int B, int Tq, int Tk, int H);
 int rp_mha_fwd(int dtype, const rp_mha_args* args, void* stream);
-/* phases: 1 = delta pre-pass, 2 = dK/dV, 4 = dQ (7 = all, in that order) */
+/* phases: 1 = delta pre-pass, 2 = dK/dV, 4 = dQ.  1 and 4 together fuse the delta pre-pass into the
+ * dQ kernel, which then runs before dK/dV (7 = all: fused dQ + delta, then dK/dV). */
 int rp_mha_bwd(int dtype, const rp_mha_args* args, int phases, void* stream);
 int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk,
                 float scale, float dropout_p, uint32_t seed, void* out, float* lse, uint16_t* dropmask,
                 void* stream);
 /* Backward; dqkv: [B*T, 3*H*dk] (fully overwritten); delta_ws: [B, H, T] fp32 workspace.
- * = rp_attn_bwd_delta (delta = rowsum(dout * out)), then rp_attn_bwd_dkdv (dK, dV columns of dqkv,
- * one workgroup per 128-key block) and rp_attn_bwd_dq (dQ columns, one per 128-query block); the
- * three phases are also exported separately (per-kernel timing; same arguments). */
+ * = rp_attn_bwd_dq_delta (dQ columns of dqkv, one workgroup per 128-query block, which also writes
+ * delta = rowsum(dout * out) to delta_ws), then rp_attn_bwd_dkdv (dK, dV columns, one workgroup per
+ * 128-key block, reading delta).  The phases are also exported separately (per-kernel timing);
+ * rp_attn_bwd_delta + rp_attn_bwd_dq is the unfused equivalent of rp_attn_bwd_dq_delta. */
 int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
                 const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                 const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream);
@@ -243,6 +247,9 @@ int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, int B, int T
 int rp_attn_bwd_dkdv(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
                      const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                      const uint16_t* dropmask, void* dqkv, void* stream);
+int rp_attn_bwd_dq_delta(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
+                         float* delta_ws, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
+                         float dropout_p, const uint16_t* dropmask, void* dqkv, void* stream);
 int rp_attn_bwd_dq(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
                    const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                    const uint16_t* dropmask, void* dqkv, void* stream);

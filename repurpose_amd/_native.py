@@ -39,7 +39,8 @@ class LnBwdArgs(ctypes.Structure):
                 ("y_dtype", c_i), ("ldy", c_i64), ("dropout_p", c_f), ("dropout_seed", c_u32),
                 ("dres", c_vp), ("lddres", c_i64), ("dx_f32", c_vp), ("lddx", c_i64), ("dx_lp", c_vp),
                 ("dx_lp_dtype", c_i), ("lddx_lp", c_i64), ("dx_lp_dropout_p", c_f),
-                ("dx_lp_seed", c_u32), ("dgamma_part", c_vp), ("dbeta_part", c_vp)]
+                ("dx_lp_seed", c_u32), ("dgamma_part", c_vp), ("dbeta_part", c_vp),
+                ("ld_part", c_i64)]
 
 
 class MhaArgs(ctypes.Structure):
@@ -71,6 +72,8 @@ _SIGNATURES = {
                           c_vp, c_vp, c_vp]),
     "rp_attn_bwd_delta": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_vp, c_vp]),
     "rp_attn_bwd_dkdv": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp]),
+    "rp_attn_bwd_dq_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp,
+                                   c_vp]),
     "rp_attn_bwd_dq": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp]),
     "rp_mha_dropmask_elems": (c_i64, [c_i, c_i, c_i, c_i]),
     "rp_mha_fwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_vp]),

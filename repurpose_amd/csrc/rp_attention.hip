@@ -453,10 +453,20 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     if (q >= Tq) continue;
     const float inv = drop_scale / l;
     T* orow = out + ((int64_t)b * Tq + q) * ldo + h * HD;
+    if constexpr (BF) {  // the lane's 4 consecutive dims of a 16-dim tile -> one 8-byte store
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) rp_st(orow + dt * 16 + 4 * g + r, o[qt][dt][r] * inv);
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[qt][dt][r] * inv);
+        *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = v;
+      }
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rp_st(orow + dt * 16 + 4 * g + r, o[qt][dt][r] * inv);
+    }
     if (g == 0) lse[(int64_t)bh * Tq + q] = m[qt] * scale + logf(l);
   }
 }
@@ -747,7 +757,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
 // =================================================================================================
 // backward: dQ per 128-query block (4 waves x 32 queries), sweep over 64-key tiles
 // =================================================================================================
-template <typename T, bool DROP>
+// DELTA: the kernel also forms delta = rowsum(dO * O) of its queries (the lane's 16 dims of dO are
+// already in registers; the 4 lanes of a query combine by quad_sum) and writes it for the dK/dV
+// kernel, which then runs second — no separate delta pre-pass over dO and O.
+template <typename T, bool DROP, bool DELTA>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
   using C = AttnCfg<T>;
   constexpr bool BF = std::is_same<T, bf16>::value;
@@ -783,19 +796,34 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + qt * 16 + i;
     lq[qt] = q < Tq ? lse[(int64_t)bh * Tq + q] * LOG2E : INFINITY;
-    dq[qt] = q < Tq ? -delta[(int64_t)bh * Tq + q] * (DROP ? 1.f / drop_scale : 1.f) : 0.f;  // -delta/ds
+    if constexpr (!DELTA)
+      dq[qt] = q < Tq ? -delta[(int64_t)bh * Tq + q] * (DROP ? 1.f / drop_scale : 1.f) : 0.f;  // -delta/ds
+    float part = 0.f;  // DELTA: this lane's share of rowsum(dO * O)
     if constexpr (BF) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         qf[qt][s] = row_frag_gmem((const bf16*)Qg, ldq, q0 + qt * 16, Tq, s * 32, lane);
         df[qt][s] = row_frag_gmem((const bf16*)dOg, lddo, q0 + qt * 16, Tq, s * 32, lane);
+        if constexpr (DELTA) {
+          const bf16x8 of = row_frag_gmem((const bf16*)a.out + (int64_t)b * Tq * a.ldo + h * HD, a.ldo,
+                                          q0 + qt * 16, Tq, s * 32, lane);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) part += (float)df[qt][s][j] * (float)of[j];
+        }
       }
     } else {
+      const T* Og = (const T*)a.out + (int64_t)b * Tq * a.ldo + h * HD;
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         qs[qt][s] = q < Tq ? (float)Qg[(int64_t)q * ldq + 4 * s + g] : 0.f;
         dsv[qt][s] = q < Tq ? (float)dOg[(int64_t)q * lddo + 4 * s + g] : 0.f;
+        if constexpr (DELTA) part += dsv[qt][s] * (q < Tq ? (float)Og[(int64_t)q * a.ldo + 4 * s + g] : 0.f);
       }
+    }
+    if constexpr (DELTA) {
+      const float dl = quad_sum(part);
+      if (g == 0 && q < Tq) a.delta[(int64_t)bh * Tq + q] = dl;
+      dq[qt] = q < Tq ? -dl * (DROP ? 1.f / drop_scale : 1.f) : 0.f;
     }
   }
 
@@ -959,13 +987,23 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
   return rp_check_launch("rp_mha_fwd");
 }
 
-// phases: bit 0 = delta pre-pass, bit 1 = dK/dV kernel, bit 2 = dQ kernel
+// phases: bit 0 = delta pre-pass, bit 1 = dK/dV kernel, bit 2 = dQ kernel.  With bits 0 and 2 both
+// set the delta pre-pass is fused into the dQ kernel, which then runs first (dK/dV reads its delta).
 template <typename T>
 int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   const int64_t rows = (int64_t)a.B * a.Tq;
-  if (phases & 1) hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
   const int nkb = (a.Tk + KV_KB - 1) / KV_KB;
   const int nqb = (a.Tq + FW_QB - 1) / FW_QB;
+  const bool fused = (phases & 5) == 5;
+  if (fused) {
+    const dim3 grid((unsigned)(nqb * a.B * a.H));
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true, true>), grid, dim3(NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false, true>), grid, dim3(NT), 0, s, a);
+  } else if (phases & 1) {
+    hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
+  }
   if (phases & 2) {
     const dim3 grid((unsigned)(nkb * a.B * a.H));
     if (a.drop_thresh)
@@ -973,12 +1011,12 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     else
       hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false>), grid, dim3(NT), 0, s, a);
   }
-  if (phases & 4) {
+  if ((phases & 4) && !fused) {
     const dim3 grid((unsigned)(nqb * a.B * a.H));
     if (a.drop_thresh)
-      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true>), grid, dim3(NT), 0, s, a);
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true, false>), grid, dim3(NT), 0, s, a);
     else
-      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false>), grid, dim3(NT), 0, s, a);
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false, false>), grid, dim3(NT), 0, s, a);
   }
   return rp_check_launch("rp_mha_bwd");
 }
@@ -1129,6 +1167,14 @@ extern "C" int rp_attn_bwd_dkdv(int dtype, const void* qkv, const void* dout, co
                                 const uint16_t* dropmask, void* dqkv, void* stream) {
   return attn_bwd_packed(2, dtype, qkv, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
                          const_cast<float*>(delta_ws), stream);
+}
+
+extern "C" int rp_attn_bwd_dq_delta(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
+                                    float* delta_ws, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
+                                    float dropout_p, const uint16_t* dropmask, void* dqkv, void* stream) {
+  RP_REQUIRE(out, "rp_attn_bwd_dq_delta: null out");
+  return attn_bwd_packed(5, dtype, qkv, out, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
+                         delta_ws, stream);
 }
 
 extern "C" int rp_attn_bwd_dq(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,

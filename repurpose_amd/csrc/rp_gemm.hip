@@ -177,7 +177,8 @@ __device__ __forceinline__ void accum_chunks(float (&b)[GemmCfg<T>::VEC], const 
 }
 
 constexpr int CST = BN + 4;                 // fp32 LDS row stride of the staged C tile
-constexpr int CTILE_BYTES = BM * CST * 4;
+constexpr int CTILE_BYTES = BM * CST * 4;   // whole staged C tile
+constexpr int CHALF_BYTES = CTILE_BYTES / 2;  // C tile staged in two 64-row halves (low-LDS configs)
 
 template <typename T, bool AK, bool BKM>
 constexpr int gemm_lds_bytes() {
@@ -190,12 +191,20 @@ constexpr int gemm_lds_bytes() {
 // ---- shared epilogue: stage the 128x128 fp32 tile in LDS, then 16-byte row chunks per thread ----
 // MODE 0 applies the fused epilogue (bias, relu, dropout, gate, residual, accumulate) and converts;
 // MODE 1 stores the raw fp32 partial tile into split blockIdx.y's slab.
-template <typename TC, int MODE>
+template <typename TC, int MODE, bool HALVES = false>
 __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* lds, int tid, int lane, int wm, int wn,
                                               int64_t m0, int64_t n0, int64_t M, int64_t N, TC* __restrict__ Cout,
                                               int64_t ldc, float alpha, const EpiDev& ep) {
   float* cs = reinterpret_cast<float*>(lds);
-  {
+  constexpr int OV = 16 / (int)sizeof(TC);
+  constexpr int CPRO = BN / OV;
+  TC* Cbase = Cout + (MODE == 1 ? (int64_t)blockIdx.y * M * ldc : 0);
+  constexpr int NH = HALVES ? 2 : 1;  // staging passes
+  constexpr int HR = BM / NH;          // rows per pass
+#pragma unroll 1
+  for (int half = 0; half < NH; ++half) {
+  if (half) __syncthreads();  // the first half's rows are consumed
+  if (!HALVES || wm == half) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -203,20 +212,17 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* ld
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          cs[(wm * 64 + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
+          cs[((HALVES ? 0 : wm * 64) + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
   }
   __syncthreads();
-  constexpr int OV = 16 / (int)sizeof(TC);
-  constexpr int CPRO = BN / OV;
-  TC* Cbase = Cout + (MODE == 1 ? (int64_t)blockIdx.y * M * ldc : 0);
-  for (int id = tid; id < BM * CPRO; id += NT) {
-    const int row = id / CPRO, cc = (id % CPRO) * OV;
+  for (int id = tid; id < HR * CPRO; id += NT) {
+    const int row = id / CPRO + half * HR, cc = (id % CPRO) * OV;
     const int64_t m = m0 + row, n = n0 + cc;
     if (m >= M || n >= N) continue;
     float v[OV];
 #pragma unroll
     for (int e = 0; e < OV; e += 4) {
-      float4 q = *reinterpret_cast<const float4*>(cs + row * CST + cc + e);
+      float4 q = *reinterpret_cast<const float4*>(cs + (row - half * HR) * CST + cc + e);
       v[e] = q.x * alpha; v[e + 1] = q.y * alpha; v[e + 2] = q.z * alpha; v[e + 3] = q.w * alpha;
     }
     if (MODE == 0) {
@@ -269,6 +275,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* ld
       for (int e = 0; e < 8; ++e) ob[e] = (bf16)v[e];
       *reinterpret_cast<uint4*>(dst) = o;
     }
+  }
   }
 }
 
@@ -365,27 +372,61 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64
 // (guide §5.4 rule 21); the fragment reads apply the same involution:
 //   k-major tile [128 rows][64 k] (128-B rows): 16-B chunk c of row r lives at chunk c ^ ((r>>1)&7)
 //     -> every ds_read_b128 lane group of the 16x16x32 A/B fragment read hits 16 distinct slots;
-//   m-major tile [64 k][128 cols] (256-B rows): chunk c of row k lives at c ^ 2*s(k),
+//   k-major tile [128 rows][32 k] (64-B rows): chunk c of row r lives at c ^ f((r>>2)&3),
+//     f = {0,2,3,1} -> the four rows of each residue r&3 in a ds_read_b128 lane group (two with
+//     k-chunk g, two with g^1) land on four distinct chunks: 16 distinct slots again;
+//   m-major tile [BK k][128 cols] (256-B rows): chunk c of row k lives at c ^ 2*s(k),
 //     s(k) = (k&3) | ((k>>3)&1)<<2 -> the 8 rows of a ds_read_b64_tr_b16 half-wave read hit
 //     8 distinct 32-B slots.
-// Two LDS stages (2 x 32 KiB), one barrier per 64-deep K step; rows past M/N are clamped to the last
-// valid row (their outputs are discarded), so the path requires full 64-deep K steps.
-constexpr int GT = 16384;  // bytes of one operand tile (one stage)
+// Configurations (the 16 KiB-per-stage k=64 images, or 8 KiB k=32 ones):
+//   CFG 0  BK 64, two LDS stages, whole-tile C staging: 67.6 KiB, 2 workgroups / CU
+//   CFG 1  BK 64, one LDS stage (load, barrier, compute, barrier), C in halves: 33.8 KiB, 4 / CU
+//   CFG 2  BK 32, two LDS stages, C in halves: 33.8 KiB, 4 / CU
+// Measured on MI355X (scripts/microbench.py, M = 16384): K <= 1024 runs best on CFG 1, whose four
+// co-resident workgroups hide each other's load latency (qkv fwd 43.1 -> 41.3 us, linear1 fwd
+// 54.3 -> 50.5, K = 512 dgrad into d_ff 64.3 -> 52.8), deeper K on CFG 0 (linear2 fwd 39.5 vs 43.0);
+// CFG 2 lost to CFG 1 everywhere and serves only K % 64 == 32.  In the whole training step, though,
+// CFG 1 on the K = 512, N >= 1536 shapes (RP_GEMM_POLICY=1) measured 20.30 vs 20.15 ms per step
+// (same box, interleaved runs) although each of those kernels ran faster in the kernel trace: the
+// denser 4-workgroup residency costs more in the rest of the step (clock under load) than it saves,
+// so the default policy keeps CFG 0.
+// Rows past M/N are clamped to the last valid row (their outputs are discarded), so the path needs
+// whole BK-deep K steps.
 typedef __attribute__((address_space(3))) void lds_void;
 
+template <int CFG>
+struct DmaCfg {
+  static constexpr int BK = CFG == 2 ? 32 : 64;
+  static constexpr int STAGES = CFG == 1 ? 1 : 2;
+  static constexpr bool HALVES = CFG != 0;
+  static constexpr int GT = BM * BK * 2;  // bytes of one operand tile (one stage)
+  static constexpr int PER_WAVE = GT / 1024 / (NT / 64);  // 1-KiB DMA pieces per wave per operand
+  static constexpr int LDS_MAIN = 2 * STAGES * GT;
+  static constexpr int LDS_EPI = HALVES ? CHALF_BYTES : CTILE_BYTES;
+  static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+};
+
 __device__ __forceinline__ int kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
+__device__ __forceinline__ int kswz32(int r, int c) { return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3); }
 __device__ __forceinline__ int mswz(int k, int c) { return c ^ (2 * ((k & 3) | (((k >> 3) & 1) << 2))); }
 
-template <bool KMAJ>
+template <bool KMAJ, int BK>
 __device__ __forceinline__ void glds_tile(const bf16* __restrict__ base, int64_t ld, int64_t rows_lim, int64_t row0,
                                           int64_t k0, char* tile, int wid, int lane) {
+  constexpr int PER = BM * BK * 2 / 1024 / (NT / 64);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int I = wid * 4 + j;  // wave-instruction index (1 KiB of the 16 KiB tile)
+  for (int j = 0; j < PER; ++j) {
+    const int I = wid * PER + j;  // wave-instruction index (1 KiB of the tile)
     const bf16* src;
     if (KMAJ) {
-      const int r = I * 8 + (lane >> 3);
-      const int lc = kswz(r, lane & 7);
+      int r, lc;
+      if constexpr (BK == 64) {
+        r = I * 8 + (lane >> 3);
+        lc = kswz(r, lane & 7);
+      } else {
+        r = I * 16 + (lane >> 2);
+        lc = kswz32(r, lane & 3);
+      }
       int64_t rr = row0 + r;
       if (rr >= rows_lim) rr = rows_lim - 1;
       src = base + rr * ld + k0 + lc * 8;
@@ -400,10 +441,12 @@ __device__ __forceinline__ void glds_tile(const bf16* __restrict__ base, int64_t
   }
 }
 
+template <int BK>
 __device__ __forceinline__ bf16x8 frag_k_swz(const char* t, int rbase, int kbase, int lane) {
   const int r = rbase + (lane & 15);
   const int lc = (kbase >> 3) + (lane >> 4);
-  return *reinterpret_cast<const bf16x8*>(t + r * 128 + kswz(r, lc) * 16);
+  if constexpr (BK == 64) return *reinterpret_cast<const bf16x8*>(t + r * 128 + kswz(r, lc) * 16);
+  return *reinterpret_cast<const bf16x8*>(t + r * 64 + kswz32(r, lc) * 16);
 }
 
 __device__ __forceinline__ bf16x8 frag_m_swz(const char* t, int rbase, int kbase, int lane) {
@@ -420,14 +463,15 @@ __device__ __forceinline__ bf16x8 frag_m_swz(const char* t, int rbase, int kbase
   return r;
 }
 
-template <bool AK, bool BKM, typename TC, int MODE>
+template <bool AK, bool BKM, typename TC, int MODE, int CFG>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t N, int64_t K,
                                                               const bf16* __restrict__ A, int64_t lda,
                                                               const bf16* __restrict__ B, int64_t ldb,
                                                               TC* __restrict__ Cout, int64_t ldc, float alpha,
                                                               EpiDev ep, int64_t kchunk, float* __restrict__ bslab) {
-  constexpr int LDS = 4 * GT > CTILE_BYTES ? 4 * GT : CTILE_BYTES;
-  __shared__ __attribute__((aligned(16))) char lds[LDS];
+  using D = DmaCfg<CFG>;
+  constexpr int BK = D::BK, GT = D::GT;
+  __shared__ __attribute__((aligned(16))) char lds[D::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
@@ -451,24 +495,29 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
 #pragma unroll
   for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
 
-  const int nk = kend > kbeg ? (int)((kend - kbeg) / 64) : 0;
-  if (nk > 0) {
-    glds_tile<AK>(A, lda, M, m0, kbeg, lds, wid, lane);
-    glds_tile<BKM>(B, ldb, N, n0, kbeg, lds + GT, wid, lane);
+  const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
+  if (D::STAGES == 2 && nk > 0) {
+    glds_tile<AK, BK>(A, lda, M, m0, kbeg, lds, wid, lane);
+    glds_tile<BKM, BK>(B, ldb, N, n0, kbeg, lds + GT, wid, lane);
   }
-  __syncthreads();
+  if (D::STAGES == 2) __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = lds + (kt & 1) * 2 * GT;
+    const char* cur = lds + (D::STAGES == 2 ? (kt & 1) * 2 * GT : 0);
     char* nxt = lds + ((kt + 1) & 1) * 2 * GT;
-    if (kt + 1 < nk) {
-      const int64_t k1 = kbeg + (int64_t)(kt + 1) * 64;
-      glds_tile<AK>(A, lda, M, m0, k1, nxt, wid, lane);
-      glds_tile<BKM>(B, ldb, N, n0, k1, nxt + GT, wid, lane);
+    if (D::STAGES == 1) {  // one LDS stage: the co-resident workgroups hide the load latency
+      if (kt > 0) __syncthreads();
+      glds_tile<AK, BK>(A, lda, M, m0, kbeg + (int64_t)kt * BK, lds, wid, lane);
+      glds_tile<BKM, BK>(B, ldb, N, n0, kbeg + (int64_t)kt * BK, lds + GT, wid, lane);
+      __syncthreads();
+    } else if (kt + 1 < nk) {
+      const int64_t k1 = kbeg + (int64_t)(kt + 1) * BK;
+      glds_tile<AK, BK>(A, lda, M, m0, k1, nxt, wid, lane);
+      glds_tile<BKM, BK>(B, ldb, N, n0, k1, nxt + GT, wid, lane);
     }
-    if (want_bias) {  // column sums of the staged dY tile (bias gradient), 4 x 16 B per thread
+    if (want_bias) {  // column sums of the staged dY tile (bias gradient), BK/16 x 16 B per thread
       const int cg = tid & 15;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < BK / 16; ++j) {
         const int k = (tid >> 4) + 16 * j;
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(cur + k * 256 + mswz(k, cg) * 16);
 #pragma unroll
@@ -476,23 +525,25 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
       }
     }
 #pragma unroll
-    for (int ks = 0; ks < 64; ks += 32) {
+    for (int ks = 0; ks < BK; ks += 32) {
       bf16x8 a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        a[i] = AK ? frag_k_swz(cur, wm * 64 + i * 16, ks, lane) : frag_m_swz(cur, wm * 64 + i * 16, ks, lane);
+        a[i] = AK ? frag_k_swz<BK>(cur, wm * 64 + i * 16, ks, lane) : frag_m_swz(cur, wm * 64 + i * 16, ks, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        b[j] = BKM ? frag_k_swz(cur + GT, wn * 64 + j * 16, ks, lane) : frag_m_swz(cur + GT, wn * 64 + j * 16, ks, lane);
+        b[j] = BKM ? frag_k_swz<BK>(cur + GT, wn * 64 + j * 16, ks, lane)
+                   : frag_m_swz(cur + GT, wn * 64 + j * 16, ks, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
+    if (D::STAGES == 2) __syncthreads();
   }
-  gemm_epilogue<TC, MODE>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep);
+  if (D::STAGES == 1) __syncthreads();
+  gemm_epilogue<TC, MODE, D::HALVES>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep);
   if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab);
 }
 
@@ -537,6 +588,20 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, int S, int6
   hipLaunchKernelGGL((gemm_kernel<T, AKV, BKV, TC, MODEV>), GRID, dim3(NT), 0, s, M, N, K, a, lda, b, ldb, c, \
                      ldc, alpha, ep, kchunk, bslab)
 
+// DMA kernel configuration for a K extent (per split): RP_GEMM_CFG=0|1|2 forces one, for tuning
+static int rp_gemm_cfg(int64_t kext, int64_t n) {
+  static int forced = -2, policy = 0;
+  if (forced == -2) {
+    const char* e = getenv("RP_GEMM_CFG");
+    forced = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
+    const char* pe = getenv("RP_GEMM_POLICY");
+    policy = pe ? atoi(pe) : 0;
+  }
+  if (forced >= 0) return (forced == 2 || kext % 64 == 0) ? forced : 2;
+  if (kext % 64 != 0) return 2;
+  return (kext <= 1024 && n >= 1536 && policy == 1) ? 1 : 0;
+}
+
 static bool rp_dma_enabled() {
   static int v = -1;
   if (v < 0) {
@@ -555,13 +620,22 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
   const T* b = (const T*)B;
   TC* c = (TC*)Cp;
   if constexpr (std::is_same<T, bf16>::value) {
-    const bool full_k = K % 64 == 0 && (splits == 0 || kchunk % 64 == 0);
+    const bool full_k = K % 32 == 0 && (splits == 0 || kchunk % 32 == 0);
     if (full_k && rp_dma_enabled()) {
+      const int cfg = rp_gemm_cfg(splits == 0 ? K : kchunk, N);
       const bf16* ab = (const bf16*)A;
       const bf16* bb = (const bf16*)B;
-#define RP_DMA_LAUNCH(AKV, BKV, MODEV, GRID)                                                                       \
-  hipLaunchKernelGGL((gemm_bf16_dma_kernel<AKV, BKV, TC, MODEV>), GRID, dim3(NT), 0, s, M, N, K, ab, lda, bb, ldb, c, \
-                     ldc, alpha, ep, kchunk, bslab)
+#define RP_DMA_LAUNCH1(AKV, BKV, MODEV, CFGV, GRID)                                                        \
+  hipLaunchKernelGGL((gemm_bf16_dma_kernel<AKV, BKV, TC, MODEV, CFGV>), GRID, dim3(NT), 0, s, M, N, K, ab, lda, \
+                     bb, ldb, c, ldc, alpha, ep, kchunk, bslab)
+#define RP_DMA_LAUNCH(AKV, BKV, MODEV, GRID)                                  \
+  do {                                                                        \
+    switch (cfg) {                                                            \
+      case 0: RP_DMA_LAUNCH1(AKV, BKV, MODEV, 0, GRID); break;                \
+      case 1: RP_DMA_LAUNCH1(AKV, BKV, MODEV, 1, GRID); break;                \
+      default: RP_DMA_LAUNCH1(AKV, BKV, MODEV, 2, GRID); break;               \
+    }                                                                         \
+  } while (0)
       if (splits == 0) {
         dim3 grid((unsigned)tiles);
         if (ak && bk) RP_DMA_LAUNCH(true, true, 0, grid);
@@ -576,6 +650,7 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
         else RP_DMA_LAUNCH(false, true, 1, grid);
       }
 #undef RP_DMA_LAUNCH
+#undef RP_DMA_LAUNCH1
       return rp_check_launch("rp_gemm");
     }
   }

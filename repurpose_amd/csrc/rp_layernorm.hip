@@ -150,7 +150,7 @@ struct LnBwdDev {
   float* dx; int64_t lddx;
   void* dx_lp; int dx_lp_dtype; int64_t lddx_lp;
   uint32_t lp_thresh; float lp_scale; uint32_t lp_seed;
-  float* dgamma_part; float* dbeta_part;
+  float* dgamma_part; float* dbeta_part; int64_t ld_part;
 };
 
 template <int VPT>
@@ -228,8 +228,8 @@ __global__ __launch_bounds__(64 * LNB_WAVES) void ln_bwd_kernel(int64_t rows, Ln
       sg += red[0][k][c];
       sb += red[1][k][c];
     }
-    if (a.dgamma_part) a.dgamma_part[(int64_t)blockIdx.x * D + c] = sg;
-    if (a.dbeta_part) a.dbeta_part[(int64_t)blockIdx.x * D + c] = sb;
+    if (a.dgamma_part) a.dgamma_part[(int64_t)blockIdx.x * a.ld_part + c] = sg;
+    if (a.dbeta_part) a.dbeta_part[(int64_t)blockIdx.x * a.ld_part + c] = sb;
   }
 }
 
@@ -294,6 +294,8 @@ extern "C" int rp_layernorm_bwd(int64_t rows, int64_t D, const rp_ln_bwd_args* p
   a.lp_scale = p->dx_lp_dropout_p > 0.f ? 1.f / (1.f - p->dx_lp_dropout_p) : 1.f;
   a.lp_seed = p->dx_lp_seed;
   a.dgamma_part = p->dgamma_part; a.dbeta_part = p->dbeta_part;
+  a.ld_part = p->ld_part ? p->ld_part : D;
+  RP_REQUIRE(a.ld_part >= D, "rp_layernorm_bwd: ld_part < D");
   dim3 grid((unsigned)rp_layernorm_bwd_blocks(rows)), block(64 * LNB_WAVES);
   RP_LN_DISPATCH(ln_bwd_kernel, D, grid, block, (hipStream_t)stream, rows, a);
 }

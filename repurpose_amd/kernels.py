@@ -5,6 +5,7 @@ current torch stream through ``_native.call``.  Outputs are allocated with the t
 allocator; the library itself never allocates.  There is no CPU path: CPU tensors raise.
 """
 import ctypes
+import os
 
 import torch
 
@@ -171,15 +172,28 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, y=None, dropout_p=0.0, seed=0, dres=
     dx = torch.empty(rows, D, device=dev, dtype=torch.float32) if want_f32 else None
     dxl = torch.empty(rows, D, device=dev, dtype=lp_dtype) if lp_dtype is not None else None
     nb = N.load().rp_layernorm_bwd_blocks(rows)
-    pg = torch.empty(nb, D, device=dev, dtype=torch.float32) if dgamma is not None else None
-    pb = torch.empty(nb, D, device=dev, dtype=torch.float32) if dbeta is not None else None
+    # gamma / beta gradients adjacent in memory (a LayerNorm's weight and bias in the flat
+    # gradient buffer): interleave the partial rows [nb, 2D] and reduce both in one launch
+    both = (dgamma is not None and dbeta is not None and dgamma.is_contiguous() and dbeta.is_contiguous()
+            and dbeta.data_ptr() == dgamma.data_ptr() + 4 * D and dgamma.dtype == dbeta.dtype == torch.float32
+            and dgamma.untyped_storage().data_ptr() == dbeta.untyped_storage().data_ptr())
+    ld_part = 2 * D if both else D
+    if both:
+        part = torch.empty(nb, 2 * D, device=dev, dtype=torch.float32)
+        pg, pb = part[:, :D], part[:, D:]
+    else:
+        pg = torch.empty(nb, D, device=dev, dtype=torch.float32) if dgamma is not None else None
+        pb = torch.empty(nb, D, device=dev, dtype=torch.float32) if dbeta is not None else None
     a = N.LnBwdArgs(_p(dy).value, _dt(dy), dy.stride(0), _p(x).value, _dt(x), x.stride(0),
                     _p(mean).value, _p(rstd).value, _p(gamma).value, _p(y).value,
                     _dt(y) if y is not None else 0, y.stride(0) if y is not None else 0,
                     float(dropout_p), int(seed) & 0xFFFFFFFF, _p(dres).value, D, _p(dx).value, D,
                     _p(dxl).value, _dt(dxl) if dxl is not None else 0, D, float(lp_dropout_p),
-                    int(lp_seed) & 0xFFFFFFFF, _p(pg).value, _p(pb).value)
+                    int(lp_seed) & 0xFFFFFFFF, _p(pg).value, _p(pb).value, ld_part)
     N.call("rp_layernorm_bwd", rows, D, ctypes.byref(a), _stream(x))
+    if both:
+        colsum(part, out=dgamma.as_strided((2 * D,), (1,)), accumulate=True, ws=ws)
+        return dx, dxl
     if dgamma is not None:
         colsum(pg, out=dgamma, accumulate=True, ws=ws)
     if dbeta is not None:
@@ -221,6 +235,9 @@ def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0):
     return out, lse, mask
 
 
+_FUSED_DELTA = os.environ.get("RP_ATTN_FUSED_DELTA", "1") != "0"
+
+
 def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, dropmask=None):
     _gpu(qkv, out, dout, lse, key_valid, dropmask)
     _contig(qkv, out, dout, lse, key_valid)
@@ -231,15 +248,22 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
     delta = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
     st, dt = _stream(qkv), _dt(qkv)
     e0 = _tick("attn_bwd")
-    N.call("rp_attn_bwd_delta", dt, _p(out), _p(dout), B, T, H, dk, _p(delta), st)
+    if _FUSED_DELTA:  # dQ first, with the delta = rowsum(dO * O) pre-pass fused in; dK/dV reads it
+        e2 = _tick("attn_bwd_dq")
+        N.call("rp_attn_bwd_dq_delta", dt, _p(qkv), _p(out), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T,
+               H, dk, float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
+        _tock(e2)
+    else:
+        N.call("rp_attn_bwd_delta", dt, _p(out), _p(dout), B, T, H, dk, _p(delta), st)
     e1 = _tick("attn_bwd_dkdv")
     N.call("rp_attn_bwd_dkdv", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
            float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
     _tock(e1)
-    e2 = _tick("attn_bwd_dq")
-    N.call("rp_attn_bwd_dq", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
-           float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
-    _tock(e2)
+    if not _FUSED_DELTA:
+        e2 = _tick("attn_bwd_dq")
+        N.call("rp_attn_bwd_dq", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
+               float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
+        _tock(e2)
     _tock(e0)
     return dqkv
 

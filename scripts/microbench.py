@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--B", type=int, default=8)
     ap.add_argument("--T", type=int, default=2048)
+    ap.add_argument("--gemm", default="", help="only this GEMM shape (qkv|out_proj|linear1|linear2)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, T, H, d, dff = a.B, a.T, 8, 512, 2048
@@ -51,6 +52,8 @@ def main():
             res.append((f"attn_bwd p={p} (3 kernels)", t, 2 * fl / t / 1e9, "TFLOP/s alg"))
     if a.only in ("", "gemm"):
         for (n, k, name) in [(3 * d, d, "qkv"), (d, d, "out_proj"), (dff, d, "linear1"), (d, dff, "linear2")]:
+            if a.gemm and a.gemm != name:
+                continue
             x = torch.randn(M, k, generator=g).to(dev, bf)
             w = (torch.randn(n, k, generator=g) * 0.02).to(dev, bf)
             b = torch.zeros(n, device=dev)
