@@ -207,6 +207,17 @@ __device__ __forceinline__ uint32_t drop_masks(uint32_t seed_bh, uint32_t q, uin
   return (acc & 0xFFFFu) | (acc >> 16);
 }
 
+// Dropout select in the backward kernels: m ? a : b per bit for an all-ones / all-zero lane mask m
+// (the stored keep bit sign-extended by v_bfe_i32) as ONE gfx950 v_bitop3_b32 (truth table 0xCA =
+// S0 ? S1 : S2).  Written as C the compiler turns it into compare + cndmask (with the bit test
+// 3 VALU per element), or into and/xor/or once the mask is opaque.
+__device__ __forceinline__ uint32_t keep_mask(uint32_t w, int off) {
+  return (uint32_t)__builtin_amdgcn_sbfe((int)w, off, 1);
+}
+__device__ __forceinline__ float bfi_select(uint32_t m, float a, float b) {
+  return __uint_as_float(__builtin_amdgcn_bitop3_b32(m, __float_as_uint(a), __float_as_uint(b), 0xCA));
+}
+
 // =================================================================================================
 // forward
 // =================================================================================================
@@ -582,7 +593,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   auto load_rows = [&](int qs0) {
     if (tid < KV_QT) {
       const int q = qs0 + tid;
-      lse_r = q < Tq ? lse_bh[q] * LOG2E : INFINITY;  // +inf -> P = 0 for padded rows
+      // +inf -> P = 0 for padded rows; with dropout the 1/(1-p) scale rides in the exponent
+      lse_r = q < Tq ? lse_bh[q] * LOG2E - (DROP ? log2f(drop_scale) : 0.f) : INFINITY;
       del_r = q < Tq ? -del_bh[q] * inv_ds : 0.f;     // -delta/ds: the dP accumulators' start
     }
   };
@@ -678,15 +690,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
           const int bit = (ko >> 4) * 4 + (ko & 3);
           uint2 bits = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
           if constexpr (DROP) bits = *reinterpret_cast<const uint2*>(mw + mrow_l * KV_QT + qrow);
-          const uint32_t wd[4] = {bits.x & 0xFFFFu, bits.x >> 16, bits.y & 0xFFFFu, bits.y >> 16};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = rp_exp2(fmaf(s[qq][kt][r], c, -lq[r]));
+            const float p = rp_exp2(fmaf(s[qq][kt][r], c, -lq[r]));  // with dropout: p * ds
             if constexpr (DROP) {  // dS = p*(keep*ds*dP - delta) = p*ds*(keep ? acc : -delta/ds)
-              const bool keep = (wd[r] >> bit) & 1u;
-              const float pds = p * drop_scale;
-              s[qq][kt][r] = keep ? pds : 0.f;
-              dp[qq][kt][r] = pds * (keep ? dp[qq][kt][r] : ndq[qq][r]);
+              const uint32_t km = keep_mask(r < 2 ? bits.x : bits.y, bit + 16 * (r & 1));
+              s[qq][kt][r] = bfi_select(km, p, 0.f);
+              dp[qq][kt][r] = p * bfi_select(km, dp[qq][kt][r], ndq[qq][r]);
             } else {
               s[qq][kt][r] = p;
               dp[qq][kt][r] = p * dp[qq][kt][r];
@@ -795,7 +805,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + qt * 16 + i;
-    lq[qt] = q < Tq ? lse[(int64_t)bh * Tq + q] * LOG2E : INFINITY;
+    // with dropout the 1/(1-p) scale rides in the exponent: exp2(S*c - lq) = p * ds
+    lq[qt] = q < Tq ? lse[(int64_t)bh * Tq + q] * LOG2E - (DROP ? log2f(drop_scale) : 0.f) : INFINITY;
     if constexpr (!DELTA)
       dq[qt] = q < Tq ? -delta[(int64_t)bh * Tq + q] * (DROP ? 1.f / drop_scale : 1.f) : 0.f;  // -delta/ds
     float part = 0.f;  // DELTA: this lane's share of rowsum(dO * O)
@@ -921,10 +932,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = rp_exp2(fmaf(s[kt][qt][r], c, -lq[qt]));
+          const float p = rp_exp2(fmaf(s[kt][qt][r], c, -lq[qt]));  // with dropout: p * ds
           if constexpr (DROP) {
-            const bool keep = (kwd[qt] >> (4 * kt + r)) & 1u;
-            s[kt][qt][r] = (p * drop_scale) * (keep ? dp[kt][qt][r] : dq[qt]);
+            const uint32_t km = keep_mask(kwd[qt], 4 * kt + r);
+            s[kt][qt][r] = p * bfi_select(km, dp[kt][qt][r], dq[qt]);
           } else {
             s[kt][qt][r] = p * dp[kt][qt][r];
           }
