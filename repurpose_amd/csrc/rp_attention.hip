@@ -562,10 +562,20 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       const int k = kw0 + kt * 16 + i;
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        ks_[kt][s] = k < Tk ? (float)Kg[(int64_t)k * ldk + 4 * s + g] : 0.f;
+        ks_[kt][s] = k < Tk ? (float)Kg[(int64_t)k * ldk + 4 * s + g] * c : 0.f;
         vs_[kt][s] = k < Tk ? (float)Vg[(int64_t)k * ldv + 4 * s + g] : 0.f;
       }
     }
+  }
+  // K enters S = Q K^T prescaled by c = scale*log2(e) (once per workgroup; K feeds no other
+  // product here), so with S starting at -lse*log2(e) the probability is exp2 of the accumulator
+  if constexpr (BF) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kf[kt][s2][j] = (bf16)((float)kf[kt][s2][j] * c);
   }
 
   f32x4 dk[2][4], dv[2][4];
@@ -593,8 +603,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   auto load_rows = [&](int qs0) {
     if (tid < KV_QT) {
       const int q = qs0 + tid;
-      // +inf -> P = 0 for padded rows; with dropout the 1/(1-p) scale rides in the exponent
-      lse_r = q < Tq ? lse_bh[q] * LOG2E - (DROP ? log2f(drop_scale) : 0.f) : INFINITY;
+      // the S accumulators' start, -lse*log2(e) (-inf -> P = 0 for padded rows); with dropout the
+      // 1/(1-p) scale rides in the exponent
+      lse_r = q < Tq ? -(lse_bh[q] * LOG2E - (DROP ? log2f(drop_scale) : 0.f)) : -INFINITY;
       del_r = q < Tq ? -del_bh[q] * inv_ds : 0.f;     // -delta/ds: the dP accumulators' start
     }
   };
@@ -642,9 +653,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
         ndq[qq] = *reinterpret_cast<const f32x4*>(drow + (2 * hf + qq) * 16 + 4 * g);
+        const f32x4 nl = *reinterpret_cast<const f32x4*>(lrow + (2 * hf + qq) * 16 + 4 * g);
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
-          s[qq][kt] = zero4();
+          s[qq][kt] = nl;
           dp[qq][kt] = ndq[qq];
         }
       }
@@ -680,8 +692,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
         const int qrow = (2 * hf + qq) * 16 + 4 * g;
-        const float4 lq4 = *reinterpret_cast<const float4*>(lrow + qrow);
-        const float lq[4] = {lq4.x, lq4.y, lq4.z, lq4.w};
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
           // this lane's key: ko = key % 64 -> word row (tile half, group (ko%16)/4), bit (ko/16)*4 + ko%4
@@ -692,7 +702,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
           if constexpr (DROP) bits = *reinterpret_cast<const uint2*>(mw + mrow_l * KV_QT + qrow);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = rp_exp2(fmaf(s[qq][kt][r], c, -lq[r]));  // with dropout: p * ds
+            const float p = rp_exp2(s[qq][kt][r]);  // with dropout: p * ds
             if constexpr (DROP) {  // dS = p*(keep*ds*dP - delta) = p*ds*(keep ? acc : -delta/ds)
               const uint32_t km = keep_mask(r < 2 ? bits.x : bits.y, bit + 16 * (r & 1));
               s[qq][kt][r] = bfi_select(km, p, 0.f);
@@ -838,6 +848,23 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     }
   }
 
+  // Q enters S^T = K Q^T prescaled by c = scale*log2(e) (Q feeds no other product here), so with
+  // S^T starting at -lse*log2(e) (+ the key bias) the probability is exp2 of the accumulator
+  float nlq[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    nlq[qt] = -lq[qt];
+    if constexpr (BF) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qt][s2][j] = (bf16)((float)qf[qt][s2][j] * c);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) qs[qt][s2] *= c;
+    }
+  }
+
   f32x4 dqa[2][4];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
@@ -851,7 +878,11 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
   };
   auto stage_mask = [&](char* buf, bool ok) {
     float* kbm = reinterpret_cast<float*>(buf + 2 * TILE);
-    if (w == 0) kbm[lane] = ok ? 0.f : -INFINITY;  // key bias: the S^T accumulators' start
+    if (w == 0) {
+      kbm[lane] = ok ? 0.f : -INFINITY;  // key bias, added to the S^T accumulators' start
+      const unsigned long long bal = __ballot(ok);
+      if (lane == 0) *reinterpret_cast<int*>(buf + 2 * TILE + FW_KT * 4) = bal == ~0ull;  // no masked key
+    }
   };
   const int nkt = (Tk + FW_KT - 1) / FW_KT;
   sk.load(Kg, ldk, 0, Tk, tid);
@@ -886,16 +917,25 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     const float* kbias = reinterpret_cast<const float*>(cur + 2 * TILE);
 
     // S^T[key][q] = K Q^T, dP^T[key][q] = V dO^T : row key = kt*16 + 4g + r, col q = qt*16 + i.
-    // Row constants as the initial accumulators: S^T starts at the key bias (0 / -inf: masked keys
-    // give P = 0 with no select), dP^T at -delta/ds.
+    // Row / column constants as the initial accumulators: S^T starts at -lse*log2(e) plus the key
+    // bias (0 / -inf: masked keys give P = 0 with no select; added only on tiles with a masked
+    // key), dP^T at -delta/ds.
+    const bool full = *reinterpret_cast<const int*>(cur + 2 * TILE + FW_KT * 4) != 0;
     f32x4 s[4][2], dp[4][2];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      const f32x4 kb4 = *reinterpret_cast<const f32x4*>(kbias + kt * 16 + 4 * g);
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        s[kt][qt] = kb4;
+        s[kt][qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
         dp[kt][qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
+      }
+    }
+    if (!full) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const f32x4 kb4 = *reinterpret_cast<const f32x4*>(kbias + kt * 16 + 4 * g);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) s[kt][qt] += kb4;
       }
     }
     if constexpr (BF) {
@@ -932,7 +972,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = rp_exp2(fmaf(s[kt][qt][r], c, -lq[qt]));  // with dropout: p * ds
+          const float p = rp_exp2(s[kt][qt][r]);  // with dropout: p * ds
           if constexpr (DROP) {
             const uint32_t km = keep_mask(kwd[qt], 4 * kt + r);
             s[kt][qt][r] = p * bfi_select(km, dp[kt][qt][r], dq[qt]);
