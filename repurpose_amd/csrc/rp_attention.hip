@@ -249,7 +249,6 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   const int q0 = qb * FW_QB + w * 32;  // this wave's first query
   const uint32_t seed_bh = rp_hash(a.seed, (uint32_t)bh);
   const float c = scale * LOG2E;
-  const float rth = RESCALE_LOG2 / c;  // deferred-rescale threshold in score units
   const int KT = mask_kt(Tk);
   const int64_t ldm = mask_ld(Tq);
   uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
@@ -272,12 +271,30 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     }
   }
 
+  // Q enters S^T = K Q^T prescaled by c = scale*log2(e) (log2-domain scores), and the S^T
+  // accumulators start at -m, the running reference max: P = exp2(acc) needs no per-score op
+  // unless the reference moves on this tile.
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    if constexpr (BF) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qt][s2][j] = (bf16)((float)qf[qt][s2][j] * c);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) qs[qt][s2] *= c;
+    }
+  }
+
   f32x4 o[2][4];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[qt][dt] = zero4();
-  float m[2] = {-INFINITY, -INFINITY}, lp[2] = {0.f, 0.f};
+  // m: reference max (log2 units) once set (mset); 0 before, when O and l are still zero
+  float m[2] = {0.f, 0.f}, lp[2] = {0.f, 0.f};
+  bool mset[2] = {false, false};
 
   Stage<T, FW_KT> sk, sv;
   const int nkt = (Tk + FW_KT - 1) / FW_KT;
@@ -318,12 +335,12 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     const float* kbias = reinterpret_cast<const float*>(cur + 2 * TILE);
     const bool full = *reinterpret_cast<const int*>(cur + 2 * TILE + FW_KT * 4) != 0;
 
-    // ---- S^T[key][q] = K Q^T ----
+    // ---- S^T[key][q] = K (cQ)^T - m ----
     f32x4 s[4][2];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) s[kt][qt] = zero4();
+      for (int qt = 0; qt < 2; ++qt) s[kt][qt] = f32x4{-m[qt], -m[qt], -m[qt], -m[qt]};
     if constexpr (BF) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
@@ -343,11 +360,11 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
           for (int qt = 0; qt < 2; ++qt) s[kt][qt] = mfma_f32(kf, qs[qt][ss], s[kt][qt]);
         }
     }
-    // ---- mask (only tiles with masked keys) + column max ----
-    // Deferred rescale: the running reference m only moves when the tile max exceeds it by more
-    // than RESCALE_LOG2 (P <= 2^8 meanwhile, exact in fp32/bf16 range); l and O share the
-    // reference, so out = O / l is unchanged and the lse uses the same m.
-    float mnew[2];
+    // ---- mask (only tiles with masked keys) + column max, relative to the reference ----
+    // Deferred rescale: the reference m only moves when the tile max exceeds it by more than
+    // RESCALE_LOG2 (P <= 2^8 meanwhile, exact in fp32/bf16 range), or on the first finite max;
+    // l and O share the reference, so out = O / l is unchanged and the lse uses the same m.
+    float rel[2];
     bool grow = false;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -362,30 +379,32 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][qt][r]);
-      mx = quad_max(mx);
-      mnew[qt] = mx;
-      grow |= mx > m[qt] + rth;  // no NaN anywhere: m = -inf -> grows iff mx finite
+      rel[qt] = quad_max(mx);
+      grow |= mset[qt] ? rel[qt] > RESCALE_LOG2 : rel[qt] > -INFINITY;  // no NaN anywhere
     }
-    if (__any(grow)) {  // wave-uniform branch, per-lane update
+    if (__any(grow)) {  // wave-uniform branch: move the reference of the growing lanes
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        const bool gq = mnew[qt] > m[qt] + rth;
-        const float alpha = gq ? rp_exp2((m[qt] - mnew[qt]) * c) : 1.f;  // m = -inf -> 0
+        const bool gq = mset[qt] ? rel[qt] > RESCALE_LOG2 : rel[qt] > -INFINITY;
+        const float alpha = gq ? (mset[qt] ? rp_exp2(-rel[qt]) : 0.f) : 1.f;
+        const float sub = gq ? rel[qt] : 0.f;
         lp[qt] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
-        m[qt] = gq ? mnew[qt] : m[qt];
+        m[qt] += sub;
+        mset[qt] = mset[qt] || gq;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) s[kt][qt] -= sub;
       }
     }
-    // ---- P = exp2(S*c - m*c); per-lane partial row sums (before dropout), tree order ----
+    // ---- P = exp2(acc); per-lane partial row sums (before dropout), tree order ----
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-      const float mc = (m[qt] == -INFINITY ? 0.f : m[qt]) * c;
       float t4[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[kt][qt][r] = rp_exp2(fmaf(s[kt][qt][r], c, -mc));
+        for (int r = 0; r < 4; ++r) s[kt][qt][r] = rp_exp2(s[kt][qt][r]);
         t4[kt] = (s[kt][qt][0] + s[kt][qt][1]) + (s[kt][qt][2] + s[kt][qt][3]);
       }
       lp[qt] += (t4[0] + t4[1]) + (t4[2] + t4[3]);
@@ -478,7 +497,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 #pragma unroll
         for (int r = 0; r < 4; ++r) rp_st(orow + dt * 16 + 4 * g + r, o[qt][dt][r] * inv);
     }
-    if (g == 0) lse[(int64_t)bh * Tq + q] = m[qt] * scale + logf(l);
+    if (g == 0) lse[(int64_t)bh * Tq + q] = m[qt] * 0.6931471805599453f + logf(l);  // m: log2 units
   }
 }
 
