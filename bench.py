@@ -126,10 +126,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ranks map to GPUs one to one; RP_DIST_BACKEND=gloo and more ranks than GPUs (ranks sharing a
+    # device) exist only to rehearse the multi-process path on a one-GPU box
+    ndev = max(1, torch.cuda.device_count())
+    gpu = local % ndev
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(gpu)
+        backend = os.environ.get("RP_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu if world > 1 else 0)
 
     from repurpose_amd import kernels as K
     from repurpose_amd.MMCTransformer import MMCTransformer

@@ -105,8 +105,12 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_fwd_kernel(int64_t rows, LnF
   if (row >= rows) return;
   constexpr int D = VPT * 64;
   const int c0 = lane * VPT;
-  float v[VPT];
+  float v[VPT], pe[VPT], gm[VPT], bt[VPT];
   load_row<VPT>(v, a.x, a.x_dtype, row * a.ldx + c0);
+  // the row-independent operands are issued with the row load, not after the reductions
+  if (a.pe) load_row<VPT>(pe, a.pe, RP_F32, (row % a.pe_period) * D + c0);
+  load_row<VPT>(gm, a.gamma, RP_F32, c0);
+  load_row<VPT>(bt, a.beta, RP_F32, c0);
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) s += v[i];
@@ -119,10 +123,6 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_fwd_kernel(int64_t rows, LnF
   }
   const float var = rp_wave_sum(q) * (1.f / D);
   const float rstd = rsqrtf(var + a.eps);
-  float pe[VPT], gm[VPT], bt[VPT];
-  if (a.pe) load_row<VPT>(pe, a.pe, RP_F32, (row % a.pe_period) * D + c0);
-  load_row<VPT>(gm, a.gamma, RP_F32, c0);
-  load_row<VPT>(bt, a.beta, RP_F32, c0);
   const uint32_t kb = a.drop_thresh ? rp_keep_bits<VPT>(a.drop_seed, (uint32_t)(row * D + c0), a.drop_thresh) : 0u;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
@@ -172,14 +172,14 @@ __global__ __launch_bounds__(64 * LNB_WAVES) void ln_bwd_kernel(int64_t rows, Ln
     load_row<VPT>(g, a.dy, a.dy_dtype, row * a.lddy + c0);
     load_row<VPT>(x, a.x, a.x_dtype, row * a.ldx + c0);
     if (a.dres) load_row<VPT>(r, a.dres, RP_F32, row * a.lddres + c0);  // issued with the other loads
+    float yv[VPT];
+    if (a.y) load_row<VPT>(yv, a.y, a.y_dtype, row * a.ldy + c0);
     if (a.drop_thresh) {
       const uint32_t kb = rp_keep_bits<VPT>(a.drop_seed, (uint32_t)(row * D + c0), a.drop_thresh);
 #pragma unroll
       for (int i = 0; i < VPT; ++i) g[i] = ((kb >> i) & 1u) ? g[i] * a.drop_scale : 0.f;
     }
     if (a.y) {
-      float yv[VPT];
-      load_row<VPT>(yv, a.y, a.y_dtype, row * a.ldy + c0);
 #pragma unroll
       for (int i = 0; i < VPT; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
     }
