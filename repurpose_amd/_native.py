@@ -105,7 +105,7 @@ def load(path=None):
     global _lib, _load_error
     if _lib is not None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("RP_LIB_PATH") or LIB_PATH  # RP_LIB_PATH: A/B builds for tuning
     try:
         lib = ctypes.CDLL(p)
     except OSError as e:  # no silent fallback: the HIP library is the product
