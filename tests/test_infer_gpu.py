@@ -115,3 +115,18 @@ def test_inference_end_to_end_matches_oracle_postprocess(dev):
         assert r["video_id"] == e["video_id"]
         assert r["labels"].cpu().tolist() == e["labels"].tolist()
         np.testing.assert_allclose(r["segments"].cpu().numpy(), e["segments"].numpy())
+
+
+def test_val_split_atiou_matches_cpu_reference(dev):
+    """North-star check on the reference's own validation labels (tests/golden/val_labels_64.json)
+    with synthetic features: GPU inference_ + GPU tIoU vs the CPU restatement + calculate_tiou —
+    identical proposals and AtIoU (the bar is +-0.1).  L = 2 keeps the CPU side fast; the L = 16
+    run is scripts/val_atiou.py (profiles/)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import val_atiou
+    r = val_atiou.run(videos=12, layers=2, threads=8)
+    assert r["identical_proposals"], r
+    assert r["abs_diff"] < 1e-12, r
+    assert r["proposals_gpu"] > 0 and r["gt_segments"] > 0
