@@ -49,7 +49,7 @@ def main():
             t = timeit(lambda: K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 1), a.reps)
             res.append((f"attn_fwd p={p}", t, fl / t / 1e9, "TFLOP/s"))
             t = timeit(lambda: K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, 1, *extra), a.reps)
-            res.append((f"attn_bwd p={p} (3 kernels)", t, 2 * fl / t / 1e9, "TFLOP/s alg"))
+            res.append((f"attn_bwd p={p} (dQ+delta, dK/dV)", t, 2 * fl / t / 1e9, "TFLOP/s alg"))
     if a.only in ("", "gemm"):
         for (n, k, name) in [(3 * d, d, "qkv"), (d, d, "out_proj"), (dff, d, "linear1"), (d, dff, "linear2")]:
             if a.gemm and a.gemm != name:
