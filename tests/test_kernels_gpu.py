@@ -402,3 +402,57 @@ def test_attention_bwd_fused_delta_matches_unfused(dev, dtype, p):
         assert torch.isfinite(dqkv).all()
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     close(outs[0][0], outs[1][0].double(), atol=tol, rtol=tol, what="fused vs unfused dqkv")
+
+
+# ------------------------------------------------------------------- metric-shape (full size) checks
+def test_gemm_metric_shapes_bf16(dev):
+    """Every Linear of an encoder layer at the bench shape (M = B*T = 16384 tokens): fwd, dgrad and
+    the split-K wgrad against an fp64 torch product of the same bf16 operands."""
+    M = 16384
+    for (n, k) in [(1536, 512), (512, 512), (2048, 512), (512, 2048)]:
+        x = rnd(M, k, dev=dev, seed=n + k).to(torch.bfloat16)
+        w = rnd(n, k, dev=dev, seed=n * k, scale=0.05).to(torch.bfloat16)
+        b = rnd(n, dev=dev, seed=3)
+        y = K.linear_fwd(x, w, b, out_dtype=torch.float32)
+        close(y, x.double() @ w.double().T + b.double(), atol=2e-3 * math.sqrt(k), what=f"fwd {n}x{k}")
+        dy = rnd(M, n, dev=dev, seed=n - k).to(torch.bfloat16)
+        close(K.linear_dgrad(dy, w, out_dtype=torch.float32), dy.double() @ w.double(), atol=2e-3 * math.sqrt(n),
+              what=f"dgrad {n}x{k}")
+        dW = torch.zeros(n, k, device=dev)
+        db = torch.zeros(n, device=dev)
+        K.linear_wgrad(dy, x, dW, db=db)
+        close(dW, dy.double().T @ x.double(), atol=4e-3 * math.sqrt(M), what=f"wgrad {n}x{k}")
+        close(db, dy.double().sum(0), atol=1e-3 * math.sqrt(M), what=f"bias grad {n}")
+
+
+def test_attention_metric_shape_bf16_dropout(dev):
+    """Attention at the bench shape (B = 8, T = 2048, H = 8, dk = 64) with dropout 0.1 and ragged key
+    padding: forward output and all three gradients against an fp64 torch restatement (same bf16
+    inputs, the restated keep bits) on a sample of 2 (batch, head) pairs."""
+    B, T, H = 8, 2048, 8
+    qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=21).to(torch.bfloat16)
+    lens = torch.tensor([T, T - 1, 1900, 1537, T, 1024, 2047, 64], device=dev)
+    kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
+    p, seed = 0.1, 777
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed)
+    do = rnd(B * T, H * 64, dev=dev, seed=22).to(torch.bfloat16)
+    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask)
+    keep_all = attn_keep(B, H, T, p, seed, dev)                       # [B, H, T, T]
+    q, k, v = qkv.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)        # [B, H, T, 64]
+    dq, dk, dv = dqkv.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    og = o.view(B, T, H, 64).permute(0, 2, 1, 3)
+    dog = do.view(B, T, H, 64).permute(0, 2, 1, 3)
+    for (bb, hh) in [(3, 5), (6, 0)]:
+        qd, kd, vd = (t[bb, hh].double().requires_grad_(True) for t in (q, k, v))
+        s = (qd @ kd.T) * 0.125
+        s = s.masked_fill(~kv[bb].bool()[None, :], float("-inf"))
+        P = torch.softmax(s, -1)
+        P = torch.where(keep_all[bb, hh], P / (1 - p), torch.zeros_like(P))
+        ref = P @ vd
+        close(og[bb, hh], ref.detach(), atol=2e-2, rtol=2e-2, what=f"fwd b{bb} h{hh}")
+        gq, gk, gv = torch.autograd.grad(ref, (qd, kd, vd), dog[bb, hh].double())
+        valid = kv[bb].bool()
+        close(dq[bb, hh], gq, atol=6e-2, rtol=6e-2, what=f"dq b{bb} h{hh}")
+        close(dk[bb, hh][valid], gk[valid], atol=6e-2, rtol=6e-2, what=f"dk b{bb} h{hh}")
+        close(dv[bb, hh][valid], gv[valid], atol=6e-2, rtol=6e-2, what=f"dv b{bb} h{hh}")
+        assert torch.count_nonzero(dk[bb, hh][~valid]) == 0 and torch.count_nonzero(dv[bb, hh][~valid]) == 0
