@@ -9,7 +9,10 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Wall -Wno-unu
 
 # attention: no NaN semantics needed (scores are finite or -inf), drops the canonicalising
 # v_max before every fmaxf of an MFMA result
-build/rp_attention.o: EXTRA := -fno-honor-nans
+# -fno-slp-vectorize: no v_pk_*_f32 packing of the softmax / row-sum VALU, which issues beside the
+# MFMAs at a higher cost than the scalar pairs (MI355X attention microbench: fwd 162.6 -> 153.1 us,
+# bwd 310.8 -> 305.1 us at p = 0.1)
+build/rp_attention.o: EXTRA := -fno-honor-nans -fno-slp-vectorize
 
 all: $(LIB)
 

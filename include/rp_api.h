@@ -177,10 +177,10 @@ int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ldx,
  * qkv: [B*T, 3*H*dk] rows = (q heads | k heads | v heads), dk == 64.
  * key_valid: [B, T] uint8 (0 -> key masked with -inf, torch key_padding_mask semantics).
  * out: [B*T, H*dk];  lse: [B, H, T] fp32 (natural-log sum-exp of scaled scores).
- * Dropout on the attention probabilities with probability p (KT = ceil(T/64)): for query q, key
- * tile t and group g the state st = rp_hash(rp_hash(seed, b*H+h), (q*KT + t)*4 + g) is advanced by
- * xorshift32 (x ^= x<<13; x ^= x>>17; x ^= x<<5) eight times; word j (1..8th) holds the keys
- * 64t + 16*(j>>1) + 4g + 2*(j&1) + {0: low 16 bits, 1: high 16 bits}; a key is kept iff its 16 bits
+ * Dropout on the attention probabilities with probability p: for query q and group g one stream
+ * st = rp_hash(rp_hash(seed, b*H+h), q*4 + g) is advanced by xorshift32 (x ^= x<<13; x ^= x>>17;
+ * x ^= x<<5) eight times per 64-key tile, tiles in order; in tile t word j (1..8th of the tile)
+ * holds the keys 64t + 16*(j>>1) + 4g + 2*(j&1) + {0: low 16 bits, 1: high 16 bits}; a key is kept iff its 16 bits
  * read as int16 are >= round(p*65536) - 32768 (rp_hash: repurpose_amd/csrc/rp_common.h).
  * The forward writes the keep bits to `dropmask` (uint16 [B*H][ceil(T/64)][4][roundup(T,64)],
  * bit (kt*4 + r) of word (bh, tile, g, q) = keep(q, 64*tile + 16*kt + 4*g + r);

@@ -178,17 +178,16 @@ __device__ __forceinline__ float quad_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-// Attention dropout stream (include/rp_api.h, rp_attn_fwd): for query q, key tile `tile` and lane
-// group g (keys 64*tile + 16*kt + 4*g + r, kt, r in 0..3) the state st = rp_hash(seed_bh,
-// (q*KT + tile)*4 + g) is advanced by xorshift32 eight times; word j covers keys
-// (kt = j>>1, r = 2*(j&1) + {0: low half, 1: high half}); a key is kept iff its half, read as a signed
-// 16-bit integer, is >= round(p*65536) - 32768 (probability 1 - p, exact to 2^-16).
+// Attention dropout stream (include/rp_api.h, rp_attn_fwd): for query q and lane group g one
+// xorshift32 stream runs over the whole key range: st = rp_hash(seed_bh, q*4 + g), then eight
+// xorshift32 steps per 64-key tile, in tile order; in tile `tile` word j covers keys
+// 64*tile + 16*(j>>1) + 4*g + r with r = 2*(j&1) + {0: low half, 1: high half}; a key is kept iff its
+// half, read as a signed 16-bit integer, is >= round(p*65536) - 32768 (probability 1 - p, exact to
+// 2^-16).  One seeding hash per (query, lane group) per launch, carried across tiles in a register.
 // Outputs dm[j] (0xFFFF in each dropped half: the AND-NOT mask of the packed bf16 P pair) and
 // returns the 16 keep bits, bit (kt*4 + r).  Full-rate VALU only: a saturating packed 16-bit
-// subtract + arithmetic shift per pair, no 32-bit multiplies beyond the one seeding hash.
-__device__ __forceinline__ uint32_t drop_masks(uint32_t seed_bh, uint32_t q, uint32_t KT, uint32_t tile, uint32_t g,
-                                               uint32_t thr, uint32_t dm[8]) {
-  uint32_t st = rp_hash(seed_bh, (q * KT + tile) * 4u + g);
+// subtract + arithmetic shift per pair, no 32-bit multiplies in the tile loop.
+__device__ __forceinline__ uint32_t drop_masks(uint32_t& st, uint32_t thr, uint32_t dm[8]) {
   const short ts = (short)((int)thr - 32768);
   const i16x2 t2 = {ts, ts};
   uint32_t acc = 0u;
@@ -295,6 +294,12 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   // m: reference max (log2 units) once set (mset); 0 before, when O and l are still zero
   float m[2] = {0.f, 0.f}, lp[2] = {0.f, 0.f};
   bool mset[2] = {false, false};
+  // dropout stream state of this lane's two queries (carried across the key tiles)
+  uint32_t dst[2] = {0u, 0u};
+  if constexpr (DROP) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) dst[qt] = rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g);
+  }
 
   Stage<T, FW_KT> sk, sv;
   const int nkt = (Tk + FW_KT - 1) / FW_KT;
@@ -415,7 +420,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         const int q = q0 + qt * 16 + i;
-        const uint32_t word = drop_masks(seed_bh, (uint32_t)q, (uint32_t)KT, (uint32_t)kt_i, (uint32_t)g, drop_thresh, dm[qt]);
+        const uint32_t word = drop_masks(dst[qt], drop_thresh, dm[qt]);
         if (q < Tq) mrow[((int64_t)kt_i * 4 + g) * ldm + q] = (uint16_t)word;
       }
     }
@@ -668,18 +673,14 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
     for (int hf = 0; hf < 2; ++hf) {
       // S[q][key], dP[q][key]: C-layout row q = (2hf+qq)*16 + 4g + r, col key = kt*16 + i
       // dP starts at -delta/ds (row constant as the initial accumulator): dS = p*ds*acc
-      f32x4 s[2][2], dp[2][2], ndq[2];
+      f32x4 s[2][2], dp[2][2], ndq[2], nl[2];
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
         ndq[qq] = *reinterpret_cast<const f32x4*>(drow + (2 * hf + qq) * 16 + 4 * g);
-        const f32x4 nl = *reinterpret_cast<const f32x4*>(lrow + (2 * hf + qq) * 16 + 4 * g);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          s[qq][kt] = nl;
-          dp[qq][kt] = ndq[qq];
-        }
+        nl[qq] = *reinterpret_cast<const f32x4*>(lrow + (2 * hf + qq) * 16 + 4 * g);
       }
       if constexpr (BF) {
+        // the row constants enter as the first MFMA's C operand (no register copies)
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
 #pragma unroll
@@ -688,11 +689,18 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
             bf16x8 da = row_frag_lds(dOl, (2 * hf + qq) * 16, ss * 32, lane);
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt) {
-              s[qq][kt] = mfma_bf16(qa, kf[kt][ss], s[qq][kt]);
-              dp[qq][kt] = mfma_bf16(da, vf[kt][ss], dp[qq][kt]);
+              s[qq][kt] = mfma_bf16(qa, kf[kt][ss], ss == 0 ? nl[qq] : s[qq][kt]);
+              dp[qq][kt] = mfma_bf16(da, vf[kt][ss], ss == 0 ? ndq[qq] : dp[qq][kt]);
             }
           }
       } else {
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            s[qq][kt] = nl[qq];
+            dp[qq][kt] = ndq[qq];
+          }
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
 #pragma unroll
@@ -941,23 +949,15 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     // key), dP^T at -delta/ds.
     const bool full = *reinterpret_cast<const int*>(cur + 2 * TILE + FW_KT * 4) != 0;
     f32x4 s[4][2], dp[4][2];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
+    if constexpr (BF) {
+      // the constants enter as the first MFMA's C operand (no per-tile register copies); the key
+      // bias is added after the chain (0 + x == x, -inf + x == -inf: same values as adding it first)
+      f32x4 s0[2], d0[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        s[kt][qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
-        dp[kt][qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
+        s0[qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
+        d0[qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
       }
-    }
-    if (!full) {
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const f32x4 kb4 = *reinterpret_cast<const f32x4*>(kbias + kt * 16 + 4 * g);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) s[kt][qt] += kb4;
-      }
-    }
-    if constexpr (BF) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -966,11 +966,35 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
           bf16x8 va = row_frag_lds(Vl, kt * 16, ss * 32, lane);
 #pragma unroll
           for (int qt = 0; qt < 2; ++qt) {
-            s[kt][qt] = mfma_bf16(ka, qf[qt][ss], s[kt][qt]);
-            dp[kt][qt] = mfma_bf16(va, df[qt][ss], dp[kt][qt]);
+            s[kt][qt] = mfma_bf16(ka, qf[qt][ss], ss == 0 ? s0[qt] : s[kt][qt]);
+            dp[kt][qt] = mfma_bf16(va, df[qt][ss], ss == 0 ? d0[qt] : dp[kt][qt]);
           }
         }
+      if (!full) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+          const f32x4 kb4 = *reinterpret_cast<const f32x4*>(kbias + kt * 16 + 4 * g);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt) s[kt][qt] += kb4;
+        }
+      }
     } else {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          s[kt][qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
+          dp[kt][qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
+        }
+      }
+      if (!full) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+          const f32x4 kb4 = *reinterpret_cast<const f32x4*>(kbias + kt * 16 + 4 * g);
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt) s[kt][qt] += kb4;
+        }
+      }
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll

@@ -162,21 +162,24 @@ def test_layernorm_relu_dropout(dev):
 # ----------------------------------------------------------------------------------- attention
 def attn_keep(B, H, T, p, seed, dev):
     """torch restatement of the attention dropout bits (include/rp_api.h, rp_attn_fwd): per (query,
-    key tile, lane group g) an xorshift32 stream seeded by rp_hash; 16-bit halves read as int16."""
+    lane group g) one xorshift32 stream seeded by rp_hash, eight words per 64-key tile in tile order;
+    16-bit halves read as int16."""
     KT = (T + 63) // 64
     bh = torch.arange(B * H, device=dev, dtype=torch.int64)
-    sbh = rp_hash(seed, bh).view(B * H, 1, 1, 1)
-    q = torch.arange(T, device=dev, dtype=torch.int64).view(1, T, 1, 1)
-    tile = torch.arange(KT, device=dev, dtype=torch.int64).view(1, 1, KT, 1)
-    g = torch.arange(4, device=dev, dtype=torch.int64).view(1, 1, 1, 4)
-    st = rp_hash(sbh, (q * KT + tile) * 4 + g)                 # [BH, T, KT, 4]
-    words = []
-    for _ in range(8):
-        st = (st ^ (st << 13)) & M32
-        st = st ^ (st >> 17)
-        st = (st ^ (st << 5)) & M32
-        words.append(st)
-    w = torch.stack(words, -1)                                  # [BH, T, KT, g, j]
+    sbh = rp_hash(seed, bh).view(B * H, 1, 1)
+    q = torch.arange(T, device=dev, dtype=torch.int64).view(1, T, 1)
+    g = torch.arange(4, device=dev, dtype=torch.int64).view(1, 1, 4)
+    st = rp_hash(sbh, q * 4 + g)                                # [BH, T, 4]
+    tiles = []
+    for _ in range(KT):
+        words = []
+        for _ in range(8):
+            st = (st ^ (st << 13)) & M32
+            st = st ^ (st >> 17)
+            st = (st ^ (st << 5)) & M32
+            words.append(st)
+        tiles.append(torch.stack(words, -1))                    # [BH, T, g, j]
+    w = torch.stack(tiles, 2)                                   # [BH, T, KT, g, j]
     half = torch.stack([w & 0xFFFF, w >> 16], -1)               # [BH, T, KT, g, j, lo/hi]
     sgn = torch.where(half >= 32768, half - 65536, half)
     keep = sgn >= int(p * 65536 + 0.5) - 32768
