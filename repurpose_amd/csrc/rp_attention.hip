@@ -34,6 +34,13 @@ constexpr int NT = NW * 64;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float RESCALE_LOG2 = 8.f;  // forward: deferred-rescale threshold (log2 units)
 
+// RP_ATTN_SETPRIO: raise the wave priority around each MFMA cluster (cdna_hip_programming.md T5)
+#ifdef RP_ATTN_SETPRIO
+#define RP_PRIO(x) __builtin_amdgcn_s_setprio(x)
+#else
+#define RP_PRIO(x) ((void)0)
+#endif
+
 template <typename T>
 struct AttnCfg {
   // bf16 tiles: 128-byte rows, XOR-swizzled (see lds_off); fp32 parity tiles: 16-byte row padding
@@ -347,6 +354,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) s[kt][qt] = f32x4{-m[qt], -m[qt], -m[qt], -m[qt]};
     if constexpr (BF) {
+      RP_PRIO(1);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -355,6 +363,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 #pragma unroll
           for (int qt = 0; qt < 2; ++qt) s[kt][qt] = mfma_bf16(kf, qf[qt][ss], s[kt][qt]);
         }
+      RP_PRIO(0);
     } else {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
@@ -441,6 +450,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
             pf[qt][ks] = __builtin_bit_cast(bf16x8, u);
           }
         }
+      RP_PRIO(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -449,6 +459,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 #pragma unroll
           for (int qt = 0; qt < 2; ++qt) o[qt][dt] = mfma_bf16(vf, pf[qt][ks], o[qt][dt]);
         }
+      RP_PRIO(0);
     } else {
       if constexpr (DROP) {
 #pragma unroll
@@ -681,6 +692,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       }
       if constexpr (BF) {
         // the row constants enter as the first MFMA's C operand (no register copies)
+        RP_PRIO(1);
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
 #pragma unroll
@@ -693,6 +705,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
               dp[qq][kt] = mfma_bf16(da, vf[kt][ss], ss == 0 ? ndq[qq] : dp[qq][kt]);
             }
           }
+        RP_PRIO(0);
       } else {
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
@@ -749,6 +762,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
           pa[kt] = pack8(s[0][kt], s[1][kt]);
           sa[kt] = pack8(dp[0][kt], dp[1][kt]);
         }
+        RP_PRIO(1);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
           const bf16x8 dob = col_frag_lds(dOl, hf * 32, dt * 16, lane);
@@ -759,6 +773,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
             dk[kt][dt] = mfma_bf16(sa[kt], qb, dk[kt][dt]);
           }
         }
+        RP_PRIO(0);
       } else {
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
@@ -958,6 +973,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
         s0[qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
         d0[qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
       }
+      RP_PRIO(1);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -970,6 +986,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
             dp[kt][qt] = mfma_bf16(va, df[qt][ss], ss == 0 ? d0[qt] : dp[kt][qt]);
           }
         }
+      RP_PRIO(0);
       if (!full) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
@@ -1026,6 +1043,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     }
     // dQ[q][dk] += dS K : A = dS (q on row = lane i, key slots), B = K columns (tr read)
     if constexpr (BF) {
+      RP_PRIO(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8 sa[2];
@@ -1038,6 +1056,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
           for (int qt = 0; qt < 2; ++qt) dqa[qt][dt] = mfma_bf16(sa[qt], kb, dqa[qt][dt]);
         }
       }
+      RP_PRIO(0);
     } else {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
