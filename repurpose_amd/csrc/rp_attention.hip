@@ -227,11 +227,14 @@ __device__ __forceinline__ float bfi_select(uint32_t m, float a, float b) {
 // =================================================================================================
 // forward
 // =================================================================================================
-constexpr int FW_QB = NW * 32;  // queries per workgroup
+constexpr int FW_QB = NW * 32;  // queries per workgroup (dQ kernel; the forward's QT = 2 block)
 constexpr int FW_KT = 64;       // keys per tile
 
-template <typename T, bool DROP>
+// QT query tiles of 16 per wave: QT = 2 (128 queries per workgroup) by default; QT = 1 (64 per
+// workgroup) doubles the waves of a small problem (B*H*T/128 below two workgroups per CU)
+template <typename T, bool DROP, int QT>
 __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2) void attn_fwd_kernel(MhaDev a) {
+  constexpr int QB = NW * 16 * QT;  // queries per workgroup
   using C = AttnCfg<T>;
   constexpr int TILE = FW_KT * C::ROWB;
   constexpr int BUF = 2 * TILE + FW_KT * 4 + 16;
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   const uint32_t drop_thresh = a.drop_thresh;
   const float drop_scale = a.drop_scale;
   float* __restrict__ lse = a.lse;
-  const int nqb = (Tq + FW_QB - 1) / FW_QB;
+  const int nqb = (Tq + QB - 1) / QB;
   const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
   const int bh = L / nqb, qb = L % nqb;
   const int b = bh / H, h = bh % H;
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   const T* Qg = (const T*)a.q + (int64_t)b * Tq * ldq + h * HD;
   const T* Kg = (const T*)a.k + (int64_t)b * Tk * ldk + h * HD;
   const T* Vg = (const T*)a.v + (int64_t)b * Tk * ldv + h * HD;
-  const int q0 = qb * FW_QB + w * 32;  // this wave's first query
+  const int q0 = qb * QB + w * 16 * QT;  // this wave's first query
   const uint32_t seed_bh = rp_hash(a.seed, (uint32_t)bh);
   const float c = scale * LOG2E;
   const int KT = mask_kt(Tk);
@@ -261,16 +264,16 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 
   // Q^T operand (B operand of S^T = K Q^T): lane holds Q[q0 + qt*16 + i][dk slots]
   constexpr bool BF = std::is_same<T, bf16>::value;
-  bf16x8 qf[2][2];
-  float qs[2][16];
+  bf16x8 qf[QT][2];
+  float qs[QT][16];
   if constexpr (BF) {
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
+    for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
       for (int s = 0; s < 2; ++s) qf[qt][s] = row_frag_gmem((const bf16*)Qg, ldq, q0 + qt * 16, Tq, s * 32, lane);
   } else {
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
       int q = q0 + qt * 16 + i;
 #pragma unroll
       for (int s = 0; s < 16; ++s) qs[qt][s] = q < Tq ? (float)Qg[(int64_t)q * ldq + 4 * s + g] : 0.f;
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   // accumulators start at -m, the running reference max: P = exp2(acc) needs no per-score op
   // unless the reference moves on this tile.
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
+  for (int qt = 0; qt < QT; ++qt) {
     if constexpr (BF) {
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
@@ -293,19 +296,26 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     }
   }
 
-  f32x4 o[2][4];
+  f32x4 o[QT][4];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
+  for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[qt][dt] = zero4();
   // m: reference max (log2 units) once set (mset); 0 before, when O and l are still zero
-  float m[2] = {0.f, 0.f}, lp[2] = {0.f, 0.f};
-  bool mset[2] = {false, false};
-  // dropout stream state of this lane's two queries (carried across the key tiles)
-  uint32_t dst[2] = {0u, 0u};
+  float m[QT], lp[QT];
+  bool mset[QT];
+  // dropout stream state of this lane's queries (carried across the key tiles)
+  uint32_t dst[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    m[qt] = 0.f;
+    lp[qt] = 0.f;
+    mset[qt] = false;
+    dst[qt] = 0u;
+  }
   if constexpr (DROP) {
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) dst[qt] = rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g);
+    for (int qt = 0; qt < QT; ++qt) dst[qt] = rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g);
   }
 
   Stage<T, FW_KT> sk, sv;
@@ -348,11 +358,11 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     const bool full = *reinterpret_cast<const int*>(cur + 2 * TILE + FW_KT * 4) != 0;
 
     // ---- S^T[key][q] = K (cQ)^T - m ----
-    f32x4 s[4][2];
+    f32x4 s[4][QT];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) s[kt][qt] = f32x4{-m[qt], -m[qt], -m[qt], -m[qt]};
+      for (int qt = 0; qt < QT; ++qt) s[kt][qt] = f32x4{-m[qt], -m[qt], -m[qt], -m[qt]};
     if constexpr (BF) {
       RP_PRIO(1);
 #pragma unroll
@@ -361,7 +371,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
         for (int ss = 0; ss < 2; ++ss) {
           bf16x8 kf = row_frag_lds(Kl, kt * 16, ss * 32, lane);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) s[kt][qt] = mfma_bf16(kf, qf[qt][ss], s[kt][qt]);
+          for (int qt = 0; qt < QT; ++qt) s[kt][qt] = mfma_bf16(kf, qf[qt][ss], s[kt][qt]);
         }
       RP_PRIO(0);
     } else {
@@ -371,17 +381,17 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
         for (int ss = 0; ss < 16; ++ss) {
           float kf = ldsf(Kl, kt * 16 + i, 4 * ss + g);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) s[kt][qt] = mfma_f32(kf, qs[qt][ss], s[kt][qt]);
+          for (int qt = 0; qt < QT; ++qt) s[kt][qt] = mfma_f32(kf, qs[qt][ss], s[kt][qt]);
         }
     }
     // ---- mask (only tiles with masked keys) + column max, relative to the reference ----
     // Deferred rescale: the reference m only moves when the tile max exceeds it by more than
     // RESCALE_LOG2 (P <= 2^8 meanwhile, exact in fp32/bf16 range), or on the first finite max;
     // l and O share the reference, so out = O / l is unchanged and the lse uses the same m.
-    float rel[2];
+    float rel[QT];
     bool grow = false;
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
       if (!full) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
@@ -398,7 +408,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     }
     if (__any(grow)) {  // wave-uniform branch: move the reference of the growing lanes
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      for (int qt = 0; qt < QT; ++qt) {
         const bool gq = mset[qt] ? rel[qt] > RESCALE_LOG2 : rel[qt] > -INFINITY;
         const float alpha = gq ? (mset[qt] ? rp_exp2(-rel[qt]) : 0.f) : 1.f;
         const float sub = gq ? rel[qt] : 0.f;
@@ -413,7 +423,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     }
     // ---- P = exp2(acc); per-lane partial row sums (before dropout), tree order ----
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
       float t4[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
@@ -424,10 +434,10 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
       lp[qt] += (t4[0] + t4[1]) + (t4[2] + t4[3]);
     }
     // ---- dropout: 8 drop masks per (query, tile) from one xorshift stream; keep bits stored ----
-    uint32_t dm[2][8];
+    uint32_t dm[QT][8];
     if constexpr (DROP) {
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      for (int qt = 0; qt < QT; ++qt) {
         const int q = q0 + qt * 16 + i;
         const uint32_t word = drop_masks(dst[qt], drop_thresh, dm[qt]);
         if (q < Tq) mrow[((int64_t)kt_i * 4 + g) * ldm + q] = (uint16_t)word;
@@ -435,9 +445,9 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     }
     // ---- O^T[dk][q] += V^T P^T ----
     if constexpr (BF) {
-      bf16x8 pf[2][2];
+      bf16x8 pf[QT][2];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+      for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           pf[qt][ks] = pack8(s[2 * ks][qt], s[2 * ks + 1][qt]);
@@ -457,13 +467,13 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
         for (int dt = 0; dt < 4; ++dt) {
           bf16x8 vf = col_frag_lds(Vl, ks * 32, dt * 16, lane);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) o[qt][dt] = mfma_bf16(vf, pf[qt][ks], o[qt][dt]);
+          for (int qt = 0; qt < QT; ++qt) o[qt][dt] = mfma_bf16(vf, pf[qt][ks], o[qt][dt]);
         }
       RP_PRIO(0);
     } else {
       if constexpr (DROP) {
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
+        for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
           for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -478,7 +488,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
           for (int dt = 0; dt < 4; ++dt) {
             float vf = ldsf(Vl, kt * 16 + 4 * g + r, dt * 16 + i);
 #pragma unroll
-            for (int qt = 0; qt < 2; ++qt) o[qt][dt] = mfma_f32(vf, s[kt][qt][r], o[qt][dt]);
+            for (int qt = 0; qt < QT; ++qt) o[qt][dt] = mfma_f32(vf, s[kt][qt][r], o[qt][dt]);
           }
     }
     if (more) {
@@ -493,7 +503,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   const int64_t ldo = a.ldo;
   T* __restrict__ out = (T*)a.out;
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
+  for (int qt = 0; qt < QT; ++qt) {
     const float l = quad_sum(lp[qt]);
     const int q = q0 + qt * 16 + i;
     if (q >= Tq) continue;
@@ -822,8 +832,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
 // DELTA: the kernel also forms delta = rowsum(dO * O) of its queries (the lane's 16 dims of dO are
 // already in registers; the 4 lanes of a query combine by quad_sum) and writes it for the dK/dV
 // kernel, which then runs second — no separate delta pre-pass over dO and O.
-template <typename T, bool DROP, bool DELTA>
+template <typename T, bool DROP, bool DELTA, int QT>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
+  constexpr int QB = NW * 16 * QT;  // queries per workgroup (QT query tiles of 16 per wave)
   using C = AttnCfg<T>;
   constexpr bool BF = std::is_same<T, bf16>::value;
   constexpr int TILE = FW_KT * C::ROWB;
@@ -836,7 +847,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
   const float scale = a.scale, drop_scale = a.drop_scale;
   const float* __restrict__ lse = a.lse;
   const float* __restrict__ delta = a.delta;
-  const int nqb = (Tq + FW_QB - 1) / FW_QB;
+  const int nqb = (Tq + QB - 1) / QB;
   const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
   const int bh = L / nqb, qb = L % nqb;
   const int b = bh / H, h = bh % H;
@@ -845,17 +856,17 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
   const T* Kg = (const T*)a.k + (int64_t)b * Tk * ldk + h * HD;
   const T* Vg = (const T*)a.v + (int64_t)b * Tk * ldv + h * HD;
   const T* dOg = (const T*)a.dout + (int64_t)b * Tq * lddo + h * HD;
-  const int q0 = qb * FW_QB + w * 32;
+  const int q0 = qb * QB + w * 16 * QT;
   const float c = scale * LOG2E;
   const int KT = mask_kt(Tk);
   const int64_t ldm = mask_ld(Tq);
   const uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
 
-  bf16x8 qf[2][2], df[2][2];
-  float qs[2][16], dsv[2][16];
-  float lq[2], dq[2];
+  bf16x8 qf[QT][2], df[QT][2];
+  float qs[QT][16], dsv[QT][16];
+  float lq[QT], dq[QT];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
+  for (int qt = 0; qt < QT; ++qt) {
     const int q = q0 + qt * 16 + i;
     // with dropout the 1/(1-p) scale rides in the exponent: exp2(S*c - lq) = p * ds
     lq[qt] = q < Tq ? lse[(int64_t)bh * Tq + q] * LOG2E - (DROP ? log2f(drop_scale) : 0.f) : INFINITY;
@@ -892,9 +903,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
 
   // Q enters S^T = K Q^T prescaled by c = scale*log2(e) (Q feeds no other product here), so with
   // S^T starting at -lse*log2(e) (+ the key bias) the probability is exp2 of the accumulator
-  float nlq[2];
+  float nlq[QT];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
+  for (int qt = 0; qt < QT; ++qt) {
     nlq[qt] = -lq[qt];
     if constexpr (BF) {
 #pragma unroll
@@ -907,9 +918,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     }
   }
 
-  f32x4 dqa[2][4];
+  f32x4 dqa[QT][4];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
+  for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dqa[qt][dt] = zero4();
 
@@ -941,10 +952,12 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     const bool more = it + 1 < nkt;
     const int k0 = it * FW_KT;
     // keep-bit word of this lane's queries for the tile (same register layout as the forward)
-    uint32_t kwd[2] = {0u, 0u};
+    uint32_t kwd[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) kwd[qt] = 0u;
     if constexpr (DROP) {
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      for (int qt = 0; qt < QT; ++qt) {
         const int q = q0 + qt * 16 + i;
         kwd[qt] = q < Tq ? (uint32_t)mrow[((int64_t)it * 4 + g) * ldm + q] : 0u;
       }
@@ -963,13 +976,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     // bias (0 / -inf: masked keys give P = 0 with no select; added only on tiles with a masked
     // key), dP^T at -delta/ds.
     const bool full = *reinterpret_cast<const int*>(cur + 2 * TILE + FW_KT * 4) != 0;
-    f32x4 s[4][2], dp[4][2];
+    f32x4 s[4][QT], dp[4][QT];
     if constexpr (BF) {
       // the constants enter as the first MFMA's C operand (no per-tile register copies); the key
       // bias is added after the chain (0 + x == x, -inf + x == -inf: same values as adding it first)
-      f32x4 s0[2], d0[2];
+      f32x4 s0[QT], d0[QT];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      for (int qt = 0; qt < QT; ++qt) {
         s0[qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
         d0[qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
       }
@@ -981,7 +994,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
           bf16x8 ka = row_frag_lds(Kl, kt * 16, ss * 32, lane);
           bf16x8 va = row_frag_lds(Vl, kt * 16, ss * 32, lane);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) {
+          for (int qt = 0; qt < QT; ++qt) {
             s[kt][qt] = mfma_bf16(ka, qf[qt][ss], ss == 0 ? s0[qt] : s[kt][qt]);
             dp[kt][qt] = mfma_bf16(va, df[qt][ss], ss == 0 ? d0[qt] : dp[kt][qt]);
           }
@@ -992,14 +1005,14 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
         for (int kt = 0; kt < 4; ++kt) {
           const f32x4 kb4 = *reinterpret_cast<const f32x4*>(kbias + kt * 16 + 4 * g);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) s[kt][qt] += kb4;
+          for (int qt = 0; qt < QT; ++qt) s[kt][qt] += kb4;
         }
       }
     } else {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < QT; ++qt) {
           s[kt][qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
           dp[kt][qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
         }
@@ -1009,7 +1022,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
         for (int kt = 0; kt < 4; ++kt) {
           const f32x4 kb4 = *reinterpret_cast<const f32x4*>(kbias + kt * 16 + 4 * g);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) s[kt][qt] += kb4;
+          for (int qt = 0; qt < QT; ++qt) s[kt][qt] += kb4;
         }
       }
 #pragma unroll
@@ -1019,7 +1032,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
           float ka = ldsf(Kl, kt * 16 + i, 4 * ss + g);
           float va = ldsf(Vl, kt * 16 + i, 4 * ss + g);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) {
+          for (int qt = 0; qt < QT; ++qt) {
             s[kt][qt] = mfma_f32(ka, qs[qt][ss], s[kt][qt]);
             dp[kt][qt] = mfma_f32(va, dsv[qt][ss], dp[kt][qt]);
           }
@@ -1029,7 +1042,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+      for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float p = rp_exp2(s[kt][qt][r]);  // with dropout: p * ds
@@ -1046,14 +1059,14 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
       RP_PRIO(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 sa[2];
+        bf16x8 sa[QT];
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) sa[qt] = pack8(s[2 * ks][qt], s[2 * ks + 1][qt]);
+        for (int qt = 0; qt < QT; ++qt) sa[qt] = pack8(s[2 * ks][qt], s[2 * ks + 1][qt]);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
           bf16x8 kb = col_frag_lds(Kl, ks * 32, dt * 16, lane);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) dqa[qt][dt] = mfma_bf16(sa[qt], kb, dqa[qt][dt]);
+          for (int qt = 0; qt < QT; ++qt) dqa[qt][dt] = mfma_bf16(sa[qt], kb, dqa[qt][dt]);
         }
       }
       RP_PRIO(0);
@@ -1066,7 +1079,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
           for (int dt = 0; dt < 4; ++dt) {
             const float kb = ldsf(Kl, kt * 16 + 4 * g + r, dt * 16 + i);
 #pragma unroll
-            for (int qt = 0; qt < 2; ++qt) dqa[qt][dt] = mfma_f32(s[kt][qt][r], kb, dqa[qt][dt]);
+            for (int qt = 0; qt < QT; ++qt) dqa[qt][dt] = mfma_f32(s[kt][qt][r], kb, dqa[qt][dt]);
           }
     }
     if (more) {
@@ -1079,7 +1092,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
   // store: dqa[qt][dt][r] = dQ[q = q0 + qt*16 + 4g + r][dk = dt*16 + i]
   T* dQ = (T*)a.dq + (int64_t)b * Tq * a.lddq + h * HD;
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
+  for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int q = q0 + qt * 16 + 4 * g + r;
@@ -1091,29 +1104,56 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
 
 template <typename T>
 int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
-  const int nqb = (a.Tq + FW_QB - 1) / FW_QB;
+  // 128-query blocks unless that leaves fewer than two workgroups per CU (256 CUs): then 64
+  const int64_t big = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H;
+  const bool small = big < 512;
+  const int qb = small ? NW * 16 : FW_QB;
+  const int nqb = (a.Tq + qb - 1) / qb;
   const dim3 grid((unsigned)(nqb * a.B * a.H));
-  if (a.drop_thresh)
-    hipLaunchKernelGGL((attn_fwd_kernel<T, true>), grid, dim3(NT), 0, s, a);
-  else
-    hipLaunchKernelGGL((attn_fwd_kernel<T, false>), grid, dim3(NT), 0, s, a);
+  if (small) {
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_fwd_kernel<T, true, 1>), grid, dim3(NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<T, false, 1>), grid, dim3(NT), 0, s, a);
+  } else {
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_fwd_kernel<T, true, 2>), grid, dim3(NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<T, false, 2>), grid, dim3(NT), 0, s, a);
+  }
   return rp_check_launch("rp_mha_fwd");
 }
 
 // phases: bit 0 = delta pre-pass, bit 1 = dK/dV kernel, bit 2 = dQ kernel.  With bits 0 and 2 both
 // set the delta pre-pass is fused into the dQ kernel, which then runs first (dK/dV reads its delta).
+template <typename T, int QT>
+void launch_bwd_q(bool delta, const MhaDev& a, hipStream_t s) {
+  const dim3 grid((unsigned)((a.Tq + NW * 16 * QT - 1) / (NW * 16 * QT) * a.B * a.H));
+  if (delta) {
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true, true, QT>), grid, dim3(NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false, true, QT>), grid, dim3(NT), 0, s, a);
+  } else {
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true, false, QT>), grid, dim3(NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false, false, QT>), grid, dim3(NT), 0, s, a);
+  }
+}
+
 template <typename T>
 int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   const int64_t rows = (int64_t)a.B * a.Tq;
   const int nkb = (a.Tk + KV_KB - 1) / KV_KB;
-  const int nqb = (a.Tq + FW_QB - 1) / FW_QB;
+  // dQ: 128-query blocks unless that leaves fewer than two workgroups per CU (then 64, as the forward)
+  const bool small = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H < 512;
   const bool fused = (phases & 5) == 5;
   if (fused) {
-    const dim3 grid((unsigned)(nqb * a.B * a.H));
-    if (a.drop_thresh)
-      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true, true>), grid, dim3(NT), 0, s, a);
+    if (small)
+      launch_bwd_q<T, 1>(true, a, s);
     else
-      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false, true>), grid, dim3(NT), 0, s, a);
+      launch_bwd_q<T, 2>(true, a, s);
   } else if (phases & 1) {
     hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
   }
@@ -1125,11 +1165,10 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
       hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false>), grid, dim3(NT), 0, s, a);
   }
   if ((phases & 4) && !fused) {
-    const dim3 grid((unsigned)(nqb * a.B * a.H));
-    if (a.drop_thresh)
-      hipLaunchKernelGGL((attn_bwd_q_kernel<T, true, false>), grid, dim3(NT), 0, s, a);
+    if (small)
+      launch_bwd_q<T, 1>(false, a, s);
     else
-      hipLaunchKernelGGL((attn_bwd_q_kernel<T, false, false>), grid, dim3(NT), 0, s, a);
+      launch_bwd_q<T, 2>(false, a, s);
   }
   return rp_check_launch("rp_mha_bwd");
 }
