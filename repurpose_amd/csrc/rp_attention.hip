@@ -554,17 +554,20 @@ __global__ void attn_delta_kernel(MhaDev a) {
 }
 
 // =================================================================================================
-// backward: dK, dV per 128-key block (4 waves x 32 keys), sweep over 64-query tiles
+// backward: dK, dV per 128-key block (4 waves x 32 keys; 64 / 16 for small problems), sweep over
+// 64-query tiles
 // =================================================================================================
-constexpr int KV_KB = NW * 32;
+constexpr int KV_KB = NW * 32;  // keys per workgroup at KTW = 2
 constexpr int KV_QT = 64;
 
-template <typename T, bool DROP>
+// KTW key tiles of 16 per wave: 2 (128 keys per workgroup) by default, 1 (64) for small problems
+template <typename T, bool DROP, int KTW>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
+  constexpr int KB = NW * 16 * KTW;  // keys per workgroup
   using C = AttnCfg<T>;
   constexpr bool BF = std::is_same<T, bf16>::value;
   constexpr int TILE = KV_QT * C::ROWB;
-  constexpr int MASKB = (KV_KB / 64) * 4 * KV_QT * 2;    // 2 key tiles x 4 groups x 64 queries, u16
+  constexpr int MASKB = (KB / 64) * 4 * KV_QT * 2;    // KB/64 key tiles x 4 groups x 64 queries, u16
   constexpr int BUF = 2 * TILE + 2 * KV_QT * 4 + MASKB;  // Q, dO, lse*log2e, delta, keep bits
   __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -573,7 +576,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   const uint8_t* __restrict__ kvalid = a.kvalid;
   const float scale = a.scale, drop_scale = a.drop_scale;
   const uint16_t* __restrict__ dmask = a.dmask;
-  const int nkb = (Tk + KV_KB - 1) / KV_KB;
+  const int nkb = (Tk + KB - 1) / KB;
   const int L = rp_xcd_remap(blockIdx.x, nkb * B * H);
   const int bh = L / nkb, kb = L % nkb;
   const int b = bh / H, h = bh % H;
@@ -584,18 +587,18 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   const T* dOg = (const T*)a.dout + (int64_t)b * Tq * lddo + h * HD;
   const float* lse_bh = a.lse + (int64_t)bh * Tq;
   const float* del_bh = a.delta + (int64_t)bh * Tq;
-  const int kw0 = kb * KV_KB + w * 32;
+  const int kw0 = kb * KB + w * 16 * KTW;
   const float c = scale * LOG2E;
   const float inv_ds = DROP ? 1.f / drop_scale : 1.f;
   const int KT = mask_kt(Tk);
   const int64_t ldm = mask_ld(Tq);
 
   // K, V as B operands of S = Q K^T and dP = dO V^T: lane holds X[kw0 + kt*16 + i][dk slots]
-  bf16x8 kf[2][2], vf[2][2];
-  float ks_[2][16], vs_[2][16];
+  bf16x8 kf[KTW][2], vf[KTW][2];
+  float ks_[KTW][16], vs_[KTW][16];
   if constexpr (BF) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < KTW; ++kt)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         kf[kt][s] = row_frag_gmem((const bf16*)Kg, ldk, kw0 + kt * 16, Tk, s * 32, lane);
@@ -603,7 +606,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       }
   } else {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < KTW; ++kt) {
       const int k = kw0 + kt * 16 + i;
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
@@ -616,27 +619,28 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   // product here), so with S starting at -lse*log2(e) the probability is exp2 of the accumulator
   if constexpr (BF) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < KTW; ++kt)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int j = 0; j < 8; ++j) kf[kt][s2][j] = (bf16)((float)kf[kt][s2][j] * c);
   }
 
-  f32x4 dk[2][4], dv[2][4];
+  f32x4 dk[KTW][4], dv[KTW][4];
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int kt = 0; kt < KTW; ++kt)
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dk[kt][dt] = dv[kt][dt] = zero4();
 
   Stage<T, KV_QT> sq, sdo;
   uint4 mreg = make_uint4(0u, 0u, 0u, 0u);
-  // keep-bit words of this workgroup's 2 key tiles x 4 groups x 64 queries: thread t < 64 moves
-  // 16 bytes (row = tile*4 + g, 8 queries)
+  // keep-bit words of this workgroup's KB/64 key tiles x 4 groups x 64 queries: thread
+  // t < (KB/64)*32 moves 16 bytes (row = tile*4 + g, 8 queries)
+  constexpr int MT = (KB / 64) * 32;
   auto load_mask = [&](int qs0) {
-    if (DROP && tid < 64) {
+    if (DROP && tid < MT) {
       const int r = tid >> 3, cch = tid & 7;
-      const int tile = kb * (KV_KB / 64) + (r >> 2);
+      const int tile = kb * (KB / 64) + (r >> 2);
       if (tile < KT)
         mreg = *reinterpret_cast<const uint4*>(dmask + (((int64_t)bh * KT + tile) * 4 + (r & 3)) * ldm + qs0 + cch * 8);
       else
@@ -660,7 +664,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       lb[tid] = lse_r;
       lb[KV_QT + tid] = del_r;
     }
-    if (DROP && tid < 64) *reinterpret_cast<uint4*>(buf + 2 * TILE + 2 * KV_QT * 4 + tid * 16) = mreg;
+    if (DROP && tid < MT) *reinterpret_cast<uint4*>(buf + 2 * TILE + 2 * KV_QT * 4 + tid * 16) = mreg;
   };
   const int nqt = (Tq + KV_QT - 1) / KV_QT;
   sq.load(Qg, ldq, 0, Tq, tid);
@@ -694,7 +698,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
     for (int hf = 0; hf < 2; ++hf) {
       // S[q][key], dP[q][key]: C-layout row q = (2hf+qq)*16 + 4g + r, col key = kt*16 + i
       // dP starts at -delta/ds (row constant as the initial accumulator): dS = p*ds*acc
-      f32x4 s[2][2], dp[2][2], ndq[2], nl[2];
+      f32x4 s[2][KTW], dp[2][KTW], ndq[2], nl[2];
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
         ndq[qq] = *reinterpret_cast<const f32x4*>(drow + (2 * hf + qq) * 16 + 4 * g);
@@ -710,7 +714,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
             bf16x8 qa = row_frag_lds(Ql, (2 * hf + qq) * 16, ss * 32, lane);
             bf16x8 da = row_frag_lds(dOl, (2 * hf + qq) * 16, ss * 32, lane);
 #pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
+            for (int kt = 0; kt < KTW; ++kt) {
               s[qq][kt] = mfma_bf16(qa, kf[kt][ss], ss == 0 ? nl[qq] : s[qq][kt]);
               dp[qq][kt] = mfma_bf16(da, vf[kt][ss], ss == 0 ? ndq[qq] : dp[qq][kt]);
             }
@@ -720,7 +724,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
 #pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
+          for (int kt = 0; kt < KTW; ++kt) {
             s[qq][kt] = nl[qq];
             dp[qq][kt] = ndq[qq];
           }
@@ -731,7 +735,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
             float qa = ldsf(Ql, (2 * hf + qq) * 16 + i, 4 * ss + g);
             float da = ldsf(dOl, (2 * hf + qq) * 16 + i, 4 * ss + g);
 #pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
+            for (int kt = 0; kt < KTW; ++kt) {
               s[qq][kt] = mfma_f32(qa, ks_[kt][ss], s[qq][kt]);
               dp[qq][kt] = mfma_f32(da, vs_[kt][ss], dp[qq][kt]);
             }
@@ -743,10 +747,11 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       for (int qq = 0; qq < 2; ++qq) {
         const int qrow = (2 * hf + qq) * 16 + 4 * g;
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
+        for (int kt = 0; kt < KTW; ++kt) {
           // this lane's key: ko = key % 64 -> word row (tile half, group (ko%16)/4), bit (ko/16)*4 + ko%4
-          const int ko = (w * 32 + kt * 16 + i) & 63;
-          const int mrow_l = ((w * 32 + kt * 16) >> 6) * 4 + ((ko & 15) >> 2);
+          const int kw = w * 16 * KTW + kt * 16 + i;
+          const int ko = kw & 63;
+          const int mrow_l = (kw >> 6) * 4 + ((ko & 15) >> 2);
           const int bit = (ko >> 4) * 4 + (ko & 3);
           uint2 bits = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
           if constexpr (DROP) bits = *reinterpret_cast<const uint2*>(mw + mrow_l * KV_QT + qrow);
@@ -766,9 +771,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       }
       // dV[key][dk] += P_d^T dO ; dK[key][dk] += dS^T Q     (key on the row, k = query slots)
       if constexpr (BF) {
-        bf16x8 pa[2], sa[2];
+        bf16x8 pa[KTW], sa[KTW];
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
+        for (int kt = 0; kt < KTW; ++kt) {
           pa[kt] = pack8(s[0][kt], s[1][kt]);
           sa[kt] = pack8(dp[0][kt], dp[1][kt]);
         }
@@ -778,7 +783,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
           const bf16x8 dob = col_frag_lds(dOl, hf * 32, dt * 16, lane);
           const bf16x8 qb = col_frag_lds(Ql, hf * 32, dt * 16, lane);
 #pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
+          for (int kt = 0; kt < KTW; ++kt) {
             dv[kt][dt] = mfma_bf16(pa[kt], dob, dv[kt][dt]);
             dk[kt][dt] = mfma_bf16(sa[kt], qb, dk[kt][dt]);
           }
@@ -794,7 +799,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
               const float dob = ldsf(dOl, (2 * hf + qq) * 16 + 4 * g + r, dt * 16 + i);
               const float qb = ldsf(Ql, (2 * hf + qq) * 16 + 4 * g + r, dt * 16 + i);
 #pragma unroll
-              for (int kt = 0; kt < 2; ++kt) {
+              for (int kt = 0; kt < KTW; ++kt) {
                 dv[kt][dt] = mfma_f32(s[qq][kt][r], dob, dv[kt][dt]);
                 dk[kt][dt] = mfma_f32(dp[qq][kt][r], qb, dk[kt][dt]);
               }
@@ -812,7 +817,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   T* dK = (T*)a.dk + (int64_t)b * Tk * a.lddk + h * HD;
   T* dV = (T*)a.dv + (int64_t)b * Tk * a.lddv + h * HD;
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int kt = 0; kt < KTW; ++kt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = kw0 + kt * 16 + 4 * g + r;
@@ -1158,11 +1163,20 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
   }
   if (phases & 2) {
-    const dim3 grid((unsigned)(nkb * a.B * a.H));
-    if (a.drop_thresh)
-      hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true>), grid, dim3(NT), 0, s, a);
-    else
-      hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false>), grid, dim3(NT), 0, s, a);
+    // 128-key blocks unless that leaves fewer than two workgroups per CU: then 64
+    if ((int64_t)nkb * a.B * a.H < 512) {
+      const dim3 grid((unsigned)((a.Tk + NW * 16 - 1) / (NW * 16) * a.B * a.H));
+      if (a.drop_thresh)
+        hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true, 1>), grid, dim3(NT), 0, s, a);
+      else
+        hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false, 1>), grid, dim3(NT), 0, s, a);
+    } else {
+      const dim3 grid((unsigned)(nkb * a.B * a.H));
+      if (a.drop_thresh)
+        hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true, 2>), grid, dim3(NT), 0, s, a);
+      else
+        hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false, 2>), grid, dim3(NT), 0, s, a);
+    }
   }
   if ((phases & 4) && !fused) {
     if (small)
