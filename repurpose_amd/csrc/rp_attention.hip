@@ -1107,11 +1107,21 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     }
 }
 
+// RP_ATTN_BLOCK=64 | 128 forces the workgroup block (queries for fwd / dQ, keys for dK/dV), for tuning
+static int attn_block_override() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_ATTN_BLOCK");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 template <typename T>
 int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
   // 128-query blocks unless that leaves fewer than two workgroups per CU (256 CUs): then 64
   const int64_t big = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H;
-  const bool small = big < 512;
+  const bool small = attn_block_override() ? attn_block_override() == 64 : big < 512;
   const int qb = small ? NW * 16 : FW_QB;
   const int nqb = (a.Tq + qb - 1) / qb;
   const dim3 grid((unsigned)(nqb * a.B * a.H));
@@ -1152,7 +1162,8 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   const int64_t rows = (int64_t)a.B * a.Tq;
   const int nkb = (a.Tk + KV_KB - 1) / KV_KB;
   // dQ: 128-query blocks unless that leaves fewer than two workgroups per CU (then 64, as the forward)
-  const bool small = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H < 512;
+  const bool small = attn_block_override() ? attn_block_override() == 64
+                                           : (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H < 512;
   const bool fused = (phases & 5) == 5;
   if (fused) {
     if (small)
@@ -1164,7 +1175,7 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   }
   if (phases & 2) {
     // 128-key blocks unless that leaves fewer than two workgroups per CU: then 64
-    if ((int64_t)nkb * a.B * a.H < 512) {
+    if (attn_block_override() ? attn_block_override() == 64 : (int64_t)nkb * a.B * a.H < 512) {
       const dim3 grid((unsigned)((a.Tk + NW * 16 - 1) / (NW * 16) * a.B * a.H));
       if (a.drop_thresh)
         hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true, 1>), grid, dim3(NT), 0, s, a);
