@@ -266,6 +266,55 @@ def test_mha_cross_strided(dev, dtype, Tq, Tk):
     close(dv, gv, atol=btol, rtol=btol, what="mha dv")
 
 
+@pytest.mark.gpu
+def test_attention_128_blocks_ragged_dropout(dev):
+    """Self attention on the 128-row block path (B*H*ceil(T/128) >= 512 workgroups; the smaller test
+    shapes above take the 64-row path), ragged T and key padding, dropout keep bits vs the
+    restatement, fwd and bwd vs fp64."""
+    B, H, T, p = 8, 8, 1030, 0.1
+    qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(torch.bfloat16)
+    # key lengths >= 33: with one valid key every query's whole mass lands on it and dK/dV sum ~1000
+    # bf16-recomputed P values (forward and backward prescale different operands by scale*log2e, so P
+    # differs by ~2^-8 relative), which exceeds a fixed absolute tolerance; fp32 mode has no such gap
+    lens = torch.tensor([T, T - 1, 1000, 777, 640, 129, 64, 33], device=dev)
+    kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
+    seed = 99
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed)
+    ref_in = qkv.double().requires_grad_(True)
+    ref = attn_ref(ref_in, kv, B, T, H, p, seed)
+    close(o, ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd (128 blocks)")
+    KT, ldm = (T + 63) // 64, (T + 63) // 64 * 64
+    words = mask.view(B * H, KT, 4, ldm)[..., :T].to(torch.int64) & 0xFFFF
+    bits = ((words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1).view(B * H, KT, 4, T, 4, 4)
+    got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, T, KT * 64)[:, :, :T].bool()
+    assert torch.equal(got, attn_keep(B, H, T, p, seed, dev).view(B * H, T, T))
+    do = rnd(B * T, H * 64, dev=dev, seed=T + 1).to(torch.bfloat16)
+    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask)
+    gref = torch.autograd.grad(ref, ref_in, do.double())[0]
+    close(dqkv, gref, atol=6e-2, rtol=6e-2, what="attn bwd (128 blocks)")
+
+
+@pytest.mark.gpu
+def test_mha_cross_128_blocks(dev):
+    """Cross attention (Tq != Tk, both ragged) on the 128-row block path of all three kernels."""
+    B, H, Tq, Tk, dk = 8, 8, 1100, 1000, 64
+    q = rnd(B * Tq, H * dk, dev=dev, seed=5).to(torch.bfloat16)
+    kvbuf = rnd(B * Tk, 2 * H * dk, dev=dev, seed=6).to(torch.bfloat16)
+    k, v = kvbuf[:, :H * dk], kvbuf[:, H * dk:]
+    lens = torch.tensor([Tk, 999, 900, 513, 500, 128, 65, 40], device=dev)  # >= 33: see the test above
+    kv = (torch.arange(Tk, device=dev)[None] < lens[:, None]).to(torch.uint8)
+    o, lse, _ = K.mha_fwd(q, k, v, kv, B, Tq, Tk, H, 0.125)
+    qd, kd, vd = (t.double().requires_grad_(True) for t in (q, k, v))
+    ref = mha_ref(qd, kd, vd, kv, B, Tq, Tk, H, 0.125)
+    close(o, ref.detach(), atol=2e-2, rtol=2e-2, what="mha fwd (128 blocks)")
+    do = rnd(B * Tq, H * dk, dev=dev, seed=7).to(torch.bfloat16)
+    dq, dkk, dv = K.mha_bwd(q, k, v, o, do, lse, kv, B, Tq, Tk, H, 0.125)
+    gq, gk, gv = torch.autograd.grad(ref, (qd, kd, vd), do.double())
+    close(dq, gq, atol=6e-2, rtol=6e-2, what="mha dq (128 blocks)")
+    close(dkk, gk, atol=6e-2, rtol=6e-2, what="mha dk (128 blocks)")
+    close(dv, gv, atol=6e-2, rtol=6e-2, what="mha dv (128 blocks)")
+
+
 def test_attention_lse(dev):
     B, H, T = 1, 8, 96
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=3)
