@@ -67,7 +67,8 @@ int rp_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream);
  * A and B share `dtype` (RP_F32: exact-f32 MFMA parity mode; RP_BF16: bf16 MFMA, fp32 acc).
  * Requirements: the contiguous dimension of A, B and C is a multiple of 8 elements, leading
  * dimensions multiples of 8, base pointers 16-byte aligned.
- * Epilogue order: v = alpha*acc (+ bias[n]); relu; dropout(p, seed, index m*N+n);
+ * Epilogue order: v = alpha*acc (+ bias[n]); v *= col_scale if n < col_scale_n; relu;
+ *   dropout(p, seed, index m*N+n);
  *   gate: v *= gate_scale * (gate[m, n] > 0);  residual: v += residual[m, n];
  *   accumulate (fp32 C only): C[m, n] += v, else C[m, n] = v. */
 typedef struct rp_gemm_epilogue {
@@ -82,6 +83,9 @@ typedef struct rp_gemm_epilogue {
   int64_t ldg;
   float gate_scale;
   int accumulate;
+  int64_t col_scale_n; /* multiple of 8; 0 = off.  The Q columns of the QKV projection use it to emit
+                          Q * scale * log2(e) for the attention kernels (RP_ATTN_Q_PRESCALED) */
+  float col_scale;
 } rp_gemm_epilogue;
 
 int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int a_kmajor,
@@ -173,6 +177,15 @@ int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ldx,
               float* out, int accumulate, float* workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
+/* Flag or-ed into the dtype argument of every rp_attn_* / rp_mha_* entry point: the q operand
+ * already holds Q * scale * log2(e), rounded to the operand dtype (rp_gemm's col_scale epilogue
+ * on the Q columns of the QKV projection).  The kernels then skip their own prescale, and the
+ * backward's recomputed scores are the forward's bit for bit in bf16 too.  dq is still the gradient
+ * w.r.t. the unscaled Q (the producer's pre-scale output), so it chains into the producer's
+ * backward unchanged.  Without the flag the kernels compute the same bf16(Q * scale * log2 e)
+ * themselves (the forward and dQ kernels in registers, the dK/dV kernel as it stages Q tiles). */
+enum { RP_ATTN_Q_PRESCALED = 0x100 };
+
 /* Multi-head self attention, flash-style (no T x T materialisation).
  * qkv: [B*T, 3*H*dk] rows = (q heads | k heads | v heads), dk == 64.
  * key_valid: [B, T] uint8 (0 -> key masked with -inf, torch key_padding_mask semantics).
@@ -291,11 +304,15 @@ int rp_infer_select(const float* logits, const uint8_t* mask, const float* offse
                     float thresh, int topk, float dur_min, float dur_max, int* count,
                     int64_t* idx, float* score, float* seg, void* stream);
 /* Soft-NMS with the exact semantics of soft_nms_intervals_cpu (one workgroup per video,
- * n = count[b] <= cap <= 1024).  keep[b, 0:keep_count[b]] = positions into the candidate list.
- * final_scores (optional): the decayed, permuted score array the reference leaves behind. */
+ * n = count[b] <= cap candidates, any cap).  keep[b, 0:keep_count[b]] = positions into the candidate
+ * list.  final_scores (optional): the decayed, permuted score array the reference leaves behind.
+ * The Gaussian decay uses numpy's float32 exp algorithm bit for bit (reference softnms.py:35).
+ * Candidates live in LDS up to cap = 6144; above that the kernel keeps them in `workspace`
+ * (rp_softnms_workspace(B, cap) bytes, 0 below the LDS limit: workspace may then be NULL). */
+int64_t rp_softnms_workspace(int B, int cap);
 int rp_softnms(const float* scores, const float* segs, const int* count, int B, int cap,
                float sigma, float thresh, const int* max_seg, int* keep, int* keep_count,
-               float* final_scores, void* stream);
+               float* final_scores, void* workspace, int64_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Batch collation on the device (dataset/RepurposeClip.py:449-533 preprocessing): the rows of B

@@ -26,6 +26,7 @@ be constructed on CPU (as ``main.py:139`` does) and moved with ``.to(device)``.
 import copy
 import math
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -39,6 +40,17 @@ from .softnms import soft_nms_intervals_cpu  # noqa: F401  (re-exported, referen
 _F32 = torch.float32
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
            "bfloat16": torch.bfloat16}
+
+# Parameter -> owning model (weak), so FusedAdam(model.parameters()) finds the flat buffers
+_OWNERS = weakref.WeakValueDictionary()
+
+
+def owner_of(param):
+    """The MMCTransformer that ``param`` belongs to, or None."""
+    m = _OWNERS.get(id(param))
+    if m is not None and any(q is param for q in m.parameters()):
+        return m
+    return None
 
 
 class PositionalEncoding(nn.Module):
@@ -124,6 +136,8 @@ class MMCTransformer(nn.Module):
         self._grad_ready_hooks = []   # called with (lo, hi) flat ranges whose gradients are final
         self._grad_done_hooks = []    # called once at the end of backward
         self._build_flat()
+        for p in self.parameters():
+            _OWNERS[id(p)] = self
 
     # ---------------------------------------------------------------- init / storage -----------
     def _init_weights(self):
@@ -237,20 +251,29 @@ class MMCTransformer(nn.Module):
             for h in self._grad_ready_hooks:
                 h(lo, hi)
 
+    def _master_version(self):
+        """Version key of the fp32 master.  ``_build_flat`` rebinds every Parameter with
+        ``p.data = view``, which gives the Parameter a version counter of its own: in-place updates
+        through the Parameters (torch.optim.Adam, ``load_state_dict``'s copy_) bump only those, writes
+        through the flat buffer bump only ``flat._version`` — the key covers both."""
+        return (self._flat._version,) + tuple(p._version for p in self.parameters())
+
     def lowp_weights(self):
         """bf16 operand copy of the flat weights, refreshed when the fp32 master changed."""
         f = self.flat_params()
         if self._lp is None or self._lp.device != f.device:
             self._lp = torch.empty(f.numel(), device=f.device, dtype=torch.bfloat16)
             self._lp_version = None
-        if self._lp_version != f._version:
+        key = self._master_version()
+        if self._lp_version != key:
             K.cast_bf16(f, self._lp)
-            self._lp_version = f._version
+            self._lp_version = key
         return self._lp
 
     def mark_lowp_fresh(self):
-        """Called by FusedAdam after it rewrote both the fp32 master and the bf16 copy."""
-        self._lp_version = self._flat._version
+        """Called by FusedAdam after its kernel rewrote both the fp32 master and the bf16 copy
+        through raw pointers (no version counter moves)."""
+        self._lp_version = self._master_version()
 
     @property
     def device(self):
@@ -399,8 +422,11 @@ class _Schedule:
             pre = f"multimodal_encoder.layers.{l}."
             _, h1, mu1, rs1 = K.layernorm_fwd(x, self.P(pre + "norm1.weight"), self.P(pre + "norm1.bias"),
                                               out_f32=False, lp_dtype=dt, save_stats=save)
-            qkv = K.linear_fwd(h1, self.W(pre + "self_attn.in_proj_weight"), self.P(pre + "self_attn.in_proj_bias"))
-            o, lse, dmask = K.attn_fwd(qkv, kv, B, T, H, scale, p, self.seed(100 + 4 * l))
+            # the Q columns leave the GEMM as Q * scale * log2(e) (rounded once, read by the attention
+            # forward and both backward kernels: the backward recomputes the forward's exact scores)
+            qkv = K.linear_fwd(h1, self.W(pre + "self_attn.in_proj_weight"), self.P(pre + "self_attn.in_proj_bias"),
+                               col_scale_n=d, col_scale=scale * K.LOG2E)
+            o, lse, dmask = K.attn_fwd(qkv, kv, B, T, H, scale, p, self.seed(100 + 4 * l), q_prescaled=True)
             x1 = K.linear_fwd(o, self.W(pre + "self_attn.out_proj.weight"), self.P(pre + "self_attn.out_proj.bias"),
                               out_dtype=_F32, dropout_p=p, seed=self.seed(101 + 4 * l), residual=x)
             _, h2, mu2, rs2 = K.layernorm_fwd(x1, self.P(pre + "norm2.weight"), self.P(pre + "norm2.bias"),
@@ -527,7 +553,7 @@ class _Schedule:
             wgrad(g1, o, pre + "self_attn.out_proj.weight", pre + "self_attn.out_proj.bias")
             do = K.linear_dgrad(g1, self.W(pre + "self_attn.out_proj.weight"), out_dtype=dt)
             # attention
-            dqkv = K.attn_bwd(qkv, o, do, lse, self.kv, B, T, H, self.scale, p, dropmask=dmask)
+            dqkv = K.attn_bwd(qkv, o, do, lse, self.kv, B, T, H, self.scale, p, dropmask=dmask, q_prescaled=True)
             # in_proj
             wgrad(dqkv, h1, pre + "self_attn.in_proj_weight", pre + "self_attn.in_proj_bias")
             dh1 = K.linear_dgrad(dqkv, self.W(pre + "self_attn.in_proj_weight"), out_dtype=_F32)

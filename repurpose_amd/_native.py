@@ -23,7 +23,8 @@ c_u32 = ctypes.c_uint32
 class GemmEpilogue(ctypes.Structure):
     _fields_ = [("bias", c_vp), ("relu", c_i), ("dropout_p", c_f), ("dropout_seed", c_u32),
                 ("residual", c_vp), ("ldr", c_i64), ("gate", c_vp), ("gate_dtype", c_i),
-                ("ldg", c_i64), ("gate_scale", c_f), ("accumulate", c_i)]
+                ("ldg", c_i64), ("gate_scale", c_f), ("accumulate", c_i), ("col_scale_n", c_i64),
+                ("col_scale", c_f)]
 
 
 class LnFwdArgs(ctypes.Structure):
@@ -91,7 +92,8 @@ _SIGNATURES = {
     "rp_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_f, c_f, c_f, c_i, c_vp, c_vp]),
     "rp_infer_select": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_f, c_i, c_f, c_f, c_vp, c_vp, c_vp, c_vp,
                               c_vp]),
-    "rp_softnms": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rp_softnms_workspace": (c_i64, [c_i, c_i]),
+    "rp_softnms": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
 }
 
 EXPORTED = tuple(_SIGNATURES)

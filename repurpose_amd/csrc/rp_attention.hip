@@ -84,6 +84,7 @@ struct MhaDev {
   const void* dout; int64_t lddo;
   float* delta;
   void* dq; int64_t lddq; void* dk; int64_t lddk; void* dv; int64_t lddv;
+  int qpre;  // RP_ATTN_Q_PRESCALED: q holds Q * scale * log2(e) (see include/rp_api.h)
 };
 
 // ----- global [rows][64] (row stride ld elements) <-> LDS [rows][ROWB] staging ------------------
@@ -117,6 +118,18 @@ struct Stage {
       int id = tid + NT * i;
       int row = id / AttnCfg<T>::CPR, c = id % AttnCfg<T>::CPR;
       *reinterpret_cast<uint4*>(lds + lds_off<T>(row, c * 16)) = r[i];
+    }
+  }
+  // bf16 only: store bf16(x * c) — the same rounding as the forward's prescale of Q
+  __device__ __forceinline__ void store_scaled(char* lds, int tid, float c) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int id = tid + NT * i;
+      int row = id / AttnCfg<T>::CPR, cc = id % AttnCfg<T>::CPR;
+      bf16x8 v = __builtin_bit_cast(bf16x8, r[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] * c);
+      *reinterpret_cast<uint4*>(lds + lds_off<T>(row, cc * 16)) = __builtin_bit_cast(uint4, v);
     }
   }
 };
@@ -280,11 +293,11 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     }
   }
 
-  // Q enters S^T = K Q^T prescaled by c = scale*log2(e) (log2-domain scores), and the S^T
-  // accumulators start at -m, the running reference max: P = exp2(acc) needs no per-score op
-  // unless the reference moves on this tile.
+  // Q enters S^T = K Q^T prescaled by c = scale*log2(e) (log2-domain scores; already done by the
+  // producer when a.qpre), and the S^T accumulators start at -m, the running reference max:
+  // P = exp2(acc) needs no per-score op unless the reference moves on this tile.
 #pragma unroll
-  for (int qt = 0; qt < QT; ++qt) {
+  for (int qt = 0; qt < QT && !a.qpre; ++qt) {
     if constexpr (BF) {
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
@@ -589,6 +602,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   const float* del_bh = a.delta + (int64_t)bh * Tq;
   const int kw0 = kb * KB + w * 16 * KTW;
   const float c = scale * LOG2E;
+  const float kc = a.qpre ? 1.f : c;  // fp32 path: K prescale
+  const bool scale_q = BF && !a.qpre;  // bf16 path: Q prescale at LDS staging
+  const float dk_scale = (BF || a.qpre) ? 1.f / LOG2E : scale;  // dS^T Q' -> dK
   const float inv_ds = DROP ? 1.f / drop_scale : 1.f;
   const int KT = mask_kt(Tk);
   const int64_t ldm = mask_ld(Tq);
@@ -610,21 +626,15 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       const int k = kw0 + kt * 16 + i;
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        ks_[kt][s] = k < Tk ? (float)Kg[(int64_t)k * ldk + 4 * s + g] * c : 0.f;
+        ks_[kt][s] = k < Tk ? (float)Kg[(int64_t)k * ldk + 4 * s + g] * kc : 0.f;
         vs_[kt][s] = k < Tk ? (float)Vg[(int64_t)k * ldv + 4 * s + g] : 0.f;
       }
     }
   }
-  // K enters S = Q K^T prescaled by c = scale*log2(e) (once per workgroup; K feeds no other
-  // product here), so with S starting at -lse*log2(e) the probability is exp2 of the accumulator
-  if constexpr (BF) {
-#pragma unroll
-    for (int kt = 0; kt < KTW; ++kt)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) kf[kt][s2][j] = (bf16)((float)kf[kt][s2][j] * c);
-  }
+  // S = Q' K^T must reproduce the forward's log2-domain scores bit for bit, so that the recomputed
+  // P is the forward's P.  bf16: Q' = bf16(Q * c) exactly as the forward rounds it — either the
+  // producer wrote it (a.qpre) or the Q tiles are scaled as they are staged into LDS — and K stays
+  // as is; dK = dS^T Q' / log2(e).  fp32 (no rounding to speak of): K * c in registers unless a.qpre.
 
   f32x4 dk[KTW][4], dv[KTW][4];
 #pragma unroll
@@ -667,11 +677,20 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
     if (DROP && tid < MT) *reinterpret_cast<uint4*>(buf + 2 * TILE + 2 * KV_QT * 4 + tid * 16) = mreg;
   };
   const int nqt = (Tq + KV_QT - 1) / KV_QT;
+  auto store_q = [&](char* buf) {
+    if constexpr (BF) {
+      if (scale_q) {
+        sq.store_scaled(buf, tid, c);
+        return;
+      }
+    }
+    sq.store(buf, tid);
+  };
   sq.load(Qg, ldq, 0, Tq, tid);
   sdo.load(dOg, lddo, 0, Tq, tid);
   load_mask(0);
   load_rows(0);
-  sq.store(lds, tid);
+  store_q(lds);
   sdo.store(lds + TILE, tid);
   stage_rows(lds);
   __syncthreads();
@@ -807,7 +826,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       }
     }
     if (more) {
-      sq.store(nxt, tid);
+      store_q(nxt);
       sdo.store(nxt + TILE, tid);
       stage_rows(nxt);
     }
@@ -825,7 +844,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       const bool ok = kvalid[(int64_t)b * Tk + key] != 0;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        rp_st(dK + (int64_t)key * a.lddk + dt * 16 + i, ok ? dk[kt][dt][r] * scale : 0.f);
+        rp_st(dK + (int64_t)key * a.lddk + dt * 16 + i, ok ? dk[kt][dt][r] * dk_scale : 0.f);
         rp_st(dV + (int64_t)key * a.lddv + dt * 16 + i, ok ? dv[kt][dt][r] : 0.f);
       }
     }
@@ -912,6 +931,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
     nlq[qt] = -lq[qt];
+    if (a.qpre) continue;  // the producer already wrote Q * c
     if constexpr (BF) {
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
@@ -1203,7 +1223,7 @@ int launch_mha_bwd_dtype(int dtype, int phases, const MhaDev& a, hipStream_t s) 
 }
 
 // host validation of rp_mha_args -> MhaDev; phases 0 = forward
-int make_dev(const char* fn, int dtype, const rp_mha_args* p, int phases, MhaDev& a) {
+int make_dev(const char* fn, int dtype, int qpre, const rp_mha_args* p, int phases, MhaDev& a) {
   RP_REQUIRE(p, "%s: null args", fn);
   RP_REQUIRE(dtype == RP_BF16 || dtype == RP_F32, "%s: bad dtype %d", fn, dtype);
   RP_REQUIRE(p->head_dim == HD, "%s: head dim %d unsupported (64)", fn, p->head_dim);
@@ -1224,6 +1244,7 @@ int make_dev(const char* fn, int dtype, const rp_mha_args* p, int phases, MhaDev
   a.out = p->out; a.ldo = p->ldo; a.lse = p->lse; a.dmask = thr ? p->dropmask : nullptr;
   a.dout = p->dout; a.lddo = p->lddo; a.delta = p->delta_ws;
   a.dq = p->dq; a.lddq = p->lddq; a.dk = p->dk; a.lddk = p->lddk; a.dv = p->dv; a.lddv = p->lddv;
+  a.qpre = qpre;
   if (phases == 0 || (phases & 1)) {
     RP_REQUIRE(p->out && p->ldo >= w && p->ldo % 8 == 0 && rp_aligned16(p->out), "%s: bad out / ldo", fn);
   }
@@ -1239,9 +1260,14 @@ int make_dev(const char* fn, int dtype, const rp_mha_args* p, int phases, MhaDev
   return RP_OK;
 }
 
-int mha_fwd_entry(int dtype, const rp_mha_args* p, void* stream) {
+// the attention entry points take RP_ATTN_Q_PRESCALED or-ed into their dtype argument
+inline int attn_qpre(int dtype) { return (dtype & RP_ATTN_Q_PRESCALED) ? 1 : 0; }
+inline int attn_dtype(int dtype) { return dtype & ~RP_ATTN_Q_PRESCALED; }
+
+int mha_fwd_entry(int flagged, const rp_mha_args* p, void* stream) {
+  const int dtype = attn_dtype(flagged);
   MhaDev a;
-  const int rc = make_dev("rp_mha_fwd", dtype, p, 0, a);
+  const int rc = make_dev("rp_mha_fwd", dtype, attn_qpre(flagged), p, 0, a);
   if (rc) return rc;
   if (a.B == 0 || a.Tq == 0) return RP_OK;
   RP_REQUIRE(a.Tk > 0, "rp_mha_fwd: no keys");
@@ -1249,10 +1275,11 @@ int mha_fwd_entry(int dtype, const rp_mha_args* p, void* stream) {
   return dtype == RP_BF16 ? launch_mha_fwd<bf16>(a, s) : launch_mha_fwd<float>(a, s);
 }
 
-int mha_bwd_entry(int dtype, const rp_mha_args* p, int phases, void* stream) {
+int mha_bwd_entry(int flagged, const rp_mha_args* p, int phases, void* stream) {
   RP_REQUIRE(phases >= 1 && phases <= 7, "rp_mha_bwd: phases must be in 1..7");
+  const int dtype = attn_dtype(flagged);
   MhaDev a;
-  const int rc = make_dev("rp_mha_bwd", dtype, p, phases, a);
+  const int rc = make_dev("rp_mha_bwd", dtype, attn_qpre(flagged), p, phases, a);
   if (rc) return rc;
   if (a.B == 0 || a.Tq == 0 || a.Tk == 0) return RP_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -1304,7 +1331,7 @@ extern "C" int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid,
   RP_REQUIRE(qkv, "rp_attn_fwd: null qkv");
   rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, seed, out, lse, dropmask, nullptr, nullptr,
                          nullptr);
-  packed_offsets(a, dtype);
+  packed_offsets(a, attn_dtype(dtype));
   return mha_fwd_entry(dtype, &a, stream);
 }
 
@@ -1315,7 +1342,7 @@ static int attn_bwd_packed(int phases, int dtype, const void* qkv, const void* o
   RP_REQUIRE(qkv && dqkv, "rp_attn_bwd: null qkv / dqkv");
   rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, 0, out, const_cast<float*>(lse), dropmask, dout,
                          dqkv, delta_ws);
-  packed_offsets(a, dtype);
+  packed_offsets(a, attn_dtype(dtype));
   return mha_bwd_entry(dtype, &a, phases, stream);
 }
 
@@ -1332,6 +1359,7 @@ extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, i
   RP_REQUIRE(B >= 0 && T >= 0 && H > 0, "rp_attn_bwd_delta: bad shape");
   if (B == 0 || T == 0) return RP_OK;
   RP_REQUIRE(out && dout && delta_ws, "rp_attn_bwd_delta: null pointer");
+  dtype = attn_dtype(dtype);
   RP_REQUIRE(dtype == RP_BF16 || dtype == RP_F32, "rp_attn_bwd_delta: bad dtype");
   MhaDev a{};
   a.B = B; a.Tq = T; a.Tk = T; a.H = H; a.out = const_cast<void*>(out); a.ldo = (int64_t)H * HD; a.dout = dout;

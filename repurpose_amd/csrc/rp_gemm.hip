@@ -46,6 +46,8 @@ struct EpiDev {
   int64_t ldg;
   float gate_scale;
   int accumulate;
+  int64_t col_scale_n;  // columns n < col_scale_n are multiplied by col_scale after the bias
+  float col_scale;
 };
 
 // --- global -> register staging -----------------------------------------------------------
@@ -232,6 +234,10 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* ld
           float4 q = *reinterpret_cast<const float4*>(ep.bias + n + e);
           v[e] += q.x; v[e + 1] += q.y; v[e + 2] += q.z; v[e + 3] += q.w;
         }
+      }
+      if (n < ep.col_scale_n) {  // chunks never straddle col_scale_n (a multiple of 8)
+#pragma unroll
+        for (int e = 0; e < OV; ++e) v[e] *= ep.col_scale;
       }
       if (ep.relu) {
 #pragma unroll
@@ -730,6 +736,9 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
     e.ldg = ep->ldg;
     e.gate_scale = ep->gate_scale;
     e.accumulate = ep->accumulate;
+    e.col_scale_n = ep->col_scale_n;
+    e.col_scale = ep->col_scale;
+    RP_REQUIRE(e.col_scale_n >= 0 && e.col_scale_n % 8 == 0, "rp_gemm: col_scale_n must be a multiple of 8");
     RP_REQUIRE(!e.accumulate || c_dtype == RP_F32, "rp_gemm: accumulate needs an fp32 C");
     RP_REQUIRE(!e.drop_thresh || M * N < (int64_t)UINT32_MAX, "rp_gemm: dropout index overflow");
     RP_REQUIRE(!e.bias || rp_aligned16(e.bias), "rp_gemm: bias must be 16-byte aligned");

@@ -7,7 +7,7 @@
 //
 // Soft-NMS reproduces every reference quirk bit-for-bit in float32:
 // positional (stale) lengths, pre-swap selection score, first-index argmax, break before decay,
-// IEEE-rounded division and a correctly rounded exp (computed in double, rounded once).
+// IEEE-rounded arithmetic and numpy's own float32 exp (np_expf below).
 #include <math.h>
 
 #include "rp_common.h"
@@ -126,14 +126,42 @@ __global__ __launch_bounds__(SEL_THREADS) void select_kernel(const float* __rest
 
 // ---------------------------------------------------------------- Soft-NMS -----------------
 constexpr int NMS_THREADS = 1024;
+constexpr int NMS_LDS_CAP = 6144;  // candidates held in LDS (5 floats each, 120 KiB); beyond: workspace
 
+// numpy's float32 exp, the SIMD routine np.exp runs on AVX2 / AVX512F hosts (what the reference's
+// `np.exp(-(r*r)/sigma)` executes, models/softnms.py:35): Cody-Waite reduction by round(x*log2 e)
+// with a two-constant ln 2, a [5/2] rational minimax polynomial evaluated with FMAs, one IEEE
+// division and a 2^k scale.  It is not correctly rounded (about 10 % of the float32 inputs in
+// [-2, 0] land one ulp away from the correctly rounded exp); this restatement matches numpy 2.2
+// bit for bit on every float32 of [-2, 0] (checked exhaustively on a host: tests/golden/np_exp_check.py).
+__device__ __forceinline__ float np_expf(float x) {
+  if (x != x) return x;
+  if (x > 88.72283935546875f) return INFINITY;
+  if (x < -103.97208404541015625f) return 0.f;
+  const float q = rintf(__fmul_rn(x, 1.442695040888963407359924681001892137f));
+  float y = fmaf(q, -6.93145752e-1f, x);
+  y = fmaf(q, -1.42860677e-6f, y);
+  float num = fmaf(5.082762527590693718096e-04f, y, 6.757896990527504603057e-03f);
+  num = fmaf(num, y, 5.114512081637298353406e-02f);
+  num = fmaf(num, y, 2.473615434895520810817e-01f);
+  num = fmaf(num, y, 7.257664613233124478488e-01f);
+  num = fmaf(num, y, 9.999999999980870924916e-01f);
+  float den = fmaf(2.159509375685829852307e-02f, y, -2.742335390411667452936e-01f);
+  den = fmaf(den, y, 1.0f);
+  return ldexpf(__fdiv_rn(num, den), (int)q);
+}
+
+// One workgroup per video; per-candidate state (score, begin, end, original index, positional length)
+// in LDS for n <= NMS_LDS_CAP, else in a global workspace slice of the video (GLOBAL): the workgroup
+// barriers order those accesses the same way (workgroup-scope fences, one CU).
+template <bool GLOBAL>
 __global__ __launch_bounds__(NMS_THREADS) void softnms_kernel(const float* __restrict__ scores,
                                                               const float* __restrict__ segs,
                                                               const int* __restrict__ count, int cap, float sigma,
                                                               float thresh, const int* __restrict__ max_seg,
                                                               int* __restrict__ keep, int* __restrict__ keep_count,
-                                                              float* __restrict__ final_scores) {
-  __shared__ float s[NMS_THREADS], beg[NMS_THREADS], en[NMS_THREADS], org[NMS_THREADS], len[NMS_THREADS];
+                                                              float* __restrict__ final_scores, float* __restrict__ ws) {
+  extern __shared__ float dyn[];
   __shared__ float wv[16];
   __shared__ int wi[16];
   __shared__ int sh[32];
@@ -143,30 +171,43 @@ __global__ __launch_bounds__(NMS_THREADS) void softnms_kernel(const float* __res
   const int n = count[b];
   const int ms = max_seg[b];
   const int limit = ms < n ? ms : n;
-  if (t < n) {
-    s[t] = scores[(int64_t)b * cap + t];
-    beg[t] = segs[((int64_t)b * cap + t) * 2 + 0];
-    en[t] = segs[((int64_t)b * cap + t) * 2 + 1];
-    org[t] = (float)t;
-    len[t] = en[t] - beg[t];  // positional, never swapped (reference softnms.py:13)
+  float* base = GLOBAL ? ws + (int64_t)b * 5 * cap : dyn;
+  const int st = GLOBAL ? cap : n;
+  float* s = base;
+  float* beg = base + st;
+  float* en = base + 2 * st;
+  float* org = base + 3 * st;
+  float* len = base + 4 * st;
+  for (int e = t; e < n; e += NMS_THREADS) {
+    s[e] = scores[(int64_t)b * cap + e];
+    beg[e] = segs[((int64_t)b * cap + e) * 2 + 0];
+    en[e] = segs[((int64_t)b * cap + e) * 2 + 1];
+    org[e] = (float)e;
+    len[e] = en[e] - beg[e];  // positional, never swapped (reference softnms.py:13)
   }
+  __threadfence_block();
   __syncthreads();
   int picked = 0;
   for (int i = 0; i < n; ++i) {
     const float ts = s[i];  // pre-swap score (:18)
     if (i != n - 1) {
-      // first-index argmax over s[i+1 : n]
+      // first-index argmax over s[i+1 : n]: each thread scans its elements in increasing order
+      // (strict > keeps the first), then the wave / workgroup reductions break ties by index
       float v = -INFINITY;
       int vi = 0x7fffffff;
-      if (t > i && t < n) {
-        v = s[t];
-        vi = t;
+      for (int e = t; e < n; e += NMS_THREADS) {
+        if (e <= i) continue;
+        const float x = s[e];
+        if (vi == 0x7fffffff || x > v) {
+          v = x;
+          vi = e;
+        }
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
         const float ov = __shfl_xor(v, o, 64);
         const int oi = __shfl_xor(vi, o, 64);
-        if (ov > v || (ov == v && oi < vi)) {
+        if (oi != 0x7fffffff && (vi == 0x7fffffff || ov > v || (ov == v && oi < vi))) {
           v = ov;
           vi = oi;
         }
@@ -180,11 +221,11 @@ __global__ __launch_bounds__(NMS_THREADS) void softnms_kernel(const float* __res
         float bv = wv[0];
         int bi = wi[0];
         for (int k = 1; k < NMS_THREADS / 64; ++k)
-          if (wv[k] > bv || (wv[k] == bv && wi[k] < bi)) {
+          if (wi[k] != 0x7fffffff && (bi == 0x7fffffff || wv[k] > bv || (wv[k] == bv && wi[k] < bi))) {
             bv = wv[k];
             bi = wi[k];
           }
-        bj = (ts < bv) ? bi : -1;
+        bj = (ts < bv) ? bi : -1;  // np.amax / np.argmax; a NaN never compares greater
         if (bj >= 0) {
           // swap rows i <-> j (begin, end, original index) and scores (:23-25)
           float x;
@@ -194,30 +235,40 @@ __global__ __launch_bounds__(NMS_THREADS) void softnms_kernel(const float* __res
           x = s[i]; s[i] = s[bj]; s[bj] = x;
         }
       }
+      __threadfence_block();
       __syncthreads();
     }
     if (ts > thresh) {
       ++picked;
       if (picked >= limit) break;  // before the decay (:26-29)
     }
-    if (t > i && t < n) {
-      const float ov = fmaxf(fminf(en[i], en[t]) - fmaxf(beg[i], beg[t]), 0.f);
-      const float tl = (len[i] + len[t]) - ov;
+    const float bi = beg[i], ei = en[i], li = len[i];
+    for (int e = t; e < n; e += NMS_THREADS) {
+      if (e <= i) continue;
+      const float ov = fmaxf(__fsub_rn(fminf(ei, en[e]), fmaxf(bi, beg[e])), 0.f);
+      const float tl = __fsub_rn(__fadd_rn(li, len[e]), ov);
       const float r = __fdiv_rn(ov, tl);
-      const float e = __fdiv_rn(-(r * r), sigma);
-      const float wgt = (float)exp((double)e);
-      s[t] = __fmul_rn(wgt, s[t]);
+      const float ex = __fdiv_rn(-__fmul_rn(r, r), sigma);
+      s[e] = __fmul_rn(np_expf(ex), s[e]);
     }
+    __threadfence_block();
     __syncthreads();
   }
+  __threadfence_block();
   __syncthreads();
-  // keep = rows[s > thresh][:limit, 2]
-  const int ok = (t < n) && (s[t] > thresh);
-  int tot = 0;
-  const int pos = block_excl_scan(ok, sh, tot);
-  if (ok && pos < limit) keep[(int64_t)b * cap + pos] = (int)org[t];
-  if (t == 0) keep_count[b] = tot < limit ? tot : limit;
-  if (final_scores && t < n) final_scores[(int64_t)b * cap + t] = s[t];
+  // keep = rows[s > thresh][:limit, 2], in row order, 1024 rows per pass
+  int written = 0;
+  for (int e0 = 0; e0 < n && written < limit; e0 += NMS_THREADS) {
+    const int e = e0 + t;
+    const int ok = (e < n) && (s[e] > thresh);
+    int tot = 0;
+    const int pos = written + block_excl_scan(ok, sh, tot);
+    if (ok && pos < limit) keep[(int64_t)b * cap + pos] = (int)org[e];
+    written += tot;
+  }
+  if (t == 0) keep_count[b] = written < limit ? written : limit;
+  if (final_scores)
+    for (int e = t; e < n; e += NMS_THREADS) final_scores[(int64_t)b * cap + e] = s[e];
 }
 
 }  // namespace
@@ -236,14 +287,27 @@ extern "C" int rp_infer_select(const float* logits, const uint8_t* mask, const f
   return rp_check_launch("rp_infer_select");
 }
 
+extern "C" int64_t rp_softnms_workspace(int B, int cap) {
+  return cap > NMS_LDS_CAP && B > 0 ? (int64_t)B * 5 * cap * (int64_t)sizeof(float) : 0;
+}
+
 extern "C" int rp_softnms(const float* scores, const float* segs, const int* count, int B, int cap, float sigma,
                           float thresh, const int* max_seg, int* keep, int* keep_count, float* final_scores,
-                          void* stream) {
-  RP_REQUIRE(B >= 0 && cap >= 0 && cap <= NMS_THREADS, "rp_softnms: cap must be <= %d", NMS_THREADS);
+                          void* workspace, int64_t ws_bytes, void* stream) {
+  RP_REQUIRE(B >= 0 && cap >= 0, "rp_softnms: bad shape");
   if (B == 0) return RP_OK;
   RP_REQUIRE(count && max_seg && keep_count, "rp_softnms: null pointer");
   RP_REQUIRE(cap == 0 || (scores && segs && keep), "rp_softnms: null pointer");
-  hipLaunchKernelGGL(softnms_kernel, dim3(B), dim3(NMS_THREADS), 0, (hipStream_t)stream, scores, segs, count, cap, sigma,
-                     thresh, max_seg, keep, keep_count, final_scores);
+  hipStream_t st = (hipStream_t)stream;
+  if (cap <= NMS_LDS_CAP) {
+    const size_t lds = (size_t)5 * (cap > 0 ? cap : 1) * sizeof(float);
+    hipLaunchKernelGGL(softnms_kernel<false>, dim3(B), dim3(NMS_THREADS), lds, st, scores, segs, count, cap, sigma,
+                       thresh, max_seg, keep, keep_count, final_scores, (float*)nullptr);
+  } else {
+    RP_REQUIRE(workspace && ws_bytes >= rp_softnms_workspace(B, cap),
+               "rp_softnms: cap %d > %d needs rp_softnms_workspace(B, cap) bytes of workspace", cap, NMS_LDS_CAP);
+    hipLaunchKernelGGL(softnms_kernel<true>, dim3(B), dim3(NMS_THREADS), 0, st, scores, segs, count, cap, sigma, thresh,
+                       max_seg, keep, keep_count, final_scores, (float*)workspace);
+  }
   return rp_check_launch("rp_softnms");
 }

@@ -42,16 +42,27 @@ def find_free_port() -> int:
 
 
 def detect_slurm_env() -> Dict[str, Any]:
-    """Reference ``utils/distributed.py:32-74`` (SLURM_* variables -> rank / world / master)."""
+    """Reference ``utils/distributed.py:32-74``: torchrun's ``RANK``/``WORLD_SIZE`` win over SLURM
+    (:41-45); SLURM is used only with ``SLURM_PROCID``, ``SLURM_NTASKS`` and ``SLURM_NTASKS > 1``
+    (:46); the master is ``SLURM_LAUNCH_NODE_IPADDR`` (default ``localhost``), replaced by the first
+    node of ``SLURM_STEP_NODELIST`` when set (compressed ``node[01-04]`` -> ``node01``, :51-63);
+    port ``MASTER_PORT`` or 29500 (:66)."""
     env = os.environ
-    info = {"is_slurm": "SLURM_PROCID" in env and "SLURM_NTASKS" in env}
-    if info["is_slurm"]:
-        nodes = env.get("SLURM_JOB_NODELIST", env.get("SLURM_NODELIST", "127.0.0.1"))
-        master = nodes.split(",")[0].split("[")[0]
-        info.update(rank=int(env["SLURM_PROCID"]), world_size=int(env["SLURM_NTASKS"]),
-                    local_rank=int(env.get("SLURM_LOCALID", 0)), master_addr=env.get("MASTER_ADDR", master),
-                    master_port=int(env.get("MASTER_PORT", 29500)))
-    return info
+    if "RANK" in env and "WORLD_SIZE" in env:
+        return {"is_slurm": False}
+    if not ("SLURM_PROCID" in env and "SLURM_NTASKS" in env and int(env.get("SLURM_NTASKS", 1)) > 1):
+        return {"is_slurm": False}
+    master = env.get("SLURM_LAUNCH_NODE_IPADDR", "localhost")
+    nodes = env.get("SLURM_STEP_NODELIST")
+    if nodes is not None:
+        if "[" in nodes:
+            head, rest = nodes.split("[", 1)
+            master = head + rest.split("-")[0].split(",")[0]
+        else:
+            master = nodes.split(",")[0]
+    return {"is_slurm": True, "rank": int(env["SLURM_PROCID"]), "world_size": int(env["SLURM_NTASKS"]),
+            "local_rank": int(env.get("SLURM_LOCALID", 0)), "master_addr": master,
+            "master_port": int(env.get("MASTER_PORT", 29500))}
 
 
 def setup_distributed(rank: int, world_size: int, backend: str = "nccl", master_addr: str = "127.0.0.1",
@@ -213,37 +224,41 @@ class MultiGPUStrategy:
         self._setup_device_info()
 
     def _auto_detect_strategy(self) -> str:
-        if self.slurm_info["is_slurm"] and self.slurm_info["world_size"] > 1:
-            return "ddp"
-        if "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            return "ddp"
+        """Reference :279-311, same order: no GPU -> single; SLURM with > 1 task -> ddp; torchrun's
+        RANK / WORLD_SIZE with WORLD_SIZE > 1 -> ddp; one GPU -> single; several -> ddp."""
         if not torch.cuda.is_available():
             return "single"
+        if self.slurm_info["is_slurm"] and self.slurm_info["world_size"] > 1:
+            return "ddp"
+        if "RANK" in os.environ and "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+            return "ddp"
         return "ddp" if torch.cuda.device_count() > 1 else "single"
 
     def _setup_device_info(self):
+        """Reference :313-353.  'dp' (nn.DataParallel in the reference, :409-413) runs on one device:
+        a single process cannot replicate the flat-buffer model across GPUs, and one process per GPU
+        (ddp) is the MI355X path — a documented divergence, with a warning."""
         if self.strategy in ("single", "dp"):
             if self.strategy == "dp":
-                # single-process DataParallel cannot replicate a flat-buffer model; one process per
-                # GPU (ddp) is the MI355X path, 'dp' runs on one device
                 self.logger.warning("strategy 'dp' runs single-device on MI355X; launch one process per GPU")
             self.device = get_device()
             self.world_size, self.rank, self.local_rank = 1, 0, 0
             return
         self.is_distributed = True
+        ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
         if self.slurm_info["is_slurm"]:
             self.rank, self.world_size = self.slurm_info["rank"], self.slurm_info["world_size"]
             self.local_rank = self.slurm_info["local_rank"]
         elif "RANK" in os.environ:
             self.rank = int(os.environ["RANK"])
             self.world_size = int(os.environ["WORLD_SIZE"])
-            ndev = torch.cuda.device_count() if torch.cuda.is_available() else 1
             self.local_rank = int(os.environ.get("LOCAL_RANK", self.rank % max(ndev, 1)))
         else:
             self.rank, self.local_rank = 0, 0
-            self.world_size = torch.cuda.device_count() if torch.cuda.is_available() else 1
-        self.device = (torch.device("cuda", self.local_rank) if torch.cuda.is_available() and self.backend == "nccl"
-                       else torch.device("cpu"))
+            self.world_size = ndev if ndev else 1
+        # cuda:{local_rank} as the reference (:349-350); ranks beyond the device count (a gloo
+        # rehearsal of N ranks on one GPU) share devices round robin
+        self.device = torch.device("cuda", self.local_rank % ndev) if ndev else torch.device("cpu")
 
     def setup(self) -> bool:
         if self.strategy == "ddp" and self.world_size > 1:

@@ -12,6 +12,13 @@ import torch
 from . import _native as N
 
 _DT = {torch.float32: N.RP_F32, torch.bfloat16: N.RP_BF16}
+RP_ATTN_Q_PRESCALED = 0x100  # include/rp_api.h: q holds Q * scale * log2(e)
+LOG2E = 1.4426950408889634
+
+
+def _adt(t, q_prescaled):
+    """dtype argument of the attention entry points (with the Q-prescaled flag)."""
+    return _dt(t) | (RP_ATTN_Q_PRESCALED if q_prescaled else 0)
 
 # Live per-kernel timing with HIP events recorded on the launch stream (bench.py roofline).
 _timer = {"names": (), "ev": {}}
@@ -97,7 +104,7 @@ def cast_bf16(src, dst):
 # ------------------------------------------------------------------------------------- GEMM
 def gemm(A, B, C, M, Nn, K, lda, a_kmajor, ldb, b_kmajor, ldc, alpha=1.0, bias=None, relu=False,
          dropout_p=0.0, seed=0, residual=None, ldr=0, gate=None, ldg=0, gate_scale=1.0,
-         accumulate=False):
+         accumulate=False, col_scale_n=0, col_scale=1.0):
     """Raw rp_gemm (see include/rp_api.h for the operand conventions)."""
     _gpu(A, B, C, bias, residual, gate)
     if A.dtype != B.dtype:
@@ -105,20 +112,22 @@ def gemm(A, B, C, M, Nn, K, lda, a_kmajor, ldb, b_kmajor, ldc, alpha=1.0, bias=N
     ep = N.GemmEpilogue(_p(bias).value, int(relu), float(dropout_p), int(seed) & 0xFFFFFFFF,
                         _p(residual).value, int(ldr), _p(gate).value,
                         _dt(gate) if gate is not None else 0, int(ldg), float(gate_scale),
-                        int(accumulate))
+                        int(accumulate), int(col_scale_n), float(col_scale))
     N.call("rp_gemm", _dt(A), int(M), int(Nn), int(K), _p(A), int(lda), int(a_kmajor), _p(B), int(ldb),
            int(b_kmajor), _p(C), int(ldc), _dt(C), float(alpha), ctypes.byref(ep), _stream(A))
     return C
 
 
-def linear_fwd(x, W, b=None, out_dtype=None, relu=False, dropout_p=0.0, seed=0, residual=None, tag=None):
-    """y = epilogue(x W^T + b); x [M, K], W [N, K] (same dtype), residual fp32 [M, N]."""
+def linear_fwd(x, W, b=None, out_dtype=None, relu=False, dropout_p=0.0, seed=0, residual=None, tag=None,
+               col_scale_n=0, col_scale=1.0):
+    """y = epilogue(x W^T + b); x [M, K], W [N, K] (same dtype), residual fp32 [M, N]; columns
+    < col_scale_n are multiplied by col_scale after the bias (the attention's Q prescale)."""
     M, K = x.shape
     Nn = W.shape[0]
     out = torch.empty(M, Nn, device=x.device, dtype=out_dtype or x.dtype)
     e0 = _tick(tag) if tag else None
     gemm(x, W, out, M, Nn, K, K, True, K, True, Nn, bias=b, relu=relu, dropout_p=dropout_p,
-         seed=seed, residual=residual, ldr=Nn)
+         seed=seed, residual=residual, ldr=Nn, col_scale_n=col_scale_n, col_scale=col_scale)
     _tock(e0)
     return out
 
@@ -217,9 +226,10 @@ def colsum(X, w=None, out=None, accumulate=False, ws=None):
 
 
 # ------------------------------------------------------------------------------------- attention
-def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0):
+def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, q_prescaled=False):
     """-> (out [B*T, H*dk], lse [B, H, T], dropmask or None).  The dropout keep bits drawn by the
-    forward are returned and must be handed to attn_bwd."""
+    forward are returned and must be handed to attn_bwd.  q_prescaled: the Q columns of qkv hold
+    Q * scale * log2(e) (linear_fwd's col_scale); the same flag must go to attn_bwd."""
     _gpu(qkv, key_valid)
     _contig(qkv, key_valid)
     dk = qkv.shape[1] // (3 * H)
@@ -229,7 +239,7 @@ def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0):
     if dropout_p > 0:
         mask = torch.empty(N.load().rp_attn_dropmask_elems(B, T, H), device=qkv.device, dtype=torch.int16)
     e0 = _tick("attn_fwd")
-    N.call("rp_attn_fwd", _dt(qkv), _p(qkv), _p(key_valid), B, T, H, dk, float(scale), float(dropout_p),
+    N.call("rp_attn_fwd", _adt(qkv, q_prescaled), _p(qkv), _p(key_valid), B, T, H, dk, float(scale), float(dropout_p),
            int(seed) & 0xFFFFFFFF, _p(out), _p(lse), _p(mask), _stream(qkv))
     _tock(e0)
     return out, lse, mask
@@ -238,7 +248,8 @@ def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0):
 _FUSED_DELTA = os.environ.get("RP_ATTN_FUSED_DELTA", "1") != "0"
 
 
-def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, dropmask=None):
+def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, dropmask=None,
+             q_prescaled=False):
     _gpu(qkv, out, dout, lse, key_valid, dropmask)
     _contig(qkv, out, dout, lse, key_valid)
     if dropout_p > 0 and dropmask is None:
@@ -246,7 +257,7 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
     dk = qkv.shape[1] // (3 * H)
     dqkv = torch.empty_like(qkv)
     delta = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
-    st, dt = _stream(qkv), _dt(qkv)
+    st, dt = _stream(qkv), _adt(qkv, q_prescaled)
     e0 = _tick("attn_bwd")
     if _FUSED_DELTA:  # dQ first, with the delta = rowsum(dO * O) pre-pass fused in; dK/dV reads it
         e2 = _tick("attn_bwd_dq")
@@ -275,7 +286,7 @@ def _rows(t, H, dk):
     return t.data_ptr(), t.stride(0)
 
 
-def mha_fwd(q, k, v, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, seed=0):
+def mha_fwd(q, k, v, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, seed=0, q_prescaled=False):
     """General (self / cross) attention core.  q [B*Tq, >=H*dk], k/v [B*Tk, >=H*dk] row views (any row
     stride), key_valid [B, Tk] uint8.  -> (out [B*Tq, H*dk], lse [B, H, Tq], dropmask or None)."""
     _gpu(q, k, v, key_valid)
@@ -298,11 +309,12 @@ def mha_fwd(q, k, v, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, seed=0):
     a.out, a.ldo = out.data_ptr(), out.stride(0)
     a.lse = lse.data_ptr()
     a.dropmask = mask.data_ptr() if mask is not None else None
-    N.call("rp_mha_fwd", _dt(q), ctypes.byref(a), _stream(q))
+    N.call("rp_mha_fwd", _adt(q, q_prescaled), ctypes.byref(a), _stream(q))
     return out, lse, mask
 
 
-def mha_bwd(q, k, v, out, dout, lse, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, dropmask=None):
+def mha_bwd(q, k, v, out, dout, lse, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, dropmask=None,
+            q_prescaled=False):
     """-> (dq [B*Tq, H*dk], dk [B*Tk, H*dk], dv [B*Tk, H*dk]) for mha_fwd's inputs."""
     _gpu(q, k, v, out, dout, lse, key_valid, dropmask)
     _contig(out, dout, lse, key_valid)
@@ -328,7 +340,7 @@ def mha_bwd(q, k, v, out, dout, lse, key_valid, B, Tq, Tk, H, scale, dropout_p=0
     a.dk, a.lddk = dkk.data_ptr(), dkk.stride(0)
     a.dv, a.lddv = dv.data_ptr(), dv.stride(0)
     a.delta_ws = delta.data_ptr()
-    N.call("rp_mha_bwd", _dt(q), ctypes.byref(a), 7, _stream(q))
+    N.call("rp_mha_bwd", _adt(q, q_prescaled), ctypes.byref(a), 7, _stream(q))
     return dq, dkk, dv
 
 
@@ -420,8 +432,10 @@ def softnms(scores, segs, count, sigma, thresh, max_seg, want_final_scores=False
     keep = torch.empty(B, max(cap, 1), device=scores.device, dtype=torch.int32)
     keep_count = torch.empty(B, device=scores.device, dtype=torch.int32)
     final = torch.empty_like(scores) if want_final_scores else None
+    nws = N.load().rp_softnms_workspace(B, cap)
+    ws = torch.empty(max(nws // 4, 1), device=scores.device, dtype=torch.float32) if nws else None
     N.call("rp_softnms", _p(scores), _p(segs), _p(count), B, cap, float(sigma), float(thresh), _p(max_seg),
-           _p(keep), _p(keep_count), _p(final), _stream(scores))
+           _p(keep), _p(keep_count), _p(final), _p(ws), int(nws), _stream(scores))
     return keep, keep_count, final
 
 

@@ -89,21 +89,52 @@ def tiou_precision_batched(gt_segments, pred_segments, tiou_thresholds=THRESHOLD
     return torch.where(n > 0, hits / n.clamp(min=1), torch.zeros_like(hits))
 
 
-def evaluate_tiou(gt_segments, pred_segments, tiou_thresholds=THRESHOLDS, gather=True):
+def gather_precisions(prec, video_ids=None, group=None):
+    """All ranks' per-video precision rows [V_r, n_thr], concatenated in rank order.  The test
+    loader's DistributedSampler (drop_last=False) pads the last shard by repeating videos, so with
+    ``video_ids`` (one per row) each video is kept once, at its first occurrence — the mean is then
+    over the split, not biased toward the repeated videos.  gloo gathers through host memory."""
+    world = dist.get_world_size(group)
+    host = dist.get_backend(group) == "gloo"
+    src = prec.detach().double().cpu() if host else prec.detach().double()
+    n = torch.tensor([src.shape[0]], device=src.device, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    cap = max(1, int(max(s.item() for s in sizes)))
+    pad = torch.zeros(cap, src.shape[1], device=src.device, dtype=src.dtype)
+    pad[:src.shape[0]] = src
+    parts = [torch.zeros_like(pad) for _ in sizes]
+    dist.all_gather(parts, pad, group=group)
+    out = torch.cat([p[:int(s.item())] for p, s in zip(parts, sizes)], 0)
+    if video_ids is not None:
+        if len(video_ids) != prec.shape[0]:
+            raise ValueError("gather_precisions: one video id per precision row")
+        ids = [None] * world
+        dist.all_gather_object(ids, list(video_ids), group=group)
+        seen, keep = set(), []
+        for i, v in enumerate(x for r in ids for x in r):
+            if v not in seen:
+                seen.add(v)
+                keep.append(i)
+        out = out[torch.tensor(keep, dtype=torch.long, device=out.device)]
+    return out.to(prec.device)
+
+
+def evaluate_tiou(gt_segments, pred_segments, tiou_thresholds=THRESHOLDS, gather=True, video_ids=None):
     """main.py:685-703 aggregation: tIoU[th] = mean over videos, AtIoU = mean over thresholds.
     With torch.distributed initialised (and gather=True) the per-video precisions of all ranks are
-    gathered first.  Returns (tIoU dict, AtIoU, number of videos scored)."""
+    gathered first (``gather_precisions``; pass ``video_ids`` to drop the sampler's padding
+    repeats).  Returns (tIoU dict, AtIoU, number of videos scored)."""
     prec = tiou_precision_batched(gt_segments, pred_segments, tiou_thresholds)
     if gather and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        n = torch.tensor([prec.shape[0]], device=prec.device, dtype=torch.int64)
-        sizes = [torch.zeros_like(n) for _ in range(dist.get_world_size())]
-        dist.all_gather(sizes, n)
-        cap = int(max(s.item() for s in sizes))
-        pad = torch.zeros(cap, prec.shape[1], device=prec.device, dtype=prec.dtype)
-        pad[:prec.shape[0]] = prec
-        parts = [torch.zeros_like(pad) for _ in sizes]
-        dist.all_gather(parts, pad)
-        prec = torch.cat([p[:int(s.item())] for p, s in zip(parts, sizes)], 0)
+        prec = gather_precisions(prec, video_ids)
+    elif video_ids is not None:  # one process: drop repeats too
+        seen, keep = set(), []
+        for i, v in enumerate(video_ids):
+            if v not in seen:
+                seen.add(v)
+                keep.append(i)
+        prec = prec[torch.tensor(keep, dtype=torch.long, device=prec.device)]
     if prec.shape[0] == 0:
         raise ZeroDivisionError("evaluate_tiou: no videos (the reference divides by len(total_tIoU))")
     mean = prec.mean(0).cpu().tolist()

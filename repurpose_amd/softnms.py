@@ -5,15 +5,13 @@ exact semantics, including the side effect of the reference on CPU score tensors
 aliases a CPU tensor, so the reference leaves the decayed, permuted scores in the caller's tensor
 (SURVEY App. A-1).  When the caller passes a CPU tensor, the final score array computed on the GPU
 is copied back into it; GPU tensors are left untouched (``.cpu()`` copies in the reference too).
-The computation itself always runs on the GPU: there is no CPU fallback.
+The computation itself always runs on the GPU: there is no CPU fallback.  Any number of candidates
+(the reference has no cap; inference_ passes at most pre_nms_topk = 1000).
 """
 import numpy as np
 import torch
 
 from . import kernels as K
-
-MAX_CANDIDATES = 1024
-
 
 def _device():
     if not torch.cuda.is_available():
@@ -26,8 +24,6 @@ def soft_nms_intervals_cpu(out_cls_logits, out_offsets, sigma=0.5, thresh=0.001,
     scores = torch.as_tensor(out_cls_logits)
     segs = torch.as_tensor(out_offsets)
     n = int(segs.shape[0])
-    if n > MAX_CANDIDATES:
-        raise ValueError(f"soft_nms: {n} candidates > {MAX_CANDIDATES} (pre_nms_topk caps this at 1000)")
     dev = scores.device if scores.is_cuda else _device()
     s = scores.reshape(1, n).to(dev, torch.float32)
     g = segs.reshape(1, n, 2).to(dev, torch.float32)

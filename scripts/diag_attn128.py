@@ -7,7 +7,7 @@ from repurpose_amd import kernels as K
 dev = torch.device("cuda")
 B, H, T, p = 8, 8, 1030, float(sys.argv[1]) if len(sys.argv) > 1 else 0.1
 qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(torch.bfloat16)
-lens = torch.tensor([T, T - 1, 1000, 777, 640, 129, 64, 1], device=dev)
+lens = torch.tensor([T, T - 1, 1000, 777, 640, 129, 2, 1], device=dev)
 kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
 o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 99)
 ref_in = qkv.double().requires_grad_(True)
@@ -28,3 +28,8 @@ for r, c in idx[:30].tolist():
 parts = torch.bincount((idx[:, 1] // (H * 64)), minlength=3).tolist() if idx.numel() else []
 bs = torch.bincount(idx[:, 0] // T, minlength=B).tolist() if idx.numel() else []
 print("by part", parts, "by batch", bs)
+# per batch / part max error
+for b in range(B):
+    rows = slice(b * T, (b + 1) * T)
+    print(b, int(lens[b]), [round(err[rows, i * H * 64:(i + 1) * H * 64].max().item(), 4) for i in range(3)],
+          "ref max", [round(g[rows, i * H * 64:(i + 1) * H * 64].abs().max().item(), 3) for i in range(3)])

@@ -38,7 +38,10 @@ def _worker(rank, world, port, q):
                       LOCAL_RANK=str(rank))
     try:
         from repurpose_amd.distributed import GradAllReducer, MultiGPUStrategy, get_rank, get_world_size
-        s = MultiGPUStrategy(strategy="auto", backend="gloo", timeout=60)
+        from repurpose_amd.metrics import gather_precisions
+        # no GPU here: 'auto' resolves to single exactly as the reference (:281-282), so ask for ddp
+        assert MultiGPUStrategy(strategy="auto", backend="gloo").strategy == "single"
+        s = MultiGPUStrategy(strategy="ddp", backend="gloo", timeout=60)
         assert s.strategy == "ddp" and s.world_size == world and s.rank == rank
         assert s.setup() is True
         assert get_rank() == rank and get_world_size() == world
@@ -47,10 +50,28 @@ def _worker(rank, world, port, q):
         assert s.reduce_tensor(torch.tensor([1.0]), average=False).item() == world
         assert s.get_effective_batch_size(6) == 6 * world
         s.barrier()
-        # DistributedSampler partitioning (seed 0 + epoch, padded to a multiple of world)
-        dl = s.create_dataloader(list(range(11)), batch_size=2, shuffle=False)
-        seen = [int(x) for b in dl for x in b]
-        assert seen == list(range(11 + 1))[rank::world][: 6] or len(seen) == 6
+        # DistributedSampler partitioning (utils/distributed.py:453-461): the index list (a seed 0 +
+        # epoch permutation when shuffling), padded with its own head to a multiple of world, then
+        # rank r takes positions r, r + world, ...
+        for shuffle, epoch in ((False, 0), (True, 0), (True, 3)):
+            dl = s.create_dataloader(list(range(11)), batch_size=2, shuffle=shuffle)
+            dl.sampler.set_epoch(epoch)
+            seen = [int(x) for b in dl for x in b]
+            if shuffle:
+                gen = torch.Generator()
+                gen.manual_seed(0 + epoch)
+                order = torch.randperm(11, generator=gen).tolist()
+            else:
+                order = list(range(11))
+            order = order + order[:12 - 11]
+            assert seen == order[rank::world], (shuffle, epoch, seen)
+        # evaluate_tiou's cross-rank gather: 3 videos over 2 ranks -> rank 1's shard repeats video 0
+        ids = ["a", "c"] if rank == 0 else ["b", "a"]
+        prec = torch.tensor([[0.5, 0.25], [1.0, 0.0]]) if rank == 0 else torch.tensor([[0.0, 0.0], [0.5, 0.25]])
+        allp = gather_precisions(prec)
+        assert allp.shape == (4, 2)
+        uniq = gather_precisions(prec, ids)
+        assert torch.equal(uniq, torch.tensor([[0.5, 0.25], [1.0, 0.0], [0.0, 0.0]], dtype=torch.float64))
         # gradient reducer: ranges arrive in reverse order, buckets of 8 elements
         m = FakeModel(40, 36)
         r = GradAllReducer(m, bucket_mb=8 * 4 / 2 ** 20)
@@ -84,6 +105,47 @@ def test_strategy_and_reducer_world2():
         p.join(timeout=60)
     for rank, msg in res:
         assert msg == "ok", f"rank {rank}: {msg}"
+
+
+def test_detect_slurm_env_reference_priority(monkeypatch):
+    """utils/distributed.py:32-74: torchrun wins over SLURM; SLURM needs NTASKS > 1; master from the
+    first node of SLURM_STEP_NODELIST (compressed form too), else SLURM_LAUNCH_NODE_IPADDR / localhost."""
+    from repurpose_amd.distributed import detect_slurm_env
+    for k in ("RANK", "WORLD_SIZE", "SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID", "SLURM_STEP_NODELIST",
+              "SLURM_LAUNCH_NODE_IPADDR", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    assert detect_slurm_env() == {"is_slurm": False}
+    monkeypatch.setenv("SLURM_PROCID", "3")
+    monkeypatch.setenv("SLURM_NTASKS", "1")
+    assert detect_slurm_env()["is_slurm"] is False  # a one-task allocation is not distributed
+    monkeypatch.setenv("SLURM_NTASKS", "8")
+    monkeypatch.setenv("SLURM_LOCALID", "1")
+    info = detect_slurm_env()
+    assert info == {"is_slurm": True, "rank": 3, "world_size": 8, "local_rank": 1, "master_addr": "localhost",
+                    "master_port": 29500}
+    monkeypatch.setenv("SLURM_LAUNCH_NODE_IPADDR", "10.0.0.7")
+    assert detect_slurm_env()["master_addr"] == "10.0.0.7"
+    monkeypatch.setenv("SLURM_STEP_NODELIST", "gpu[01-04]")
+    monkeypatch.setenv("MASTER_PORT", "1234")
+    info = detect_slurm_env()
+    assert info["master_addr"] == "gpu01" and info["master_port"] == 1234
+    monkeypatch.setenv("SLURM_STEP_NODELIST", "nodeA,nodeB")
+    assert detect_slurm_env()["master_addr"] == "nodeA"
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert detect_slurm_env() == {"is_slurm": False}  # torchrun's variables take priority
+
+
+def test_dp_strategy_is_single_device_with_warning(caplog):
+    """'dp' (nn.DataParallel in the reference, utils/distributed.py:409-413) runs on one device here:
+    the documented divergence — one process per GPU (ddp) is the multi-GPU path."""
+    from repurpose_amd.distributed import MultiGPUStrategy
+    with caplog.at_level("WARNING"):
+        s = MultiGPUStrategy(strategy="dp")
+    assert s.strategy == "dp" and s.world_size == 1 and not s.is_distributed
+    assert any("single-device" in r.getMessage() for r in caplog.records)
+    m = torch.nn.Linear(2, 2)
+    assert s.wrap_model(m) is m
 
 
 def test_single_strategy_passthrough():

@@ -1,0 +1,133 @@
+"""The real data-parallel path on the GPU, two ranks: MultiGPUStrategy.setup() / wrap_model(), the
+HIP backward's flat-range hooks driving GradAllReducer's bucketed all-reduce, FusedAdam on the
+wrapper.  Reference semantics (utils/distributed.py:396-433 DDP around main.py:331-369): after
+``loss.backward()`` every rank holds the mean over ranks of its local gradient of
+``cls_loss / batch_size``, and the parameters were broadcast from rank 0 at wrap time.
+
+Both ranks share the box's one GPU, so the rehearsal uses the gloo backend (RCCL refuses two ranks
+on one device); the driver's 8-GPU bench runs the same code over RCCL (backend "nccl")."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+CFG = dict(vis_dim=512, aud_dim=2048, text_dim=384, d_model=512, self_num_layers=2, text_num_layers=3,
+           cross_num_layers=3, num_heads=8)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch(seed=5):
+    g = torch.Generator().manual_seed(seed)
+    B, T, lens = 2, 96, [96, 70]
+    return {"visual_feats": torch.randn(B, T, 512, generator=g), "audio_feats": torch.relu(torch.randn(B, T, 2048, generator=g)),
+            "text_feats": torch.randn(B, T, 384, generator=g),
+            "masks": (torch.arange(T)[None] < torch.tensor(lens)[:, None]).unsqueeze(1),
+            "labels": (torch.rand(B, T, generator=g) < 0.35).float(), "segments": torch.rand(B, T, 2, generator=g) * 10}
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        import torch.distributed as dist
+        from repurpose_amd.distributed import DistributedModel, MultiGPUStrategy
+        from repurpose_amd.MMCTransformer import MMCTransformer
+        from repurpose_amd.optim import FusedAdam
+
+        s = MultiGPUStrategy(strategy="auto", backend="gloo", timeout=120)
+        assert s.strategy == "ddp" and s.world_size == world and s.rank == rank, (s.strategy, s.world_size)
+        assert s.setup() is True
+        dev = s.device
+        assert dev.type == "cuda"
+
+        def fresh(seed):
+            torch.manual_seed(seed)
+            m = MMCTransformer(**CFG, compute_dtype="fp32")
+            m.DROPOUT = 0.0  # dropout off: the per-rank gradients are comparable bit for bit
+            return m
+
+        m = fresh(100 + rank)  # different init per rank: the wrap must broadcast rank 0's
+        w = s.wrap_model(m)
+        assert isinstance(w, DistributedModel) and w.module is m
+        init0 = fresh(100).flat_params().clone()
+        assert torch.equal(m.flat_params().cpu(), init0), "parameters not broadcast from rank 0"
+        opt = FusedAdam(w.parameters(), lr=1e-3, weight_decay=1e-4)
+
+        full = _batch()
+        mine = {k: v[rank:rank + 1].to(dev) for k, v in full.items()}  # one sequence per rank
+        w.train()
+        opt.zero_grad()
+        out = w(mine)
+        loss = w.module.losses(*out)["cls_loss"] / 1  # main.py:331 (batch_size = 1 per rank)
+        loss.backward()
+        torch.cuda.synchronize()
+        g_ddp = m.flat_grads().clone()
+
+        # single-process DDP average: mean over ranks of each rank's local gradient
+        ref = fresh(0)
+        ref.load_state_dict(m.state_dict())
+        ref.to(dev).train()
+        acc = None
+        for r in range(world):
+            ref.zero_grad(set_to_none=True)
+            o = ref({k: v[r:r + 1].to(dev) for k, v in full.items()})
+            ref.losses(*o)["cls_loss"].backward()
+            g = ref.flat_grads().clone()
+            acc = g if acc is None else acc + g
+        want = acc / world
+        n = m.trainable_numel()
+        rel = ((g_ddp[:n] - want[:n]).abs().max() / want[:n].abs().max()).item()
+        assert rel < 1e-5, f"DDP gradient differs from the mean of per-rank gradients: rel {rel:.2e}"
+        assert torch.equal(g_ddp[n:], torch.zeros_like(g_ddp[n:]))  # reg_head: no gradient anywhere
+
+        # the averaged loss (main.py:378-380) and identical parameters on every rank after Adam
+        avg = s.reduce_tensor(loss.detach())
+        both = torch.zeros(world, device=dev)
+        both[rank] = loss.detach()
+        dist.all_reduce(both)
+        assert abs(avg.item() - both.mean().item()) < 1e-5 * max(1.0, abs(avg.item()))
+        opt.step()
+        torch.cuda.synchronize()
+        mine_p = m.flat_params().clone()
+        rank0_p = mine_p.clone()
+        dist.broadcast(rank0_p, src=0)
+        assert torch.equal(mine_p, rank0_p), "ranks diverged after the optimizer step"
+        s.barrier()
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_ddp_two_ranks_real_backward(dev):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=240) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, msg in sorted(res):
+        assert msg == "ok", f"rank {rank}: {msg}"

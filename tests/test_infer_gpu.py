@@ -72,7 +72,30 @@ def test_softnms_batched_random_vs_oracle(dev):
         s = torch.from_numpy(sc[b, :cnt[b]].copy())
         ref = nms_ref(s, torch.from_numpy(sg[b, :cnt[b]]), 0.5, 0.01, ms[b])
         assert keep[b, :kc[b]].tolist() == ref.tolist(), f"video {b}"
-        np.testing.assert_allclose(final[b, :cnt[b]].cpu().numpy(), s.numpy(), rtol=1e-6, atol=1e-7)
+        # every decayed score bit for bit: the kernel's exp is numpy's float32 exp algorithm
+        np.testing.assert_array_equal(final[b, :cnt[b]].cpu().numpy(), s.numpy())
+
+
+@pytest.mark.parametrize("n,ms", [(1500, 1500), (3000, 40), (7000, 7000)])
+def test_softnms_beyond_1024_candidates(dev, n, ms):
+    """The reference function has no candidate cap (models/softnms.py:3-38): 1500 / 3000 candidates
+    run from LDS, 7000 from the global workspace path; indices and final scores match numpy."""
+    rs = np.random.RandomState(n)
+    s = np.sort(rs.uniform(0.0, 1, n).astype(np.float32))[::-1].copy()
+    c = rs.uniform(0, 20000, n).astype(np.float32)
+    g = np.stack([c - rs.uniform(5.5, 45, n), c + rs.uniform(5.5, 45, n)], 1).astype(np.float32)
+    keep, kc, final = K.softnms(torch.from_numpy(s).view(1, n).to(dev), torch.from_numpy(g).view(1, n, 2).to(dev),
+                                torch.tensor([n], dtype=torch.int32, device=dev), 0.5, 0.01,
+                                torch.tensor([ms], dtype=torch.int32, device=dev), want_final_scores=True)
+    st = torch.from_numpy(s.copy())
+    ref = nms_ref(st, torch.from_numpy(g), 0.5, 0.01, ms)
+    assert keep[0, :int(kc[0])].cpu().tolist() == ref.tolist()
+    np.testing.assert_array_equal(final[0].cpu().numpy(), st.numpy())
+    # and through the drop-in (CPU tensors in, the reference's in-place side effect out)
+    st2 = torch.from_numpy(s.copy())
+    k2 = nms_gpu(st2, torch.from_numpy(g), 0.5, 0.01, ms)
+    assert k2.tolist() == ref.tolist()
+    np.testing.assert_array_equal(st2.numpy(), st.numpy())
 
 
 def test_select_matches_oracle(dev):

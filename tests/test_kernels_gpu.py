@@ -49,6 +49,23 @@ def rnd(*shape, dev, scale=1.0, seed=0):
     return (torch.randn(*shape, generator=g) * scale).to(dev)
 
 
+def close_per_seq(a, b, B, atol, rtol=0.0, what=""):
+    """close() with the absolute tolerance taken relative to each sequence's gradient magnitude
+    (rows [B*T, cols], sequence s = rows s*T..): a sequence with one or two valid keys collects every
+    query's probability mass on them, so its dV is a sum of ~T dO rows (|dV| ~ 100 at T = 1030) and
+    an absolute bound sized for |dV| ~ 1 would demand 5 significant digits from bf16."""
+    a = a.double().cpu()
+    b = b.double().cpu()
+    T = a.shape[0] // B
+    lim = torch.empty_like(b)
+    for s_ in range(B):
+        rows = slice(s_ * T, (s_ + 1) * T)
+        lim[rows] = atol * max(1.0, b[rows].abs().max().item()) + rtol * b[rows].abs()
+    err = (a - b).abs()
+    bad = (err > lim).sum().item()
+    assert bad == 0, f"{what}: {bad} elements off, max err {err.max().item():.3e}"
+
+
 def close(a, b, atol, rtol=0.0, what=""):
     a = a.double().cpu()
     b = b.double().cpu()
@@ -266,21 +283,37 @@ def test_mha_cross_strided(dev, dtype, Tq, Tk):
     close(dv, gv, atol=btol, rtol=btol, what="mha dv")
 
 
+def prescale_q(qkv, H, scale):
+    """The model's QKV GEMM epilogue (col_scale): Q columns -> bf16(Q * scale * log2 e).  Returns the
+    kernel operand and the fp64 Q it stands for (Q' / c), which the reference then uses."""
+    c = scale * K.LOG2E
+    qp = qkv.clone()
+    qp[:, :H * 64] = (qkv[:, :H * 64].float() * c).to(qkv.dtype)
+    eff = qp.double()
+    eff[:, :H * 64] /= c
+    return qp, eff
+
+
 @pytest.mark.gpu
-def test_attention_128_blocks_ragged_dropout(dev):
+@pytest.mark.parametrize("q_prescaled", [False, True])
+def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
     """Self attention on the 128-row block path (B*H*ceil(T/128) >= 512 workgroups; the smaller test
-    shapes above take the 64-row path), ragged T and key padding, dropout keep bits vs the
-    restatement, fwd and bwd vs fp64."""
+    shapes above take the 64-row path), ragged T and key padding down to one and two valid keys,
+    dropout keep bits vs the restatement, fwd and bwd vs fp64.  A sequence with one valid key puts
+    every query's whole mass on it, so its dV sums ~1000 recomputed probabilities: this pins that the
+    backward recomputes exactly the forward's P (same bf16-rounded Q * scale * log2 e in all three
+    kernels, with the prescale done by the kernels or by the producer)."""
     B, H, T, p = 8, 8, 1030, 0.1
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(torch.bfloat16)
-    # key lengths >= 33: with one valid key every query's whole mass lands on it and dK/dV sum ~1000
-    # bf16-recomputed P values (forward and backward prescale different operands by scale*log2e, so P
-    # differs by ~2^-8 relative), which exceeds a fixed absolute tolerance; fp32 mode has no such gap
-    lens = torch.tensor([T, T - 1, 1000, 777, 640, 129, 64, 33], device=dev)
+    lens = torch.tensor([T, T - 1, 1000, 777, 640, 129, 2, 1], device=dev)
     kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
     seed = 99
-    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed)
-    ref_in = qkv.double().requires_grad_(True)
+    if q_prescaled:
+        qkv, eff = prescale_q(qkv, H, 0.125)
+    else:
+        eff = qkv.double()
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=q_prescaled)
+    ref_in = eff.requires_grad_(True)
     ref = attn_ref(ref_in, kv, B, T, H, p, seed)
     close(o, ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd (128 blocks)")
     KT, ldm = (T + 63) // 64, (T + 63) // 64 * 64
@@ -289,9 +322,16 @@ def test_attention_128_blocks_ragged_dropout(dev):
     got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, T, KT * 64)[:, :, :T].bool()
     assert torch.equal(got, attn_keep(B, H, T, p, seed, dev).view(B * H, T, T))
     do = rnd(B * T, H * 64, dev=dev, seed=T + 1).to(torch.bfloat16)
-    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask)
+    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=q_prescaled)
     gref = torch.autograd.grad(ref, ref_in, do.double())[0]
-    close(dqkv, gref, atol=6e-2, rtol=6e-2, what="attn bwd (128 blocks)")
+    for part, name in enumerate("qkv"):
+        cols = slice(part * H * 64, (part + 1) * H * 64)
+        close_per_seq(dqkv[:, cols], gref[:, cols], B, atol=6e-2, rtol=6e-2, what=f"attn d{name} (128 blocks)")
+    # the one-key sequence (dK = 0: its scores never matter; dV = the kept dO mass of all queries):
+    # the recomputed P is the forward's, so dV is within bf16 rounding of the exact sum
+    rows = slice(7 * T, 7 * T + 1)
+    dv1, rv1 = dqkv[rows, 2 * H * 64:].double().cpu(), gref[rows, 2 * H * 64:].cpu()
+    assert ((dv1 - rv1).abs().max() / rv1.abs().max()).item() < 1e-2
 
 
 @pytest.mark.gpu
@@ -301,7 +341,7 @@ def test_mha_cross_128_blocks(dev):
     q = rnd(B * Tq, H * dk, dev=dev, seed=5).to(torch.bfloat16)
     kvbuf = rnd(B * Tk, 2 * H * dk, dev=dev, seed=6).to(torch.bfloat16)
     k, v = kvbuf[:, :H * dk], kvbuf[:, H * dk:]
-    lens = torch.tensor([Tk, 999, 900, 513, 500, 128, 65, 40], device=dev)  # >= 33: see the test above
+    lens = torch.tensor([Tk, 999, 900, 513, 500, 128, 2, 1], device=dev)  # one / two valid keys: see above
     kv = (torch.arange(Tk, device=dev)[None] < lens[:, None]).to(torch.uint8)
     o, lse, _ = K.mha_fwd(q, k, v, kv, B, Tq, Tk, H, 0.125)
     qd, kd, vd = (t.double().requires_grad_(True) for t in (q, k, v))
@@ -310,9 +350,9 @@ def test_mha_cross_128_blocks(dev):
     do = rnd(B * Tq, H * dk, dev=dev, seed=7).to(torch.bfloat16)
     dq, dkk, dv = K.mha_bwd(q, k, v, o, do, lse, kv, B, Tq, Tk, H, 0.125)
     gq, gk, gv = torch.autograd.grad(ref, (qd, kd, vd), do.double())
-    close(dq, gq, atol=6e-2, rtol=6e-2, what="mha dq (128 blocks)")
-    close(dkk, gk, atol=6e-2, rtol=6e-2, what="mha dk (128 blocks)")
-    close(dv, gv, atol=6e-2, rtol=6e-2, what="mha dv (128 blocks)")
+    close_per_seq(dq, gq, B, atol=6e-2, rtol=6e-2, what="mha dq (128 blocks)")
+    close_per_seq(dkk, gk, B, atol=6e-2, rtol=6e-2, what="mha dk (128 blocks)")
+    close_per_seq(dv, gv, B, atol=6e-2, rtol=6e-2, what="mha dv (128 blocks)")
 
 
 def test_attention_lse(dev):

@@ -158,6 +158,7 @@ def test_torch_adam_also_drives_the_model(dev):
     opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-4)
     b = to_dev(make_batch(TRI, 2, 64, [64, 50], seed=4), dev)
     losses = []
+    n = m.trainable_numel()
     for _ in range(3):
         opt.zero_grad()
         out = m(b)
@@ -165,5 +166,52 @@ def test_torch_adam_also_drives_the_model(dev):
         loss.backward()
         opt.step()
         losses.append(loss.item())
+        # the next forward's bf16 GEMM operands are the updated weights (torch Adam writes through
+        # the Parameters, whose version counters are not the flat buffer's)
+        with torch.no_grad():
+            m.eval()
+            m(b)
+            m.train()
+        torch.cuda.synchronize()
+        assert torch.equal(m._lp[:n], m.flat_params()[:n].to(torch.bfloat16))
     assert all(np.isfinite(losses))
     assert all(p.grad is None for n, p in m.named_parameters() if n.startswith("reg_head."))
+
+
+def test_fused_adam_checkpoint_resume_bitwise(dev):
+    """main.py:519-526 saves {'model', 'optimizer'} and :216-222 resumes from it: FusedAdam's
+    state_dict carries the moments and the step, so a resumed run continues bit for bit."""
+    import io
+
+    b = to_dev(make_batch(TRI, 2, 96, [96, 64], seed=11), dev)
+
+    def step(model, opt, seed):
+        torch.manual_seed(seed)  # the dropout seeds of the step
+        opt.zero_grad()
+        out = model(b)
+        (model.losses(*out)["cls_loss"] / 2).backward()
+        opt.step()
+
+    torch.manual_seed(0)
+    m = MMCTransformer(**TRI, compute_dtype="bf16").to(dev).train()
+    opt = FusedAdam(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    for s in range(2):
+        step(m, opt, 100 + s)
+    buf = io.BytesIO()
+    torch.save({"model": m.state_dict(), "optimizer": opt.state_dict()}, buf)
+    for s in range(2, 4):
+        step(m, opt, 100 + s)
+    want = m.flat_params().clone()
+
+    torch.manual_seed(5)  # different init: everything must come from the checkpoint
+    m2 = MMCTransformer(**TRI, compute_dtype="bf16").to(dev).train()
+    opt2 = FusedAdam(m2.parameters(), lr=1e-3, weight_decay=1e-4)
+    buf.seek(0)
+    ck = torch.load(buf, map_location=dev, weights_only=True)
+    m2.load_state_dict(ck["model"])
+    opt2.load_state_dict(ck["optimizer"])
+    assert opt2._step == 2
+    for s in range(2, 4):
+        step(m2, opt2, 100 + s)
+    torch.cuda.synchronize()
+    assert torch.equal(m2.flat_params(), want)

@@ -34,8 +34,10 @@ def test_argument_errors_are_reported():
                1.0, None, None)
     with pytest.raises(RuntimeError, match="head dim"):
         N.call("rp_attn_fwd", 0, None, None, 1, 1, 1, 32, 1.0, 0.0, 0, None, None, None, None)
-    with pytest.raises(RuntimeError, match="cap must be"):
-        N.call("rp_softnms", None, None, None, 1, 2000, 0.5, 0.01, None, None, None, None, None)
+    fake = ctypes.c_void_p(16)
+    assert N.load().rp_softnms_workspace(2, 1000) == 0 and N.load().rp_softnms_workspace(2, 7000) == 2 * 5 * 7000 * 4
+    with pytest.raises(RuntimeError, match="needs rp_softnms_workspace"):
+        N.call("rp_softnms", fake, fake, fake, 1, 7000, 0.5, 0.01, fake, fake, fake, None, None, 0, None)
     with pytest.raises(RuntimeError, match="D=300 unsupported"):
         a = N.LnFwdArgs()
         a.x, a.gamma, a.beta, a.x_dtype = 16, 16, 16, 0
