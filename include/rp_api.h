@@ -190,6 +190,8 @@ enum { RP_ATTN_Q_PRESCALED = 0x100 };
  * qkv: [B*T, 3*H*dk] rows = (q heads | k heads | v heads), dk == 64.
  * key_valid: [B, T] uint8 (0 -> key masked with -inf, torch key_padding_mask semantics).
  * out: [B*T, H*dk];  lse: [B, H, T] fp32 (natural-log sum-exp of scaled scores).
+ * out_lo (bf16, optional): bf16(O - bf16(O)), the rounding residual of out, for the backward's
+ * delta = rowsum(dout * O) (pass the same pointer to the backward; NULL: delta from out alone).
  * Dropout on the attention probabilities with probability p: for query q and group g one stream
  * st = rp_hash(rp_hash(seed, b*H+h), q*4 + g) is advanced by xorshift32 (x ^= x<<13; x ^= x>>17;
  * x ^= x<<5) eight times per 64-key tile, tiles in order; in tile t word j (1..8th of the tile)
@@ -237,6 +239,11 @@ typedef struct rp_mha_args {
   void* dv;
   int64_t lddv;
   float* delta_ws;
+  void* out_lo;            /* bf16 only, optional: the forward also writes bf16(O - bf16(O)) here [B*Tq, ldo];
+                              the backward then forms delta = rowsum(dout * O) from the unrounded O */
+  int empty_rows_uniform;  /* a sequence with no valid key attends uniformly to ALL its keys (output =
+                              mean of V, dq = dk = 0): models/transformer.py's masked_fill(-1e9) semantics.
+                              0 = torch key_padding_mask semantics (-inf: such rows are NaN) */
 } rp_mha_args;
 
 int64_t rp_mha_dropmask_elems(int B, int Tq, int Tk, int H);
@@ -245,24 +252,24 @@ int rp_mha_fwd(int dtype, const rp_mha_args* args, void* stream);
  * dQ kernel, which then runs before dK/dV (7 = all: fused dQ + delta, then dK/dV). */
 int rp_mha_bwd(int dtype, const rp_mha_args* args, int phases, void* stream);
 int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk,
-                float scale, float dropout_p, uint32_t seed, void* out, float* lse, uint16_t* dropmask,
-                void* stream);
+                float scale, float dropout_p, uint32_t seed, void* out, void* out_lo, float* lse,
+                uint16_t* dropmask, void* stream);
 /* Backward; dqkv: [B*T, 3*H*dk] (fully overwritten); delta_ws: [B, H, T] fp32 workspace.
  * = rp_attn_bwd_dq_delta (dQ columns of dqkv, one workgroup per 128-query block, which also writes
  * delta = rowsum(dout * out) to delta_ws), then rp_attn_bwd_dkdv (dK, dV columns, one workgroup per
  * 128-key block, reading delta).  The phases are also exported separately (per-kernel timing);
  * rp_attn_bwd_delta + rp_attn_bwd_dq is the unfused equivalent of rp_attn_bwd_dq_delta. */
-int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
-                const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
-                const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream);
-int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, int B, int T, int H, int dk, float* delta_ws,
-                      void* stream);
+int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,
+                const float* lse, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
+                float dropout_p, const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream);
+int rp_attn_bwd_delta(int dtype, const void* out, const void* out_lo, const void* dout, int B, int T, int H, int dk,
+                      float* delta_ws, void* stream);
 int rp_attn_bwd_dkdv(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
                      const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                      const uint16_t* dropmask, void* dqkv, void* stream);
-int rp_attn_bwd_dq_delta(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
-                         float* delta_ws, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
-                         float dropout_p, const uint16_t* dropmask, void* dqkv, void* stream);
+int rp_attn_bwd_dq_delta(int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,
+                         const float* lse, float* delta_ws, const uint8_t* key_valid, int B, int T, int H, int dk,
+                         float scale, float dropout_p, const uint16_t* dropmask, void* dqkv, void* stream);
 int rp_attn_bwd_dq(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
                    const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                    const uint16_t* dropmask, void* dqkv, void* stream);

@@ -426,7 +426,11 @@ class _Schedule:
             # forward and both backward kernels: the backward recomputes the forward's exact scores)
             qkv = K.linear_fwd(h1, self.W(pre + "self_attn.in_proj_weight"), self.P(pre + "self_attn.in_proj_bias"),
                                col_scale_n=d, col_scale=scale * K.LOG2E)
-            o, lse, dmask = K.attn_fwd(qkv, kv, B, T, H, scale, p, self.seed(100 + 4 * l), q_prescaled=True)
+            # bf16 training: the output's rounding residual too, so the backward's rowsum(dO * O) is
+            # that of the unrounded output
+            olo = torch.empty(M, d, device=qkv.device, dtype=dt) if (save and dt != _F32) else None
+            o, lse, dmask = K.attn_fwd(qkv, kv, B, T, H, scale, p, self.seed(100 + 4 * l), q_prescaled=True,
+                                       out_lo=olo)
             x1 = K.linear_fwd(o, self.W(pre + "self_attn.out_proj.weight"), self.P(pre + "self_attn.out_proj.bias"),
                               out_dtype=_F32, dropout_p=p, seed=self.seed(101 + 4 * l), residual=x)
             _, h2, mu2, rs2 = K.layernorm_fwd(x1, self.P(pre + "norm2.weight"), self.P(pre + "norm2.bias"),
@@ -436,7 +440,7 @@ class _Schedule:
             x2 = K.linear_fwd(f, self.W(pre + "linear2.weight"), self.P(pre + "linear2.bias"), out_dtype=_F32,
                               dropout_p=p, seed=self.seed(103 + 4 * l), residual=x1)
             if save:
-                layers.append((x, h1, mu1, rs1, qkv, o, lse, dmask, x1, h2, mu2, rs2, f))
+                layers.append((x, h1, mu1, rs1, qkv, o, olo, lse, dmask, x1, h2, mu2, rs2, f))
             x = x2
         _, e, muE, rsE = K.layernorm_fwd(x, self.P("encoder_norm.weight"), self.P("encoder_norm.bias"),
                                          out_f32=False, lp_dtype=dt, save_stats=save)
@@ -538,7 +542,7 @@ class _Schedule:
         ready(["encoder_norm.", "feature_map.", "cls_head."])
         for l in reversed(range(L)):
             pre = f"multimodal_encoder.layers.{l}."
-            x, h1, mu1, rs1, qkv, o, lse, dmask, x1, h2, mu2, rs2, f = S["layers"][l]
+            x, h1, mu1, rs1, qkv, o, olo, lse, dmask, x1, h2, mu2, rs2, f = S["layers"][l]
             # linear2 (+dropout2 handled by g2's mask)
             wgrad(g2, f, pre + "linear2.weight", pre + "linear2.bias")
             dzf = K.linear_dgrad(g2, self.W(pre + "linear2.weight"), out_dtype=dt, gate=f, gate_scale=sd)
@@ -553,7 +557,8 @@ class _Schedule:
             wgrad(g1, o, pre + "self_attn.out_proj.weight", pre + "self_attn.out_proj.bias")
             do = K.linear_dgrad(g1, self.W(pre + "self_attn.out_proj.weight"), out_dtype=dt)
             # attention
-            dqkv = K.attn_bwd(qkv, o, do, lse, self.kv, B, T, H, self.scale, p, dropmask=dmask, q_prescaled=True)
+            dqkv = K.attn_bwd(qkv, o, do, lse, self.kv, B, T, H, self.scale, p, dropmask=dmask, q_prescaled=True,
+                              out_lo=olo)
             # in_proj
             wgrad(dqkv, h1, pre + "self_attn.in_proj_weight", pre + "self_attn.in_proj_bias")
             dh1 = K.linear_dgrad(dqkv, self.W(pre + "self_attn.in_proj_weight"), out_dtype=_F32)

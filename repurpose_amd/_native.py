@@ -49,7 +49,8 @@ class MhaArgs(ctypes.Structure):
                 ("key_valid", c_vp), ("B", c_i), ("Tq", c_i), ("Tk", c_i), ("H", c_i), ("head_dim", c_i),
                 ("scale", c_f), ("dropout_p", c_f), ("seed", c_u32), ("out", c_vp), ("ldo", c_i64), ("lse", c_vp),
                 ("dropmask", c_vp), ("dout", c_vp), ("lddo", c_i64), ("dq", c_vp), ("lddq", c_i64), ("dk", c_vp),
-                ("lddk", c_i64), ("dv", c_vp), ("lddv", c_i64), ("delta_ws", c_vp)]
+                ("lddk", c_i64), ("dv", c_vp), ("lddv", c_i64), ("delta_ws", c_vp), ("out_lo", c_vp),
+                ("empty_rows_uniform", c_i)]
 
 
 # name -> (restype, argtypes); mirrors include/rp_api.h one to one
@@ -68,13 +69,13 @@ _SIGNATURES = {
     "rp_colsum_workspace": (c_i64, [c_i64, c_i64]),
     "rp_colsum": (c_i, [c_vp, c_i, c_i64, c_i64, c_i64, c_vp, c_vp, c_i, c_vp, c_vp]),
     "rp_attn_dropmask_elems": (c_i64, [c_i, c_i, c_i]),
-    "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp, c_vp]),
-    "rp_attn_bwd": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp,
+    "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rp_attn_bwd": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp,
                           c_vp, c_vp, c_vp]),
-    "rp_attn_bwd_delta": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_vp, c_vp]),
+    "rp_attn_bwd_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_vp, c_vp]),
     "rp_attn_bwd_dkdv": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp]),
-    "rp_attn_bwd_dq_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp,
-                                   c_vp]),
+    "rp_attn_bwd_dq_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp,
+                                   c_vp, c_vp]),
     "rp_attn_bwd_dq": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp]),
     "rp_mha_dropmask_elems": (c_i64, [c_i, c_i, c_i, c_i]),
     "rp_mha_fwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_vp]),

@@ -79,13 +79,23 @@ struct MhaDev {
   float scale;
   uint32_t drop_thresh; float drop_scale; uint32_t seed;
   void* out; int64_t ldo;
+  void* out_lo;  // bf16: O - bf16(O) rounded to bf16 (same layout as out), or null
   float* lse;
   uint16_t* dmask;
   const void* dout; int64_t lddo;
   float* delta;
   void* dq; int64_t lddq; void* dk; int64_t lddk; void* dv; int64_t lddv;
   int qpre;  // RP_ATTN_Q_PRESCALED: q holds Q * scale * log2(e) (see include/rp_api.h)
+  int empty_uniform;  // a sequence with no valid key attends uniformly to all keys (masked_fill(-1e9))
 };
+
+// empty_uniform: does sequence b have no valid key at all?  (whole workgroup; uniform result)
+__device__ __forceinline__ bool seq_has_no_key(const MhaDev& a, int b, int tid) {
+  if (!a.empty_uniform) return false;
+  int any = 0;
+  for (int k = tid; k < a.Tk; k += NT) any |= a.kvalid[(int64_t)b * a.Tk + k];
+  return __syncthreads_or(any) == 0;
+}
 
 // ----- global [rows][64] (row stride ld elements) <-> LDS [rows][ROWB] staging ------------------
 template <typename T, int ROWS>
@@ -118,6 +128,14 @@ struct Stage {
       int id = tid + NT * i;
       int row = id / AttnCfg<T>::CPR, c = id % AttnCfg<T>::CPR;
       *reinterpret_cast<uint4*>(lds + lds_off<T>(row, c * 16)) = r[i];
+    }
+  }
+  __device__ __forceinline__ void store_zero(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int id = tid + NT * i;
+      int row = id / AttnCfg<T>::CPR, c = id % AttnCfg<T>::CPR;
+      *reinterpret_cast<uint4*>(lds + lds_off<T>(row, c * 16)) = make_uint4(0u, 0u, 0u, 0u);
     }
   }
   // bf16 only: store bf16(x * c) — the same rounding as the forward's prescale of Q
@@ -274,6 +292,9 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   const int KT = mask_kt(Tk);
   const int64_t ldm = mask_ld(Tq);
   uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
+  // no valid key + empty_uniform: every key counts and every score is 0 (Q taken as 0), so the
+  // output is the mean of V — softmax of a row masked_fill'ed to a constant
+  const bool novalid = seq_has_no_key(a, b, tid);
 
   // Q^T operand (B operand of S^T = K Q^T): lane holds Q[q0 + qt*16 + i][dk slots]
   constexpr bool BF = std::is_same<T, bf16>::value;
@@ -293,6 +314,17 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     }
   }
 
+  if (novalid) {
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      if constexpr (BF) {
+        qf[qt][0] = qf[qt][1] = bf16x8{};
+      } else {
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) qs[qt][s2] = 0.f;
+      }
+    }
+  }
   // Q enters S^T = K Q^T prescaled by c = scale*log2(e) (log2-domain scores; already done by the
   // producer when a.qpre), and the S^T accumulators start at -m, the running reference max:
   // P = exp2(acc) needs no per-score op unless the reference moves on this tile.
@@ -337,7 +369,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   // an additive bias + a "no masked key" flag at the LDS write
   auto load_valid = [&](int k0) -> bool {
     const int k = k0 + lane;
-    return w == 0 && k < Tk && kvalid[(int64_t)b * Tk + k];
+    return w == 0 && k < Tk && (novalid || kvalid[(int64_t)b * Tk + k]);
   };
   auto stage_mask = [&](char* buf, bool ok) {
     float* kb = reinterpret_cast<float*>(buf + 2 * TILE);
@@ -523,12 +555,18 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     const float inv = drop_scale / l;
     T* orow = out + ((int64_t)b * Tq + q) * ldo + h * HD;
     if constexpr (BF) {  // the lane's 4 consecutive dims of a 16-dim tile -> one 8-byte store
+      bf16* lorow = a.out_lo ? (bf16*)a.out_lo + ((int64_t)b * Tq + q) * ldo + h * HD : nullptr;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        bf16x4 v;
+        bf16x4 v, vl;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[qt][dt][r] * inv);
+        for (int r = 0; r < 4; ++r) {
+          const float x = o[qt][dt][r] * inv;
+          v[r] = (bf16)x;
+          vl[r] = (bf16)(x - (float)v[r]);  // the rounding residual: rowsum(dO * O) to ~2^-17
+        }
         *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = v;
+        if (lorow) *reinterpret_cast<bf16x4*>(lorow + dt * 16 + 4 * g) = vl;
       }
     } else {
 #pragma unroll
@@ -551,11 +589,12 @@ __global__ void attn_delta_kernel(MhaDev a) {
   if (row >= (int64_t)a.B * a.Tq) return;
   const int D = a.H * HD;
   const T* o = (const T*)a.out + row * a.ldo;
+  const T* ol = a.out_lo ? (const T*)a.out_lo + row * a.ldo : nullptr;
   const T* d = (const T*)a.dout + row * a.lddo;
   for (int e = lane * 8; e < D; e += 512) {
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += rp_ld(o + e + j) * rp_ld(d + e + j);
+    for (int j = 0; j < 8; ++j) s += (rp_ld(o + e + j) + (ol ? rp_ld(ol + e + j) : 0.f)) * rp_ld(d + e + j);
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
@@ -603,6 +642,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   const int kw0 = kb * KB + w * 16 * KTW;
   const float c = scale * LOG2E;
   const float kc = a.qpre ? 1.f : c;  // fp32 path: K prescale
+  // no valid key + empty_uniform: uniform P (Q staged as 0), dK = dS^T 0 = 0, dV = mean of dO
+  const bool novalid = seq_has_no_key(a, b, tid);
   const bool scale_q = BF && !a.qpre;  // bf16 path: Q prescale at LDS staging
   const float dk_scale = (BF || a.qpre) ? 1.f / LOG2E : scale;  // dS^T Q' -> dK
   const float inv_ds = DROP ? 1.f / drop_scale : 1.f;
@@ -678,6 +719,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
   };
   const int nqt = (Tq + KV_QT - 1) / KV_QT;
   auto store_q = [&](char* buf) {
+    if (novalid) {
+      sq.store_zero(buf, tid);
+      return;
+    }
     if constexpr (BF) {
       if (scale_q) {
         sq.store_scaled(buf, tid, c);
@@ -841,7 +886,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
     for (int r = 0; r < 4; ++r) {
       const int key = kw0 + kt * 16 + 4 * g + r;
       if (key >= Tk) continue;
-      const bool ok = kvalid[(int64_t)b * Tk + key] != 0;
+      const bool ok = novalid || kvalid[(int64_t)b * Tk + key] != 0;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         rp_st(dK + (int64_t)key * a.lddk + dt * 16 + i, ok ? dk[kt][dt][r] * dk_scale : 0.f);
@@ -905,8 +950,15 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
         if constexpr (DELTA) {
           const bf16x8 of = row_frag_gmem((const bf16*)a.out + (int64_t)b * Tq * a.ldo + h * HD, a.ldo,
                                           q0 + qt * 16, Tq, s * 32, lane);
+          if (a.out_lo) {  // O = hi + lo: delta from the unrounded output (exact rowsum(dO * O))
+            const bf16x8 ol = row_frag_gmem((const bf16*)a.out_lo + (int64_t)b * Tq * a.ldo + h * HD, a.ldo,
+                                            q0 + qt * 16, Tq, s * 32, lane);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) part += (float)df[qt][s][j] * (float)of[j];
+            for (int j = 0; j < 8; ++j) part += (float)df[qt][s][j] * ((float)of[j] + (float)ol[j]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) part += (float)df[qt][s][j] * (float)of[j];
+          }
         }
       }
     } else {
@@ -923,6 +975,21 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
       if (g == 0 && q < Tq) a.delta[(int64_t)bh * Tq + q] = dl;
       dq[qt] = q < Tq ? -dl * (DROP ? 1.f / drop_scale : 1.f) : 0.f;
     }
+  }
+  // no valid key + empty_uniform: the scores were constants (masked_fill), so dQ = 0 (delta above
+  // is still written: the dK/dV kernel reads it)
+  if (seq_has_no_key(a, b, tid)) {
+    T* dQz = (T*)a.dq + (int64_t)b * Tq * a.lddq + h * HD;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = q0 + qt * 16 + 4 * g + r;
+        if (q >= Tq) continue;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) rp_st(dQz + (int64_t)q * a.lddq + dt * 16 + i, 0.f);
+      }
+    return;
   }
 
   // Q enters S^T = K Q^T prescaled by c = scale*log2(e) (Q feeds no other product here), so with
@@ -1242,6 +1309,9 @@ int make_dev(const char* fn, int dtype, int qpre, const rp_mha_args* p, int phas
   a.kvalid = p->key_valid; a.B = p->B; a.Tq = p->Tq; a.Tk = p->Tk; a.H = p->H; a.scale = p->scale;
   a.drop_thresh = thr; a.drop_scale = p->dropout_p > 0.f ? 1.f / (1.f - p->dropout_p) : 1.f; a.seed = p->seed;
   a.out = p->out; a.ldo = p->ldo; a.lse = p->lse; a.dmask = thr ? p->dropmask : nullptr;
+  a.out_lo = dtype == RP_BF16 ? p->out_lo : nullptr;
+  a.empty_uniform = p->empty_rows_uniform != 0;
+  RP_REQUIRE(!a.out_lo || rp_aligned16(a.out_lo), "%s: out_lo must be 16-byte aligned", fn);
   a.dout = p->dout; a.lddo = p->lddo; a.delta = p->delta_ws;
   a.dq = p->dq; a.lddq = p->lddq; a.dk = p->dk; a.lddk = p->lddk; a.dv = p->dv; a.lddv = p->lddv;
   a.qpre = qpre;
@@ -1288,12 +1358,14 @@ int mha_bwd_entry(int flagged, const rp_mha_args* p, int phases, void* stream) {
 
 // packed self-attention (qkv [B*T, 3*H*dk]) -> general description
 rp_mha_args packed(const void* qkv, const uint8_t* kv, int B, int T, int H, int dk, float scale, float p, uint32_t seed,
-                   const void* out, float* lse, const uint16_t* dmask, const void* dout, void* dqkv, float* delta) {
+                   const void* out, const void* out_lo, float* lse, const uint16_t* dmask, const void* dout, void* dqkv,
+                   float* delta) {
   rp_mha_args a{};
   const int64_t ld = 3LL * H * dk, lo = (int64_t)H * dk;
   a.q = qkv; a.k = qkv; a.v = qkv; a.ldq = a.ldk = a.ldv = ld;
   a.key_valid = kv; a.B = B; a.Tq = T; a.Tk = T; a.H = H; a.head_dim = dk; a.scale = scale; a.dropout_p = p; a.seed = seed;
   a.out = const_cast<void*>(out); a.ldo = lo; a.lse = lse; a.dropmask = const_cast<uint16_t*>(dmask);
+  a.out_lo = const_cast<void*>(out_lo);
   a.dout = dout; a.lddo = lo; a.delta_ws = delta;
   a.dq = dqkv; a.dk = dqkv; a.dv = dqkv; a.lddq = a.lddk = a.lddv = ld;
   return a;
@@ -1326,35 +1398,36 @@ extern "C" int rp_mha_bwd(int dtype, const rp_mha_args* args, int phases, void* 
 }
 
 extern "C" int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
-                           float dropout_p, uint32_t seed, void* out, float* lse, uint16_t* dropmask, void* stream) {
+                           float dropout_p, uint32_t seed, void* out, void* out_lo, float* lse, uint16_t* dropmask,
+                           void* stream) {
   RP_REQUIRE(dk == HD, "rp_attn_fwd: head dim %d unsupported (64)", dk);
   RP_REQUIRE(qkv, "rp_attn_fwd: null qkv");
-  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, seed, out, lse, dropmask, nullptr, nullptr,
-                         nullptr);
+  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, seed, out, out_lo, lse, dropmask, nullptr,
+                         nullptr, nullptr);
   packed_offsets(a, attn_dtype(dtype));
   return mha_fwd_entry(dtype, &a, stream);
 }
 
-static int attn_bwd_packed(int phases, int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
-                           const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
-                           const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
+static int attn_bwd_packed(int phases, int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,
+                           const float* lse, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
+                           float dropout_p, const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
   RP_REQUIRE(dk == HD, "rp_attn_bwd: head dim %d unsupported (64)", dk);
   RP_REQUIRE(qkv && dqkv, "rp_attn_bwd: null qkv / dqkv");
-  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, 0, out, const_cast<float*>(lse), dropmask, dout,
-                         dqkv, delta_ws);
+  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, 0, out, out_lo, const_cast<float*>(lse),
+                         dropmask, dout, dqkv, delta_ws);
   packed_offsets(a, attn_dtype(dtype));
   return mha_bwd_entry(dtype, &a, phases, stream);
 }
 
-extern "C" int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
-                           const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
-                           const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
-  return attn_bwd_packed(7, dtype, qkv, out, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
-                         delta_ws, stream);
+extern "C" int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,
+                           const float* lse, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
+                           float dropout_p, const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
+  return attn_bwd_packed(7, dtype, qkv, out, out_lo, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask,
+                         dqkv, delta_ws, stream);
 }
 
-extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, int B, int T, int H, int dk,
-                                 float* delta_ws, void* stream) {
+extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* out_lo, const void* dout, int B, int T, int H,
+                                 int dk, float* delta_ws, void* stream) {
   RP_REQUIRE(dk == HD, "rp_attn_bwd_delta: head dim %d unsupported (64)", dk);
   RP_REQUIRE(B >= 0 && T >= 0 && H > 0, "rp_attn_bwd_delta: bad shape");
   if (B == 0 || T == 0) return RP_OK;
@@ -1363,6 +1436,7 @@ extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, i
   RP_REQUIRE(dtype == RP_BF16 || dtype == RP_F32, "rp_attn_bwd_delta: bad dtype");
   MhaDev a{};
   a.B = B; a.Tq = T; a.Tk = T; a.H = H; a.out = const_cast<void*>(out); a.ldo = (int64_t)H * HD; a.dout = dout;
+  a.out_lo = dtype == RP_BF16 ? const_cast<void*>(out_lo) : nullptr;
   a.lddo = (int64_t)H * HD; a.delta = delta_ws;
   return launch_mha_bwd_dtype(dtype, 1, a, (hipStream_t)stream);
 }
@@ -1370,21 +1444,21 @@ extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* dout, i
 extern "C" int rp_attn_bwd_dkdv(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
                                 const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                                 const uint16_t* dropmask, void* dqkv, void* stream) {
-  return attn_bwd_packed(2, dtype, qkv, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
-                         const_cast<float*>(delta_ws), stream);
+  return attn_bwd_packed(2, dtype, qkv, nullptr, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask,
+                         dqkv, const_cast<float*>(delta_ws), stream);
 }
 
-extern "C" int rp_attn_bwd_dq_delta(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
-                                    float* delta_ws, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
-                                    float dropout_p, const uint16_t* dropmask, void* dqkv, void* stream) {
+extern "C" int rp_attn_bwd_dq_delta(int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,
+                                    const float* lse, float* delta_ws, const uint8_t* key_valid, int B, int T, int H, int dk,
+                                    float scale, float dropout_p, const uint16_t* dropmask, void* dqkv, void* stream) {
   RP_REQUIRE(out, "rp_attn_bwd_dq_delta: null out");
-  return attn_bwd_packed(5, dtype, qkv, out, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
-                         delta_ws, stream);
+  return attn_bwd_packed(5, dtype, qkv, out, out_lo, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask,
+                         dqkv, delta_ws, stream);
 }
 
 extern "C" int rp_attn_bwd_dq(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
                               const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                               const uint16_t* dropmask, void* dqkv, void* stream) {
-  return attn_bwd_packed(4, dtype, qkv, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask, dqkv,
-                         const_cast<float*>(delta_ws), stream);
+  return attn_bwd_packed(4, dtype, qkv, nullptr, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask,
+                         dqkv, const_cast<float*>(delta_ws), stream);
 }

@@ -226,10 +226,11 @@ def colsum(X, w=None, out=None, accumulate=False, ws=None):
 
 
 # ------------------------------------------------------------------------------------- attention
-def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, q_prescaled=False):
+def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, q_prescaled=False, out_lo=None):
     """-> (out [B*T, H*dk], lse [B, H, T], dropmask or None).  The dropout keep bits drawn by the
     forward are returned and must be handed to attn_bwd.  q_prescaled: the Q columns of qkv hold
-    Q * scale * log2(e) (linear_fwd's col_scale); the same flag must go to attn_bwd."""
+    Q * scale * log2(e) (linear_fwd's col_scale); the same flag must go to attn_bwd.  out_lo (bf16,
+    optional, out's shape): filled with the output's rounding residual; hand it to attn_bwd too."""
     _gpu(qkv, key_valid)
     _contig(qkv, key_valid)
     dk = qkv.shape[1] // (3 * H)
@@ -239,8 +240,12 @@ def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, q_prescaled=
     if dropout_p > 0:
         mask = torch.empty(N.load().rp_attn_dropmask_elems(B, T, H), device=qkv.device, dtype=torch.int16)
     e0 = _tick("attn_fwd")
+    if out_lo is not None:
+        _gpu(out_lo)
+        if out_lo.shape != out.shape or out_lo.dtype != out.dtype or not out_lo.is_contiguous():
+            raise ValueError("attn_fwd: out_lo must be a contiguous tensor like out")
     N.call("rp_attn_fwd", _adt(qkv, q_prescaled), _p(qkv), _p(key_valid), B, T, H, dk, float(scale), float(dropout_p),
-           int(seed) & 0xFFFFFFFF, _p(out), _p(lse), _p(mask), _stream(qkv))
+           int(seed) & 0xFFFFFFFF, _p(out), _p(out_lo), _p(lse), _p(mask), _stream(qkv))
     _tock(e0)
     return out, lse, mask
 
@@ -249,7 +254,7 @@ _FUSED_DELTA = os.environ.get("RP_ATTN_FUSED_DELTA", "1") != "0"
 
 
 def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, dropmask=None,
-             q_prescaled=False):
+             q_prescaled=False, out_lo=None):
     _gpu(qkv, out, dout, lse, key_valid, dropmask)
     _contig(qkv, out, dout, lse, key_valid)
     if dropout_p > 0 and dropmask is None:
@@ -261,11 +266,11 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
     e0 = _tick("attn_bwd")
     if _FUSED_DELTA:  # dQ first, with the delta = rowsum(dO * O) pre-pass fused in; dK/dV reads it
         e2 = _tick("attn_bwd_dq")
-        N.call("rp_attn_bwd_dq_delta", dt, _p(qkv), _p(out), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T,
+        N.call("rp_attn_bwd_dq_delta", dt, _p(qkv), _p(out), _p(out_lo), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T,
                H, dk, float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
         _tock(e2)
     else:
-        N.call("rp_attn_bwd_delta", dt, _p(out), _p(dout), B, T, H, dk, _p(delta), st)
+        N.call("rp_attn_bwd_delta", dt, _p(out), _p(out_lo), _p(dout), B, T, H, dk, _p(delta), st)
     e1 = _tick("attn_bwd_dkdv")
     N.call("rp_attn_bwd_dkdv", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
            float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
@@ -286,7 +291,8 @@ def _rows(t, H, dk):
     return t.data_ptr(), t.stride(0)
 
 
-def mha_fwd(q, k, v, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, seed=0, q_prescaled=False):
+def mha_fwd(q, k, v, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, seed=0, q_prescaled=False,
+            empty_uniform=False):
     """General (self / cross) attention core.  q [B*Tq, >=H*dk], k/v [B*Tk, >=H*dk] row views (any row
     stride), key_valid [B, Tk] uint8.  -> (out [B*Tq, H*dk], lse [B, H, Tq], dropmask or None)."""
     _gpu(q, k, v, key_valid)
@@ -309,12 +315,13 @@ def mha_fwd(q, k, v, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, seed=0, q_pr
     a.out, a.ldo = out.data_ptr(), out.stride(0)
     a.lse = lse.data_ptr()
     a.dropmask = mask.data_ptr() if mask is not None else None
+    a.empty_rows_uniform = int(empty_uniform)
     N.call("rp_mha_fwd", _adt(q, q_prescaled), ctypes.byref(a), _stream(q))
     return out, lse, mask
 
 
 def mha_bwd(q, k, v, out, dout, lse, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, dropmask=None,
-            q_prescaled=False):
+            q_prescaled=False, empty_uniform=False):
     """-> (dq [B*Tq, H*dk], dk [B*Tk, H*dk], dv [B*Tk, H*dk]) for mha_fwd's inputs."""
     _gpu(q, k, v, out, dout, lse, key_valid, dropmask)
     _contig(out, dout, lse, key_valid)
@@ -340,6 +347,7 @@ def mha_bwd(q, k, v, out, dout, lse, key_valid, B, Tq, Tk, H, scale, dropout_p=0
     a.dk, a.lddk = dkk.data_ptr(), dkk.stride(0)
     a.dv, a.lddv = dv.data_ptr(), dv.stride(0)
     a.delta_ws = delta.data_ptr()
+    a.empty_rows_uniform = int(empty_uniform)
     N.call("rp_mha_bwd", _adt(q, q_prescaled), ctypes.byref(a), 7, _stream(q))
     return dq, dkk, dv
 

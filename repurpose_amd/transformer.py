@@ -18,16 +18,21 @@ fused in the epilogue), every LayerNorm rp_layernorm_fwd/bwd, the attention core
 (independent q/k/v row strides, Tq != Tk for cross attention; q/k/v of one input come from ONE
 GEMM into a [rows, 3d] buffer).  Arithmetic is fp32 (exact-f32 MFMA), like the reference.
 
-Masks: ``mask`` is [B, 1, Tk] or [B, Tk] (per-key padding, the form the reference passes); a key is
-excluded iff mask == 0.  The reference's masked_fill(-1e9) and the kernels' -inf bias give identical
-results unless a sequence has no valid key at all (the reference then averages all values, the
-kernels produce NaN); per-query masks [B, Tq, Tk] raise NotImplementedError.
+Masks: ``mask`` is [B, 1, Tk] (per-key padding, the form the reference passes), [B, Tk] (the same),
+or [B, Tq, Tk] whose rows are equal for every query (checked); a key is excluded iff mask == 0, like
+the reference's ``masked_fill(mask == 0, -1e9)`` (:69-71).  A sequence with no valid key at all gets
+the reference's result too: every score is the same constant, so each query averages ALL values
+(including the padded ones) and no gradient reaches q or k (rp_mha empty_rows_uniform).  Masks that
+differ between queries raise NotImplementedError.  Head dims d_k = d_model / num_heads up to 64 run
+on the d_k = 64 kernels with each head zero-padded to 64 (zero columns add nothing to QK^T; the
+scale stays 1/sqrt(d_k)); larger head dims raise NotImplementedError.
 Residual-branch dropout (p > 0, training) is torch's nn.Dropout on the branch, as in the reference.
 """
 import math
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import kernels as K
 
@@ -85,11 +90,12 @@ class _LayerNormFn(torch.autograd.Function):
 
 
 class _AttentionCoreFn(torch.autograd.Function):
-    """softmax(scale * Q K^T + key mask) V on [rows, H*64] row views of q, k, v."""
+    """softmax(scale * Q K^T + key mask) V on [rows, H*64] row views of q, k, v; a sequence without
+    any valid key averages all values (masked_fill(-1e9) semantics)."""
 
     @staticmethod
     def forward(ctx, q, k, v, kv, B, Tq, Tk, H, scale):
-        out, lse, _ = K.mha_fwd(q, k, v, kv, B, Tq, Tk, H, scale)
+        out, lse, _ = K.mha_fwd(q, k, v, kv, B, Tq, Tk, H, scale, empty_uniform=True)
         ctx.save_for_backward(q, k, v, out, lse, kv)
         ctx.dims = (B, Tq, Tk, H, scale)
         return out
@@ -98,7 +104,7 @@ class _AttentionCoreFn(torch.autograd.Function):
     def backward(ctx, dout):
         q, k, v, out, lse, kv = ctx.saved_tensors
         B, Tq, Tk, H, scale = ctx.dims
-        dq, dk, dv = K.mha_bwd(q, k, v, out, dout.contiguous(), lse, kv, B, Tq, Tk, H, scale)
+        dq, dk, dv = K.mha_bwd(q, k, v, out, dout.contiguous(), lse, kv, B, Tq, Tk, H, scale, empty_uniform=True)
         return dq, dk, dv, None, None, None, None, None, None
 
 
@@ -110,14 +116,17 @@ def _layernorm(ln, x):
     return _LayerNormFn.apply(x, ln.weight, ln.bias, float(ln.eps))
 
 
-def _key_valid(mask, B, Tk, device):
+def _key_valid(mask, B, Tq, Tk, device):
     if mask is None:
         return torch.ones(B, Tk, device=device, dtype=torch.uint8)
     m = mask
     if m.dim() == 3:
         if m.shape[1] != 1:
-            raise NotImplementedError("MultiHeadAttention: per-query masks [B, Tq, Tk] are not supported "
-                                      "(the reference passes key-padding masks [B, 1, Tk])")
+            if tuple(m.shape) != (B, Tq, Tk):
+                raise ValueError(f"MultiHeadAttention: mask shape {tuple(mask.shape)} does not match ({B}, {Tq}, {Tk})")
+            if not bool(((m != 0) == (m[:, :1] != 0)).all()):
+                raise NotImplementedError("MultiHeadAttention: masks that differ between queries are not supported "
+                                          "(key-padding masks [B, 1, Tk], or [B, Tq, Tk] with equal rows)")
         m = m[:, 0]
     if tuple(m.shape) != (B, Tk):
         raise ValueError(f"MultiHeadAttention: mask shape {tuple(mask.shape)} does not match keys ({B}, {Tk})")
@@ -185,8 +194,9 @@ class MultiHeadAttention(nn.Module):
         self.num_heads = num_heads
         self.d_model = d_model
         self.d_k = d_model // num_heads
-        if self.d_k != 64:
-            raise NotImplementedError(f"MultiHeadAttention: head dim {self.d_k} (the HIP kernels implement 64)")
+        if self.d_k > 64 or self.d_k * num_heads != d_model:
+            raise NotImplementedError(f"MultiHeadAttention: d_model {d_model} / {num_heads} heads (head dims up to 64 "
+                                      "dividing d_model; the HIP kernels implement 64, smaller heads are zero-padded)")
         self.q_linear = nn.Linear(d_model, d_model)
         self.k_linear = nn.Linear(d_model, d_model)
         self.v_linear = nn.Linear(d_model, d_model)
@@ -214,9 +224,15 @@ class MultiHeadAttention(nn.Module):
             (qp,) = self._project(q, [self.q_linear])
             (kp,) = self._project(k, [self.k_linear])
             (vp,) = self._project(v, [self.v_linear])
-        kv = _key_valid(mask, B, Tk, q.device)
-        att = _AttentionCoreFn.apply(qp, kp, vp, kv, B, Tq, Tk, self.num_heads, self._inv_scale)
-        return _linear(self.out, att.view(B, Tq, self.d_model), residual=residual)
+        kv = _key_valid(mask, B, Tq, Tk, q.device)
+        H, dk = self.num_heads, self.d_k
+        if dk < 64:  # zero-pad every head to the kernels' 64 columns
+            qp, kp, vp = (F.pad(t.reshape(t.shape[0], H, dk), (0, 64 - dk)).reshape(t.shape[0], H * 64)
+                          for t in (qp, kp, vp))
+        att = _AttentionCoreFn.apply(qp, kp, vp, kv, B, Tq, Tk, H, self._inv_scale)
+        if dk < 64:
+            att = att.view(-1, H, 64)[:, :, :dk].reshape(-1, H * dk)
+        return _linear(self.out, att.reshape(B, Tq, self.d_model), residual=residual)
 
 
 def _attend_residual(attn, x, q, k, v, mask, drop):

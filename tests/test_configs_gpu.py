@@ -134,12 +134,13 @@ def test_config4_bf16_attention_T4096_dropout(dev):
     kv = torch.ones(B, T, dtype=torch.uint8, device=dev)
     kv[:, 3900:] = 0
     qkv, eff = prescale_q(qkv, H, 0.125)
-    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=True)
+    olo = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=True, out_lo=olo)
     ref_in = eff.requires_grad_(True)
     ref = attn_ref64(ref_in, kv, B, T, H, p, seed, dev)
     close(o, ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd T=4096")
     do = rnd(B * T, H * 64, dev=dev, seed=4).to(torch.bfloat16)
-    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True)
+    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True, out_lo=olo)
     gref = torch.autograd.grad(ref, ref_in, do.double())[0]
     for part, name in enumerate("qkv"):
         cols = slice(part * H * 64, (part + 1) * H * 64)

@@ -302,7 +302,9 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
     dropout keep bits vs the restatement, fwd and bwd vs fp64.  A sequence with one valid key puts
     every query's whole mass on it, so its dV sums ~1000 recomputed probabilities: this pins that the
     backward recomputes exactly the forward's P (same bf16-rounded Q * scale * log2 e in all three
-    kernels, with the prescale done by the kernels or by the producer)."""
+    kernels, with the prescale done by the kernels or by the producer), and that delta = rowsum(dO * O)
+    is taken from the unrounded output (out_lo), without which that key's dK (exactly 0) would collect
+    ~1000 rounding residuals of O."""
     B, H, T, p = 8, 8, 1030, 0.1
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(torch.bfloat16)
     lens = torch.tensor([T, T - 1, 1000, 777, 640, 129, 2, 1], device=dev)
@@ -312,17 +314,20 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
         qkv, eff = prescale_q(qkv, H, 0.125)
     else:
         eff = qkv.double()
-    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=q_prescaled)
+    olo = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=q_prescaled, out_lo=olo)
     ref_in = eff.requires_grad_(True)
     ref = attn_ref(ref_in, kv, B, T, H, p, seed)
     close(o, ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd (128 blocks)")
+    # hi + lo carries the output to ~2^-17
+    close(o.double() + olo.double(), ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd hi+lo")
     KT, ldm = (T + 63) // 64, (T + 63) // 64 * 64
     words = mask.view(B * H, KT, 4, ldm)[..., :T].to(torch.int64) & 0xFFFF
     bits = ((words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1).view(B * H, KT, 4, T, 4, 4)
     got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, T, KT * 64)[:, :, :T].bool()
     assert torch.equal(got, attn_keep(B, H, T, p, seed, dev).view(B * H, T, T))
     do = rnd(B * T, H * 64, dev=dev, seed=T + 1).to(torch.bfloat16)
-    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=q_prescaled)
+    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=q_prescaled, out_lo=olo)
     gref = torch.autograd.grad(ref, ref_in, do.double())[0]
     for part, name in enumerate("qkv"):
         cols = slice(part * H * 64, (part + 1) * H * 64)
@@ -332,6 +337,7 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
     rows = slice(7 * T, 7 * T + 1)
     dv1, rv1 = dqkv[rows, 2 * H * 64:].double().cpu(), gref[rows, 2 * H * 64:].cpu()
     assert ((dv1 - rv1).abs().max() / rv1.abs().max()).item() < 1e-2
+    assert dqkv[rows, H * 64:2 * H * 64].abs().max().item() < 1e-2
 
 
 @pytest.mark.gpu
@@ -479,11 +485,11 @@ def test_attention_bwd_fused_delta_matches_unfused(dev, dtype, p):
         delta = torch.full((B, H, T), float("nan"), device=dev)
         args = (P(qkv), P(do), P(lse), P(delta), P(kv), B, T, H, 64, 0.125, p, P(mask), P(dqkv), st)
         if fused:
-            N.call("rp_attn_bwd_dq_delta", dt, P(qkv), P(o), P(do), P(lse), P(delta), P(kv), B, T, H, 64, 0.125, p,
+            N.call("rp_attn_bwd_dq_delta", dt, P(qkv), P(o), P(None), P(do), P(lse), P(delta), P(kv), B, T, H, 64, 0.125, p,
                    P(mask), P(dqkv), st)
             N.call("rp_attn_bwd_dkdv", dt, *args)
         else:
-            N.call("rp_attn_bwd_delta", dt, P(o), P(do), B, T, H, 64, P(delta), st)
+            N.call("rp_attn_bwd_delta", dt, P(o), P(None), P(do), B, T, H, 64, P(delta), st)
             N.call("rp_attn_bwd_dkdv", dt, *args)
             N.call("rp_attn_bwd_dq", dt, *args)
         outs.append((dqkv, delta))

@@ -97,9 +97,60 @@ def test_forward_backward_parity(dev, name):
         assert rel < 2e-3, f"{name} grad {n}: rel err {rel:.3e}"
 
 
+def _mha_case(dev, d_model, heads, cmask_lens, seed=0, mask_fn=None):
+    """MultiHeadAttention fwd + every gradient vs the oracle (masked_fill(-1e9) reference semantics)."""
+    torch.manual_seed(seed)
+    ref = O.MultiHeadAttention(d_model, heads)
+    torch.manual_seed(seed)
+    ours = R.MultiHeadAttention(d_model, heads).to(dev)
+    g = torch.Generator().manual_seed(3)
+    B, T, Tc = len(cmask_lens), 40, 33
+    x = torch.randn(B, T, d_model, generator=g)
+    c = torch.randn(B, Tc, d_model, generator=g)
+    mask = (torch.arange(Tc)[None] < torch.tensor(cmask_lens)[:, None]).unsqueeze(1)  # [B, 1, Tc]
+    if mask_fn is not None:
+        mask = mask_fn(mask, T)
+    xr, cr = x.clone().requires_grad_(True), c.clone().requires_grad_(True)
+    yr = ref(xr, cr, cr, mask)
+    xo, co = x.to(dev).requires_grad_(True), c.to(dev).requires_grad_(True)
+    yo = ours(xo, co, co, mask.to(dev))
+    err = (yo.detach().cpu() - yr.detach()).abs().max().item()
+    assert err < 1e-3 * max(1.0, yr.abs().max().item()), f"forward max|err| {err:.3e}"
+    w = torch.randn(yr.shape, generator=torch.Generator().manual_seed(9))
+    (yr * w).sum().backward()
+    (yo * w.to(dev)).sum().backward()
+    pairs = [("x", xr.grad, xo.grad), ("context", cr.grad, co.grad)]
+    pairs += [(n, p.grad, q.grad) for (n, p), q in zip(ref.named_parameters(), ours.parameters())]
+    gmax = max(a.abs().max().item() for _, a, _ in pairs)
+    for n, a, b in pairs:
+        rel = (b.cpu() - a).abs().max().item() / max(a.abs().max().item(), 1e-2 * gmax)
+        assert rel < 2e-3, f"grad {n}: rel err {rel:.3e}"
+
+
 @pytest.mark.gpu
-def test_per_query_mask_rejected(dev):
+def test_sequence_without_valid_keys_averages_all_values(dev):
+    """models/transformer.py:69-73: a context with no valid key gets masked_fill(-1e9) on every score,
+    so softmax is uniform over ALL keys (padded ones included) and q / k get no gradient."""
+    _mha_case(dev, D, H, [33, 0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d_model,heads", [(128, 4), (96, 6), (64, 1)])
+def test_head_dims_below_64(dev, d_model, heads):
+    """d_k = d_model / num_heads of 32, 16 and 64 (the reference takes any, :42)."""
+    _mha_case(dev, d_model, heads, [33, 20])
+
+
+@pytest.mark.gpu
+def test_per_query_masks(dev):
+    """[B, Tq, Tk] masks whose rows agree for every query run (the reference broadcasts any mask,
+    :69-71); masks that differ between queries are refused loudly."""
+    _mha_case(dev, D, H, [33, 20], mask_fn=lambda m, T: m.expand(m.shape[0], T, m.shape[2]).contiguous())
     m = R.MultiHeadAttention(D, H).to(dev)
     x = torch.randn(2, 8, D, device=dev)
+    bad = torch.ones(2, 8, 8, device=dev)
+    bad[0, 3, 5] = 0
     with pytest.raises(NotImplementedError):
-        m(x, x, x, torch.ones(2, 8, 8, device=dev))
+        m(x, x, x, bad)
+    with pytest.raises(NotImplementedError):
+        R.MultiHeadAttention(256, 2)  # head dim 128
