@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 MODEL_CFG = dict(vis_dim=512, aud_dim=2048, text_dim=384, d_model=512, self_num_layers=16, text_num_layers=3,
                  cross_num_layers=3, num_heads=8)
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP32_TFLOPS = 157.3   # exact-f32 MFMA (the fp32 parity mode)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -77,11 +78,34 @@ def synth_batch(B, T, dev, seed):
     return {k: x.to(dev) for k, x in batch.items()}
 
 
+def host_threads():
+    """Threads for the CPU baseline: every CPU this process may run on (os.cpu_count()),
+    capped by a cgroup CPU quota when the host enforces one (a GPU box's CPU share: threads beyond the
+    quota only contend).  Returns (threads, note)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        pass
+    note = f"os.cpu_count()={os.cpu_count()}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+            if quota < n:
+                note += f", cgroup cpu.max quota {quota}"
+                n = quota
+    except (OSError, ValueError):
+        pass
+    return n, note
+
+
 def cpu_baseline(T, budget_s=25.0):
     """Oracle (reference arithmetic on stock torch CPU modules, fp32) fwd+bwd at the metric shape,
     B = 1, train mode; bounded sample."""
     from oracle.mmct_oracle import MMCTransformer as Oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, note = host_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(1234)
     m = Oracle(**MODEL_CFG).train()
@@ -110,7 +134,8 @@ def cpu_baseline(T, budget_s=25.0):
         model = "unknown"
     return {"value": T / med, "unit": "feature-timesteps/sec", "cores": threads, "kind": "port",
             "sample": f"oracle fp32 train step (fwd+focal+bwd+Adam), L=16 tri-modal, B=1, T={T}; "
-                      f"{len(timed)} timed of {steps} steps, median {med:.2f}s; cpu '{model}'"}
+                      f"{len(timed)} timed of {steps} steps, median {med:.2f}s; cpu '{model}'; {threads} threads "
+                      f"({note})"}
 
 
 def main():
@@ -166,7 +191,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    K.timer_start(*KERNEL_FLOPS)
+    K.timer_start(*KERNEL_FLOPS, "gemm_wgrad")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -177,7 +202,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = K.timer_stop()
+    kern = K.timer_stop(detail=True)
+    kern_ms = {n: v[0] for n, v in kern.items()}
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -186,13 +212,14 @@ def main():
     if rank == 0:
         fpt = flops_per_timestep(T)
         H, dk = 8, 64
+        peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_FP32_TFLOPS
 
         def roofline(name):
             ms = kern_ms.get(name)
             kflops = KERNEL_FLOPS[name] * B * H * T * T * dk
             ach = kflops / (ms * 1e-3) / 1e12 if ms else None
-            return {"kernel": name, "bound": "mfma", "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": (ach / PEAK_BF16_TFLOPS) if ach else None, "traffic": traffic.get(name),
+            return {"kernel": name, "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                    "frac": (ach / peak) if ach else None, "traffic": traffic.get(name),
                     "traffic_unit": "bytes/launch (rocprofv3 PMC)", "avg_launch_ms": ms,
                     "flops_per_launch": kflops}
 
@@ -205,8 +232,18 @@ def main():
             traffic = {}
         roof = roofline(args.roofline_kernel)
         roof["step_tflops"] = fpt * value / world / 1e12
-        roof["step_frac"] = roof["step_tflops"] / PEAK_BF16_TFLOPS
+        roof["step_frac"] = roof["step_tflops"] / peak
         roof["other_kernels"] = [roofline(n) for n in KERNEL_FLOPS if n != args.roofline_kernel]
+        # the weight-gradient GEMMs (split-K dW = dY^T X + bias gradient, every Linear of the step): the
+        # largest GEMM time slice; algorithmic 2*N*K*T per launch summed over the timed launches
+        avg, n_l, tot, fl = kern["gemm_wgrad"]
+        if n_l and fl:
+            ach = fl / (tot * 1e-3) / 1e12
+            roof["other_kernels"].append({"kernel": "gemm_wgrad (all shapes)", "bound": "mfma", "achieved": ach,
+                                          "peak": peak,
+                                          "unit": "TFLOP/s", "launches_per_step": n_l / args.steps,
+                                          "ms_per_step": tot / args.steps, "avg_launch_ms": avg,
+                                          "frac": ach / peak})
         res = {"metric": METRIC, "value": value,
                "unit": "feature-timesteps/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",

@@ -29,13 +29,22 @@ def timer_start(*names):
     _timer["ev"] = {n: [] for n in names}
 
 
-def timer_stop():
-    """{name: average duration (ms) of that kernel's launches since timer_start, or None}."""
+def timer_stop(detail=False):
+    """{name: average duration (ms) of that kernel's launches since timer_start, or None}; with
+    detail, {name: (average ms, launches, total ms, total algorithmic FLOPs or None)}."""
     ev = _timer["ev"]
     _timer["names"] = ()
     _timer["ev"] = {}
     torch.cuda.synchronize()
-    return {n: (sum(a.elapsed_time(b) for a, b in v) / len(v) if v else None) for n, v in ev.items()}
+    out = {}
+    for n, v in ev.items():
+        if not v:
+            out[n] = None if not detail else (None, 0, 0.0, None)
+            continue
+        tot = sum(a.elapsed_time(b) for a, b, _ in v)
+        fl = sum(f for _, _, f in v) if all(f is not None for _, _, f in v) else None
+        out[n] = tot / len(v) if not detail else (tot / len(v), len(v), tot, fl)
+    return out
 
 
 def _tick(name):
@@ -46,11 +55,11 @@ def _tick(name):
     return (name, e)
 
 
-def _tock(t0):
+def _tock(t0, flops=None):
     if t0 is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        _timer["ev"][t0[0]].append((t0[1], e1))
+        _timer["ev"][t0[0]].append((t0[1], e1, flops))
 
 
 def _p(t):
@@ -150,8 +159,10 @@ def linear_wgrad(dy, x, dW, db=None, accumulate=True, ws=None):
     need = N.load().rp_gemm_wgrad_workspace(Nn, K, T)
     if ws is None or ws.numel() * ws.element_size() < need:
         ws = torch.empty(max(need // 4, 4), device=dy.device, dtype=torch.float32)
+    e0 = _tick("gemm_wgrad")
     N.call("rp_gemm_wgrad", _dt(dy), Nn, K, T, _p(dy), dy.stride(0), _p(x), x.stride(0), _p(dW), _p(db),
            int(accumulate), _p(ws), ws.numel() * ws.element_size(), _stream(dy))
+    _tock(e0, 2.0 * Nn * K * T)
     return dW
 
 
