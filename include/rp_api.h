@@ -209,7 +209,7 @@ int64_t rp_attn_dropmask_elems(int B, int T, int H);
  * torch key_padding_mask semantics; models/transformer.py's masked_fill(-1e9) is identical unless
  * a sequence has no valid key at all).  out [B*Tq, ldo]; lse [B, H, Tq] fp32.  Backward: dout
  * [B*Tq, lddo]; dq [B*Tq, lddq], dk / dv [B*Tk, lddk / lddv] are fully overwritten; delta_ws
- * [B, H, Tq] fp32.  Dropout keep bits (forward -> backward) as for rp_attn_fwd with T -> (Tq, Tk):
+ * [3, B, H, Tq] fp32 (plane 0 = delta; see rp_attn_bwd).  Dropout keep bits (forward -> backward) as for rp_attn_fwd with T -> (Tq, Tk):
  * rp_mha_dropmask_elems(B, Tq, Tk, H) uint16 words [B*H][ceil(Tk/64)][4][roundup(Tq,64)].
  * Replaces models/transformer.py:37-81 MultiHeadAttention's score/softmax/PV core (self attention
  * of EncoderLayer :84-102, cross attention of CrossAttentionEncoderLayer :105-130 and
@@ -254,7 +254,9 @@ int rp_mha_bwd(int dtype, const rp_mha_args* args, int phases, void* stream);
 int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk,
                 float scale, float dropout_p, uint32_t seed, void* out, void* out_lo, float* lse,
                 uint16_t* dropmask, void* stream);
-/* Backward; dqkv: [B*T, 3*H*dk] (fully overwritten); delta_ws: [B, H, T] fp32 workspace.
+/* Backward; dqkv: [B*T, 3*H*dk] (fully overwritten); delta_ws: [3, B, H, T] fp32 workspace (plane 0:
+ * delta = rowsum(dout * O); planes 1, 2: the dK/dV kernel's row constants -delta/(1/(1-p)) and
+ * -lse*log2(e) + log2(1/(1-p)), written by whichever call formed delta).
  * = rp_attn_bwd_dq_delta (dQ columns of dqkv, one workgroup per 128-query block, which also writes
  * delta = rowsum(dout * out) to delta_ws), then rp_attn_bwd_dkdv (dK, dV columns, one workgroup per
  * 128-key block, reading delta).  The phases are also exported separately (per-kernel timing);
@@ -262,8 +264,8 @@ int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int
 int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,
                 const float* lse, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
                 float dropout_p, const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream);
-int rp_attn_bwd_delta(int dtype, const void* out, const void* out_lo, const void* dout, int B, int T, int H, int dk,
-                      float* delta_ws, void* stream);
+int rp_attn_bwd_delta(int dtype, const void* out, const void* out_lo, const void* dout, const float* lse, int B,
+                      int T, int H, int dk, float dropout_p, float* delta_ws, void* stream);
 int rp_attn_bwd_dkdv(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
                      const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
                      const uint16_t* dropmask, void* dqkv, void* stream);

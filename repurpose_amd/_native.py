@@ -72,7 +72,7 @@ _SIGNATURES = {
     "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rp_attn_bwd": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp,
                           c_vp, c_vp, c_vp]),
-    "rp_attn_bwd_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_vp, c_vp]),
+    "rp_attn_bwd_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_vp, c_vp]),
     "rp_attn_bwd_dkdv": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp]),
     "rp_attn_bwd_dq_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp,
                                    c_vp, c_vp]),

@@ -600,7 +600,11 @@ __global__ void attn_delta_kernel(MhaDev a) {
     s += __shfl_xor(s, 4, 64);
     if ((lane & 7) == 0) {
       const int b = (int)(row / a.Tq), t = (int)(row % a.Tq);
-      a.delta[((int64_t)b * a.H + e / HD) * a.Tq + t] = s;
+      const int64_t at = ((int64_t)b * a.H + e / HD) * a.Tq + t, plane = (int64_t)a.B * a.H * a.Tq;
+      a.delta[at] = s;
+      // the dK/dV kernel's row constants (plane 1, 2): -delta/ds and -lse*log2(e) + log2(ds)
+      a.delta[plane + at] = -s / a.drop_scale;
+      if (a.lse) a.delta[2 * plane + at] = -(a.lse[at] * LOG2E - log2f(a.drop_scale));
     }
   }
 }
@@ -896,6 +900,300 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
 }
 
 // =================================================================================================
+// backward: dK, dV — bf16, LDS-DMA staged variant (the default for bf16; RP_ATTN_DMA=0 selects the
+// register-staged kernel above).  Same math and register layouts as attn_bwd_kv_kernel; what changes
+// is how the query tiles reach LDS:
+//  * global_load_lds (LDS-DMA) writes the Q / dO tiles straight into the XOR-swizzled images (the
+//    swizzle goes on the per-lane source address), the raw lse / delta rows and the keep-bit words:
+//    no staging registers, no ds_write, no per-tile VALU for the copies;
+//  * a three-buffer ring with the DMA two tiles ahead (a tile's loads have a whole tile of compute
+//    plus a barrier to land), one barrier per tile: it both publishes tile it and frees the buffer
+//    the DMA of tile it + 2 overwrites;
+//  * rows past Tq repeat the last row (clamped source rows, no zero fill); their probabilities are
+//    forced to 0 through the S accumulators' start (-inf), so they contribute nothing.
+// =================================================================================================
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+
+// One LDS-DMA wave instruction: lane l's 16 bytes at g land at LDS byte address lds + 16 l.  Issued as
+// inline asm on purpose: the compiler then does not track it, so it inserts no conservative
+// vmcnt(0) before the LDS reads of a step (its alias tracking cannot tell that those read another
+// ring slot, and across the loop back-edge it loses the count) — the kernels' explicit counted
+// vmcnt + barrier order every DMA before its readers.  m0 is saved and restored around it.
+__device__ __forceinline__ void dma16(const void* g, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, off\n\t"
+      "s_nop 0\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "v"(g)
+      : "memory");
+}
+
+// the same for 4 bytes per lane (lane l -> lds + 4 l)
+__device__ __forceinline__ void dma4(const void* g, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %2, off\n\t"
+      "s_nop 0\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "v"(g)
+      : "memory");
+}
+
+// DMA source of the S start of query rows past Tq: -inf, so P = 0 on those rows
+__device__ const float kPadStart[1] = {-INFINITY};
+
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// rows [row0, row0 + 64) of a [rows][64] bf16 operand (row stride ld) -> the swizzled 8 KB image of
+// lds_off<bf16>: eight 1 KB pieces (8 rows each), two per wave; lane l of a piece lands at physical
+// 16-byte chunk l & 7 of row l >> 3, which holds logical chunk (l & 7) ^ (((row >> 1) & 3) << 1)
+__device__ __forceinline__ void dma_rows64(const bf16* __restrict__ base, int64_t ld, int row0, int nrows, char* tile,
+                                           int w, int lane) {
+  const uint32_t t = lds_addr(tile);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int I = w * 2 + j;
+    const int r = I * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (((r >> 1) & 3) << 1);
+    int rr = row0 + r;
+    rr = rr < nrows ? rr : nrows - 1;
+    dma16(base + (int64_t)rr * ld + c * 8, t + I * 1024);
+  }
+}
+
+// raw workgroup barrier: no release / acquire fence, so the compiler adds no vmcnt(0) for the LDS-DMA
+// loads still in flight (the explicit counted vmcnt before it is what makes a tile's DMA visible);
+// the empty asm statements keep the compiler from moving memory operations across it
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool DROP, int KTW>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
+  constexpr int KB = NW * 16 * KTW;  // keys per workgroup
+  using C = AttnCfg<bf16>;
+  constexpr int TILE = KV_QT * C::ROWB;
+  // keep bits: KB/64 key tiles x 4 groups x 64 queries, u16 — one full 1 KB DMA piece (at KB = 64 the
+  // second half holds a copy of the first)
+  constexpr int MASKB = 1024;
+  constexpr int BUF = 2 * TILE + 2 * KV_QT * 4 + MASKB;  // Q, dO, raw lse, raw delta, keep bits
+  constexpr int NBUF = 3;
+  // three separate arrays rather than one indexed ring: every LDS address of a step is then a per-lane
+  // base plus an immediate offset
+  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const uint8_t* __restrict__ kvalid = a.kvalid;
+  const float drop_scale = a.drop_scale;
+  const uint16_t* __restrict__ dmask = a.dmask;
+  const int nkb = (Tk + KB - 1) / KB;
+  const int L = rp_xcd_remap(blockIdx.x, nkb * B * H);
+  const int bh = L / nkb, kb = L % nkb;
+  const int b = bh / H, h = bh % H;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
+  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + h * HD;
+  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + h * HD;
+  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + h * HD;
+  const bf16* dOg = (const bf16*)a.dout + (int64_t)b * Tq * lddo + h * HD;
+  // the delta workspace's row constants (written by whichever kernel formed delta): the S accumulators
+  // start at -lse*log2(e) + log2(ds) (plane 2), the dP accumulators at -delta/ds (plane 1)
+  const int64_t plane = (int64_t)B * H * Tq;
+  const float* nls_bh = a.delta + 2 * plane + (int64_t)bh * Tq;
+  const float* ndl_bh = a.delta + plane + (int64_t)bh * Tq;
+  const int kw0 = kb * KB + w * 16 * KTW;
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
+  // the kernel-side Q prescale (no RP_ATTN_Q_PRESCALED) and empty_uniform have no DMA form: the
+  // launcher sends those calls to the register-staged kernel
+
+  // K, V as B operands of S = Q' K^T and dP = dO V^T: lane holds X[kw0 + kt*16 + i][dk slots]
+  bf16x8 kf[KTW][2], vf[KTW][2];
+#pragma unroll
+  for (int kt = 0; kt < KTW; ++kt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      kf[kt][s] = row_frag_gmem(Kg, ldk, kw0 + kt * 16, Tk, s * 32, lane);
+      vf[kt][s] = row_frag_gmem(Vg, ldv, kw0 + kt * 16, Tk, s * 32, lane);
+    }
+  // consume K / V here, before the loop: otherwise the compiler places the wait for these loads at
+  // their first use inside the loop body, where it runs every ring cycle as a full vmcnt(0)
+#pragma unroll
+  for (int kt = 0; kt < KTW; ++kt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(kf[kt][s]), "v"(vf[kt][s]));
+
+  f32x4 dk[KTW][4], dv[KTW][4];
+#pragma unroll
+  for (int kt = 0; kt < KTW; ++kt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dk[kt][dt] = dv[kt][dt] = zero4();
+
+  auto ring = [&](auto bi) -> char* {
+    constexpr int BI = decltype(bi)::value;
+    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
+  };
+  // LDS-DMA of query tile it into ring slot BI: Q and dO (two 1 KB pieces each per wave), the S start
+  // (wave 1; -inf past Tq) and dP start (wave 2) rows and the keep-bit words (wave 3, with dropout):
+  // D = 4 DMA instructions per wave, 5 for waves 1, 2 and (with dropout) 3
+  auto issue = [&](int it, auto bi) {
+    char* buf = ring(bi);
+    const int qs0 = it * KV_QT;
+    dma_rows64(Qg, ldq, qs0, Tq, buf, w, lane);
+    dma_rows64(dOg, lddo, qs0, Tq, buf + TILE, w, lane);
+    const int q = qs0 + lane;
+    if (w == 1) dma4(q < Tq ? nls_bh + q : kPadStart, lds_addr(buf + 2 * TILE));
+    if (w == 2) dma4(ndl_bh + (q < Tq ? q : Tq - 1), lds_addr(buf + 2 * TILE + KV_QT * 4));
+    if (DROP && w == 3) {
+      const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
+      int tile = kb * (KB / 64) + (r >> 2);
+      tile = tile < KT ? tile : KT - 1;  // keys past Tk: their dK / dV rows are written as zeros
+      // KB = 64: lanes 32..63 repeat lanes 0..31's words into the unused second half of the slot
+      dma16(dmask + (((int64_t)bh * KT + tile) * 4 + (r & 3)) * ldm + qs0 + cch * 8,
+            lds_addr(buf + 2 * TILE + 2 * KV_QT * 4));
+    }
+  };
+  // step it waits for DMA(it); issued after it by then: DMA(it + 1) (D instructions, if it exists)
+  auto wait_tile = [&](bool next) {
+    if (!next)
+      wait_vm<0>();
+    else if (w == 1 || w == 2 || (DROP && w == 3))
+      wait_vm<5>();
+    else
+      wait_vm<4>();
+  };
+
+  const int nqt = (Tq + KV_QT - 1) / KV_QT;
+  issue(0, std::integral_constant<int, 0>());
+  if (nqt > 1) issue(1, std::integral_constant<int, 1>());
+  auto step = [&](auto bi, int it) {
+    constexpr int BI = decltype(bi)::value;
+    wait_tile(it + 1 < nqt);
+    raw_barrier();
+    if (it + 2 < nqt) issue(it + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    const char* cur = ring(bi);
+    const char* Ql = cur;
+    const char* dOl = cur + TILE;
+    const float* lrow = reinterpret_cast<const float*>(cur + 2 * TILE);
+    const float* drow = lrow + KV_QT;
+    const uint16_t* mw = reinterpret_cast<const uint16_t*>(cur + 2 * TILE + 2 * KV_QT * 4);
+
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      f32x4 s[2][KTW], dp[2][KTW], ndq[2], nl[2];
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const int r0 = (2 * hf + qq) * 16 + 4 * g;
+        nl[qq] = *reinterpret_cast<const f32x4*>(lrow + r0);
+        ndq[qq] = *reinterpret_cast<const f32x4*>(drow + r0);
+      }
+      RP_PRIO(1);
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          bf16x8 qa = row_frag_lds(Ql, (2 * hf + qq) * 16, ss * 32, lane);
+          bf16x8 da = row_frag_lds(dOl, (2 * hf + qq) * 16, ss * 32, lane);
+#pragma unroll
+          for (int kt = 0; kt < KTW; ++kt) {
+            s[qq][kt] = mfma_bf16(qa, kf[kt][ss], ss == 0 ? nl[qq] : s[qq][kt]);
+            dp[qq][kt] = mfma_bf16(da, vf[kt][ss], ss == 0 ? ndq[qq] : dp[qq][kt]);
+          }
+        }
+      RP_PRIO(0);
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const int qrow = (2 * hf + qq) * 16 + 4 * g;
+#pragma unroll
+        for (int kt = 0; kt < KTW; ++kt) {
+          // this lane's key: ko = key % 64 -> word row (tile half, group (ko%16)/4), bit (ko/16)*4 + ko%4
+          const int kw = w * 16 * KTW + kt * 16 + i;
+          const int ko = kw & 63;
+          const int mrow_l = (kw >> 6) * 4 + ((ko & 15) >> 2);
+          const int bit = (ko >> 4) * 4 + (ko & 3);
+          uint2 bits = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+          if constexpr (DROP) bits = *reinterpret_cast<const uint2*>(mw + mrow_l * KV_QT + qrow);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pr = rp_exp2(s[qq][kt][r]);  // with dropout: p * ds
+            if constexpr (DROP) {
+              const uint32_t km = keep_mask(r < 2 ? bits.x : bits.y, bit + 16 * (r & 1));
+              s[qq][kt][r] = bfi_select(km, pr, 0.f);
+              dp[qq][kt][r] = pr * bfi_select(km, dp[qq][kt][r], ndq[qq][r]);
+            } else {
+              s[qq][kt][r] = pr;
+              dp[qq][kt][r] = pr * dp[qq][kt][r];
+            }
+          }
+        }
+      }
+      bf16x8 pa[KTW], sa[KTW];
+#pragma unroll
+      for (int kt = 0; kt < KTW; ++kt) {
+        pa[kt] = pack8(s[0][kt], s[1][kt]);
+        sa[kt] = pack8(dp[0][kt], dp[1][kt]);
+      }
+      RP_PRIO(1);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 dob = col_frag_lds(dOl, hf * 32, dt * 16, lane);
+        const bf16x8 qb = col_frag_lds(Ql, hf * 32, dt * 16, lane);
+#pragma unroll
+        for (int kt = 0; kt < KTW; ++kt) {
+          dv[kt][dt] = mfma_bf16(pa[kt], dob, dv[kt][dt]);
+          dk[kt][dt] = mfma_bf16(sa[kt], qb, dk[kt][dt]);
+        }
+      }
+      RP_PRIO(0);
+    }
+  };
+  for (int it = 0; it < nqt; it += NBUF) {
+    step(std::integral_constant<int, 0>(), it);
+    if (it + 1 < nqt) step(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < nqt) step(std::integral_constant<int, 2>(), it + 2);
+  }
+  // store: dk[kt][dt][r] = dK[key = kw0 + kt*16 + 4g + r][dk = dt*16 + i]; masked keys -> 0;
+  // dK = dS^T Q' / log2(e)
+  bf16* dK = (bf16*)a.dk + (int64_t)b * Tk * a.lddk + h * HD;
+  bf16* dV = (bf16*)a.dv + (int64_t)b * Tk * a.lddv + h * HD;
+#pragma unroll
+  for (int kt = 0; kt < KTW; ++kt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = kw0 + kt * 16 + 4 * g + r;
+      if (key >= Tk) continue;
+      const bool ok = kvalid[(int64_t)b * Tk + key] != 0;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        rp_st(dK + (int64_t)key * a.lddk + dt * 16 + i, ok ? dk[kt][dt][r] * (1.f / LOG2E) : 0.f);
+        rp_st(dV + (int64_t)key * a.lddv + dt * 16 + i, ok ? dv[kt][dt][r] : 0.f);
+      }
+    }
+}
+
+// =================================================================================================
 // backward: dQ per 128-query block (4 waves x 32 queries), sweep over 64-key tiles
 // =================================================================================================
 // DELTA: the kernel also forms delta = rowsum(dO * O) of its queries (the lane's 16 dims of dO are
@@ -972,8 +1270,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     }
     if constexpr (DELTA) {
       const float dl = quad_sum(part);
-      if (g == 0 && q < Tq) a.delta[(int64_t)bh * Tq + q] = dl;
       dq[qt] = q < Tq ? -dl * (DROP ? 1.f / drop_scale : 1.f) : 0.f;
+      if (g == 0 && q < Tq) {  // delta and the dK/dV kernel's row constants (planes 1, 2)
+        const int64_t plane = (int64_t)B * H * Tq;
+        a.delta[(int64_t)bh * Tq + q] = dl;
+        a.delta[plane + (int64_t)bh * Tq + q] = dq[qt];
+        a.delta[2 * plane + (int64_t)bh * Tq + q] = -lq[qt];
+      }
     }
   }
   // no valid key + empty_uniform: the scores were constants (masked_fill), so dQ = 0 (delta above
@@ -1204,6 +1507,16 @@ static int attn_block_override() {
   return v;
 }
 
+// RP_ATTN_DMA=0 selects the register-staged backward kernels (A/B tuning)
+static bool attn_dma_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_ATTN_DMA");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
+
 template <typename T>
 int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
   // 128-query blocks unless that leaves fewer than two workgroups per CU (256 CUs): then 64
@@ -1262,14 +1575,27 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   }
   if (phases & 2) {
     // 128-key blocks unless that leaves fewer than two workgroups per CU: then 64
-    if (attn_block_override() ? attn_block_override() == 64 : (int64_t)nkb * a.B * a.H < 512) {
-      const dim3 grid((unsigned)((a.Tk + NW * 16 - 1) / (NW * 16) * a.B * a.H));
+    const bool small_kv = attn_block_override() ? attn_block_override() == 64 : (int64_t)nkb * a.B * a.H < 512;
+    const dim3 grid(small_kv ? (unsigned)((a.Tk + NW * 16 - 1) / (NW * 16) * a.B * a.H) : (unsigned)(nkb * a.B * a.H));
+    // bf16 with the producer's Q prescale: the LDS-DMA staged kernel (RP_ATTN_DMA=0: register staged)
+    if (std::is_same<T, bf16>::value && a.qpre && !a.empty_uniform && attn_dma_enabled()) {
+      if (small_kv) {
+        if (a.drop_thresh)
+          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<true, 1>), grid, dim3(NT), 0, s, a);
+        else
+          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<false, 1>), grid, dim3(NT), 0, s, a);
+      } else {
+        if (a.drop_thresh)
+          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<true, 2>), grid, dim3(NT), 0, s, a);
+        else
+          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<false, 2>), grid, dim3(NT), 0, s, a);
+      }
+    } else if (small_kv) {
       if (a.drop_thresh)
         hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true, 1>), grid, dim3(NT), 0, s, a);
       else
         hipLaunchKernelGGL((attn_bwd_kv_kernel<T, false, 1>), grid, dim3(NT), 0, s, a);
     } else {
-      const dim3 grid((unsigned)(nkb * a.B * a.H));
       if (a.drop_thresh)
         hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true, 2>), grid, dim3(NT), 0, s, a);
       else
@@ -1426,8 +1752,8 @@ extern "C" int rp_attn_bwd(int dtype, const void* qkv, const void* out, const vo
                          dqkv, delta_ws, stream);
 }
 
-extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* out_lo, const void* dout, int B, int T, int H,
-                                 int dk, float* delta_ws, void* stream) {
+extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* out_lo, const void* dout, const float* lse,
+                                 int B, int T, int H, int dk, float dropout_p, float* delta_ws, void* stream) {
   RP_REQUIRE(dk == HD, "rp_attn_bwd_delta: head dim %d unsupported (64)", dk);
   RP_REQUIRE(B >= 0 && T >= 0 && H > 0, "rp_attn_bwd_delta: bad shape");
   if (B == 0 || T == 0) return RP_OK;
@@ -1438,6 +1764,8 @@ extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* out_lo,
   a.B = B; a.Tq = T; a.Tk = T; a.H = H; a.out = const_cast<void*>(out); a.ldo = (int64_t)H * HD; a.dout = dout;
   a.out_lo = dtype == RP_BF16 ? const_cast<void*>(out_lo) : nullptr;
   a.lddo = (int64_t)H * HD; a.delta = delta_ws;
+  a.lse = const_cast<float*>(lse);
+  a.drop_scale = dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f;
   return launch_mha_bwd_dtype(dtype, 1, a, (hipStream_t)stream);
 }
 

@@ -272,7 +272,7 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
         raise ValueError("attn_bwd: dropout needs the forward's dropmask")
     dk = qkv.shape[1] // (3 * H)
     dqkv = torch.empty_like(qkv)
-    delta = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
+    delta = torch.empty(3, B, H, T, device=qkv.device, dtype=torch.float32)  # delta + 2 row-constant planes
     st, dt = _stream(qkv), _adt(qkv, q_prescaled)
     e0 = _tick("attn_bwd")
     if _FUSED_DELTA:  # dQ first, with the delta = rowsum(dO * O) pre-pass fused in; dK/dV reads it
@@ -281,7 +281,8 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
                H, dk, float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
         _tock(e2)
     else:
-        N.call("rp_attn_bwd_delta", dt, _p(out), _p(out_lo), _p(dout), B, T, H, dk, _p(delta), st)
+        N.call("rp_attn_bwd_delta", dt, _p(out), _p(out_lo), _p(dout), _p(lse), B, T, H, dk, float(dropout_p),
+               _p(delta), st)
     e1 = _tick("attn_bwd_dkdv")
     N.call("rp_attn_bwd_dkdv", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
            float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
@@ -342,7 +343,7 @@ def mha_bwd(q, k, v, out, dout, lse, key_valid, B, Tq, Tk, H, scale, dropout_p=0
     dq = torch.empty(B * Tq, H * dk, device=q.device, dtype=q.dtype)
     dkk = torch.empty(B * Tk, H * dk, device=q.device, dtype=q.dtype)
     dv = torch.empty(B * Tk, H * dk, device=q.device, dtype=q.dtype)
-    delta = torch.empty(B, H, Tq, device=q.device, dtype=torch.float32)
+    delta = torch.empty(3, B, H, Tq, device=q.device, dtype=torch.float32)
     a = N.MhaArgs()
     a.q, a.ldq = _rows(q, H, dk)
     a.k, a.ldk = _rows(k, H, dk)

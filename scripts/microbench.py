@@ -42,13 +42,20 @@ def main():
         kv = torch.ones(B, T, dtype=torch.uint8, device=dev)
         do = torch.randn(M, d, generator=g).to(dev, bf)
         fl = 4.0 * B * H * T * T * 64
+        olo = torch.empty(M, d, device=dev, dtype=bf)
         for p in (0.0, 0.1):
-            r = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 1)
-            o, lse = r[0], r[1]
-            extra = r[2:]
-            t = timeit(lambda: K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 1), a.reps)
+            # as the model calls them: Q columns prescaled by the QKV GEMM, output residual kept
+            r = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 1, q_prescaled=True, out_lo=olo)
+            o, lse, mask = r
+            t = timeit(lambda: K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 1, q_prescaled=True, out_lo=olo), a.reps)
             res.append((f"attn_fwd p={p}", t, fl / t / 1e9, "TFLOP/s"))
-            t = timeit(lambda: K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, 1, *extra), a.reps)
+            K.timer_start("attn_bwd_dq", "attn_bwd_dkdv")
+            t = timeit(lambda: K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True,
+                                          out_lo=olo), a.reps)
+            kt = K.timer_stop()
+            res.append((f"  attn_bwd_dq p={p}", kt["attn_bwd_dq"], 2 * fl / 4 / kt["attn_bwd_dq"] / 1e9, "TFLOP/s alg"))
+            res.append((f"  attn_bwd_dkdv p={p}", kt["attn_bwd_dkdv"], 6 * fl / 4 / kt["attn_bwd_dkdv"] / 1e9,
+                        "TFLOP/s alg"))
             res.append((f"attn_bwd p={p} (dQ+delta, dK/dV)", t, 2 * fl / t / 1e9, "TFLOP/s alg"))
     if a.only in ("", "gemm"):
         for (n, k, name) in [(3 * d, d, "qkv"), (d, d, "out_proj"), (dff, d, "linear1"), (d, dff, "linear2")]:

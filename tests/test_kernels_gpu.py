@@ -467,36 +467,39 @@ def test_wgrad_splitk_with_bias(dev, dtype, T, Nn, Kd):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_attention_bwd_fused_delta_matches_unfused(dev, dtype, p):
+@pytest.mark.parametrize("qpre", [False, True])
+def test_attention_bwd_fused_delta_matches_unfused(dev, dtype, p, qpre):
     """rp_attn_bwd_dq_delta (delta formed inside the dQ kernel, dQ before dK/dV) against the unfused
-    sequence rp_attn_bwd_delta -> rp_attn_bwd_dkdv -> rp_attn_bwd_dq on the same inputs."""
+    sequence rp_attn_bwd_delta -> rp_attn_bwd_dkdv -> rp_attn_bwd_dq on the same inputs; with the
+    Q-prescaled flag in bf16 the dK/dV step is the LDS-DMA kernel, which reads the row constants either
+    delta producer writes (workspace planes 1, 2)."""
     from repurpose_amd import _native as N
     B, H, T = 2, 8, 200
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=5).to(dtype)
     kv = (torch.arange(T, device=dev)[None] < torch.tensor([T, 150], device=dev)[:, None]).to(torch.uint8)
-    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 77)
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 77, q_prescaled=qpre)
     do = rnd(B * T, H * 64, dev=dev, seed=6).to(dtype)
-    dt = N.RP_BF16 if dtype == torch.bfloat16 else N.RP_F32
+    dt = (N.RP_BF16 if dtype == torch.bfloat16 else N.RP_F32) | (K.RP_ATTN_Q_PRESCALED if qpre else 0)
     st = torch.cuda.current_stream(dev).cuda_stream
     P = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     outs = []
     for fused in (True, False):
         dqkv = torch.full_like(qkv, float("nan"))
-        delta = torch.full((B, H, T), float("nan"), device=dev)
+        delta = torch.full((3, B, H, T), float("nan"), device=dev)
         args = (P(qkv), P(do), P(lse), P(delta), P(kv), B, T, H, 64, 0.125, p, P(mask), P(dqkv), st)
         if fused:
             N.call("rp_attn_bwd_dq_delta", dt, P(qkv), P(o), P(None), P(do), P(lse), P(delta), P(kv), B, T, H, 64, 0.125, p,
                    P(mask), P(dqkv), st)
             N.call("rp_attn_bwd_dkdv", dt, *args)
         else:
-            N.call("rp_attn_bwd_delta", dt, P(o), P(None), P(do), B, T, H, 64, P(delta), st)
+            N.call("rp_attn_bwd_delta", dt, P(o), P(None), P(do), P(lse), B, T, H, 64, p, P(delta), st)
             N.call("rp_attn_bwd_dkdv", dt, *args)
             N.call("rp_attn_bwd_dq", dt, *args)
         outs.append((dqkv, delta))
     torch.cuda.synchronize()
     dref = (do.double() * o.double()).view(B, T, H, 64).sum(-1).permute(0, 2, 1)
     for dqkv, delta in outs:
-        close(delta, dref, atol=1e-4, rtol=1e-4, what="delta")
+        close(delta[0], dref, atol=1e-4, rtol=1e-4, what="delta")
         assert torch.isfinite(dqkv).all()
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     close(outs[0][0], outs[1][0].double(), atol=tol, rtol=tol, what="fused vs unfused dqkv")
