@@ -48,7 +48,25 @@ struct EpiDev {
   int accumulate;
   int64_t col_scale_n;  // columns n < col_scale_n are multiplied by col_scale after the bias
   float col_scale;
+  int split_major;  // split-K: deal the (split, tile) work items split-major over the XCDs (see tile_split)
 };
+
+// Work item of a workgroup: output tile t (XCD-aware: consecutive tiles share an XCD's L2) and, for
+// split-K (MODE 1), the K split.  split_major: the (split, tile) pairs are numbered split-major and
+// dealt in contiguous ranges per XCD, so the workgroups of one XCD share K ranges (the wgrad
+// operands dY and X are then fetched once per XCD instead of once per output tile column / row).
+template <int MODE>
+__device__ __forceinline__ void tile_split(int tiles, int split_major, int& t, int& split) {
+  if (MODE == 1 && split_major) {
+    const int nwg = (int)(gridDim.x * gridDim.y);
+    const int w = rp_xcd_remap((int)(blockIdx.y * gridDim.x + blockIdx.x), nwg);
+    split = w / tiles;
+    t = w % tiles;
+  } else {
+    t = rp_xcd_remap(blockIdx.x, tiles);
+    split = MODE == 1 ? (int)blockIdx.y : 0;
+  }
+}
 
 // --- global -> register staging -----------------------------------------------------------
 // Each operand tile is 1024 chunks of 16 bytes; 256 threads own 4 chunks each.
@@ -196,11 +214,11 @@ constexpr int gemm_lds_bytes() {
 template <typename TC, int MODE, bool HALVES = false>
 __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* lds, int tid, int lane, int wm, int wn,
                                               int64_t m0, int64_t n0, int64_t M, int64_t N, TC* __restrict__ Cout,
-                                              int64_t ldc, float alpha, const EpiDev& ep) {
+                                              int64_t ldc, float alpha, const EpiDev& ep, int split) {
   float* cs = reinterpret_cast<float*>(lds);
   constexpr int OV = 16 / (int)sizeof(TC);
   constexpr int CPRO = BN / OV;
-  TC* Cbase = Cout + (MODE == 1 ? (int64_t)blockIdx.y * M * ldc : 0);
+  TC* Cbase = Cout + (MODE == 1 ? (int64_t)split * M * ldc : 0);
   constexpr int NH = HALVES ? 2 : 1;  // staging passes
   constexpr int HR = BM / NH;          // rows per pass
 #pragma unroll 1
@@ -289,7 +307,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* ld
 // threads sharing a chunk through LDS and write this split's partial row
 template <int VEC>
 __device__ __forceinline__ void bias_reduce(const float (&bacc)[VEC], char* lds, int tid, int64_t m0, int64_t M,
-                                            float* __restrict__ bslab) {
+                                            float* __restrict__ bslab, int split) {
   __syncthreads();
   constexpr int CPR = BM / VEC;
   float* red = reinterpret_cast<float*>(lds);
@@ -300,7 +318,7 @@ __device__ __forceinline__ void bias_reduce(const float (&bacc)[VEC], char* lds,
     const int c = tid / VEC, e = tid % VEC;
     float sum = 0.f;
     for (int j = 0; j < NT / CPR; ++j) sum += red[(c + CPR * j) * VEC + e];
-    bslab[(int64_t)blockIdx.y * M + m0 + tid] = sum;
+    bslab[(int64_t)split * M + m0 + tid] = sum;
   }
 }
 
@@ -320,12 +338,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_n = (int)((N + BN - 1) / BN);
   const int tiles_m = (int)((M + BM - 1) / BM);
-  const int t = rp_xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int t, split;
+  tile_split<MODE>(tiles_m * tiles_n, ep.split_major, t, split);
   const int64_t m0 = (int64_t)(t / tiles_n) * BM;
   const int64_t n0 = (int64_t)(t % tiles_n) * BN;
   int64_t kbeg = 0, kend = K;
   if (MODE == 1) {
-    kbeg = (int64_t)blockIdx.y * kchunk;
+    kbeg = (int64_t)split * kchunk;
     kend = kbeg + kchunk < K ? kbeg + kchunk : K;
   }
   const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
@@ -368,8 +387,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64
     __syncthreads();
   }
 
-  gemm_epilogue<TC, MODE>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep);
-  if (MODE == 1 && want_bias) bias_reduce<C::VEC>(bacc, lds, tid, m0, M, bslab);
+  gemm_epilogue<TC, MODE>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
+  if (MODE == 1 && want_bias) bias_reduce<C::VEC>(bacc, lds, tid, m0, M, bslab, split);
 }
 
 // ============================ bf16 fast path: LDS-DMA staged main loop ============================
@@ -483,12 +502,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_n = (int)((N + BN - 1) / BN);
   const int tiles_m = (int)((M + BM - 1) / BM);
-  const int t = rp_xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int t, split;
+  tile_split<MODE>(tiles_m * tiles_n, ep.split_major, t, split);
   const int64_t m0 = (int64_t)(t / tiles_n) * BM;
   const int64_t n0 = (int64_t)(t % tiles_n) * BN;
   int64_t kbeg = 0, kend = K;
   if (MODE == 1) {
-    kbeg = (int64_t)blockIdx.y * kchunk;
+    kbeg = (int64_t)split * kchunk;
     kend = kbeg + kchunk < K ? kbeg + kchunk : K;
   }
   const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
@@ -549,8 +569,384 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
     if (D::STAGES == 2) __syncthreads();
   }
   if (D::STAGES == 1) __syncthreads();
-  gemm_epilogue<TC, MODE, D::HALVES>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep);
-  if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab);
+  gemm_epilogue<TC, MODE, D::HALVES>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
+  if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab, split);
+}
+
+// ====================== 256-row tiles: 8 waves, whole-K-tile LDS-DMA ring =======================
+// One workgroup of 512 threads (8 waves as 2 (M) x 4 (N)) owns a 256 x BNT output tile (BNT = 256
+// or 128); each wave accumulates 128 x BNT/4 (8 x BNT/64 MFMA 16x16 tiles).  A K-tile (BK = 64) is
+// staged as 128-row "half images" in exactly the formats of the kernel above (k-major 128 x 64
+// kswz, m-major [64 k][128] mswz), so the fragment readers are shared; two K-tile stages
+// (A 32 KiB + B 16/32 KiB each) at one workgroup per CU.  Arithmetic intensity per staged byte is
+// 2x (BNT = 256) or 1.33x that of the 128x128 tile, which is what the per-CU L2 -> LDS rate bounds.
+// Pipeline (guide §5, 'Pipelining across barriers'): the LDS-DMA of K-tile t+2 is issued right
+// after the barrier that ends every wave's reads of K-tile t, so each fill has one whole K-tile of
+// MFMA time (8 waves x 64 MFMAs) to land; the loop waits with a counted s_waitcnt vmcnt and a raw
+// s_barrier (never __syncthreads(), whose fence would drain the DMA in flight), and all LDS lives
+// in one __shared__ array (guide item 4(a)).
+constexpr int NT8 = 512;
+constexpr int HIMG = 16384;  // one 128 x 64 bf16 half image
+
+template <int VM, int LGKM>
+__device__ __forceinline__ void rp_waitcnt() {
+  // gfx9 s_waitcnt immediate: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((VM & 15) | ((VM >> 4) << 14) | (7 << 4) | ((LGKM & 15) << 8));
+}
+
+__device__ __forceinline__ void rp_raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// one 1 KiB piece (wave-instruction index I) of a half image
+template <bool KMAJ, int KD>
+__device__ __forceinline__ void glds_piece8(const bf16* __restrict__ base, int64_t ld, int64_t rows_lim, int64_t row0,
+                                            int64_t k0, char* img, int I, int lane) {
+  const bf16* src;
+  if (KMAJ) {
+    int r, lc;
+    if constexpr (KD == 64) {
+      r = I * 8 + (lane >> 3);
+      lc = kswz(r, lane & 7);
+    } else {
+      r = I * 16 + (lane >> 2);
+      lc = kswz32(r, lane & 3);
+    }
+    int64_t rr = row0 + r;
+    if (rr >= rows_lim) rr = rows_lim - 1;
+    src = base + rr * ld + k0 + lc * 8;
+  } else {
+    const int k = I * 4 + (lane >> 4);
+    const int lc = mswz(k, lane & 15);
+    int64_t cc = row0 + lc * 8;
+    if (cc >= rows_lim) cc = rows_lim - 8;
+    src = base + (k0 + k) * ld + cc;
+  }
+  __builtin_amdgcn_global_load_lds(src, (lds_void*)(img + I * 1024), 16, 0, 0);
+}
+
+template <int BNT, int KD = 64, int S = 2>
+struct G8 {
+  static constexpr int NBH = BNT / 128;               // B half images per slot
+  static constexpr int HB = 128 * KD * 2;             // bytes of one half image
+  static constexpr int SLOT = (2 + NBH) * HB;         // bytes of one K-slab slot (A 256 rows + B BNT rows)
+  static constexpr int LPT = (2 + NBH) * KD / 32;     // LDS-DMA instructions per thread per slot
+  static constexpr int WN = BNT / 4;                  // output columns per wave
+  static constexpr int JT = WN / 16;                  // MFMA column tiles per wave
+  static constexpr int CST = BNT + 4;                 // fp32 row stride of an epilogue pass
+  static constexpr int EPI = 64 * CST * 4;            // one 64-row epilogue pass
+  static constexpr int LDS = S * SLOT > EPI ? S * SLOT : EPI;
+};
+
+// epilogue: four passes of 64 rows staged as fp32 in LDS, then 16-byte row chunks per thread
+template <typename TC, int MODE, int BNT>
+__device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], char* lds, int tid, int lane, int wm,
+                                               int wn, int64_t m0, int64_t n0, int64_t M, int64_t N,
+                                               TC* __restrict__ Cout, int64_t ldc, float alpha, const EpiDev& ep,
+                                               int split) {
+  using G = G8<BNT>;
+  float* cs = reinterpret_cast<float*>(lds);
+  constexpr int OV = 16 / (int)sizeof(TC);
+  constexpr int CPRO = BNT / OV;
+  TC* Cbase = Cout + (MODE == 1 ? (int64_t)split * M * ldc : 0);
+  const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    if (pass) __syncthreads();
+    if (wm == (pass >> 1)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < G::JT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cs[(i * 16 + g * 4 + r) * G::CST + wn * G::WN + j * 16 + cl] = acc[(pass & 1) * 4 + i][j][r];
+    }
+    __syncthreads();
+    for (int id = tid; id < 64 * CPRO; id += NT8) {
+      const int row = id / CPRO, cc = (id % CPRO) * OV;
+      const int64_t m = m0 + pass * 64 + row, n = n0 + cc;
+      if (m >= M || n >= N) continue;
+      float v[OV];
+#pragma unroll
+      for (int e = 0; e < OV; e += 4) {
+        float4 q = *reinterpret_cast<const float4*>(cs + row * G::CST + cc + e);
+        v[e] = q.x * alpha; v[e + 1] = q.y * alpha; v[e + 2] = q.z * alpha; v[e + 3] = q.w * alpha;
+      }
+      if (MODE == 0) {
+        if (ep.bias) {
+#pragma unroll
+          for (int e = 0; e < OV; e += 4) {
+            float4 q = *reinterpret_cast<const float4*>(ep.bias + n + e);
+            v[e] += q.x; v[e + 1] += q.y; v[e + 2] += q.z; v[e + 3] += q.w;
+          }
+        }
+        if (n < ep.col_scale_n) {
+#pragma unroll
+          for (int e = 0; e < OV; ++e) v[e] *= ep.col_scale;
+        }
+        if (ep.relu) {
+#pragma unroll
+          for (int e = 0; e < OV; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (ep.drop_thresh) {
+          const uint32_t kb = rp_keep_bits<OV>(ep.drop_seed, (uint32_t)(m * N + n), ep.drop_thresh);
+#pragma unroll
+          for (int e = 0; e < OV; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * ep.drop_scale : 0.f;
+        }
+        if (ep.gate) {
+          if (ep.gate_bf16) {
+            const bf16* gp = (const bf16*)ep.gate + m * ep.ldg + n;
+#pragma unroll
+            for (int e = 0; e < OV; ++e) v[e] = (float)gp[e] > 0.f ? v[e] * ep.gate_scale : 0.f;
+          } else {
+            const float* gp = (const float*)ep.gate + m * ep.ldg + n;
+#pragma unroll
+            for (int e = 0; e < OV; ++e) v[e] = gp[e] > 0.f ? v[e] * ep.gate_scale : 0.f;
+          }
+        }
+        if (ep.residual) {
+#pragma unroll
+          for (int e = 0; e < OV; e += 4) {
+            float4 q = *reinterpret_cast<const float4*>(ep.residual + m * ep.ldr + n + e);
+            v[e] += q.x; v[e + 1] += q.y; v[e + 2] += q.z; v[e + 3] += q.w;
+          }
+        }
+      }
+      TC* dst = Cbase + m * ldc + n;
+      if constexpr (std::is_same<TC, float>::value) {
+        if (MODE == 0 && ep.accumulate) {
+          float4 q = *reinterpret_cast<const float4*>(dst);
+          v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+        }
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint4 o;
+        bf16* ob = reinterpret_cast<bf16*>(&o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ob[e] = (bf16)v[e];
+        *reinterpret_cast<uint4*>(dst) = o;
+      }
+    }
+  }
+}
+
+// Phased main loop (cdna_hip_programming.md §5 'The 256² 8-phase template', written for this
+// tile): a 64-deep K-tile is four phases, one per quadrant (64 rows x 32 columns) of the wave's
+// 128 x 64 output: 16 MFMAs each.  A phase is a READ segment (its new fragments by ds_read, plus
+// any LDS-DMA pieces) and a COMPUTE segment (its MFMAs), each closed by a raw s_barrier.  Waves
+// 4-7 (wm = 1; the second wave of every SIMD) run one barrier behind waves 0-3, so on every SIMD
+// one wave reads while its partner computes.  Quadrant order (0,0) (0,1) (1,1) (1,0): phase 0
+// reads A rows 0-63 + B columns 0-31 of the wave's block, phase 1 B columns 32-63, phase 2 A rows
+// 64-127, phase 3 nothing.  Two LDS slots of one K-tile (A 2 x 16 KiB + B 2 x 16 KiB).
+// Slot reuse (barrier b(8t + j) = the j-th barrier of K-tile t's phases, G0's clock): the B
+// images of K-tile t are dead after b(8t+4), the A images after b(8t+6); the B pieces of K-tile
+// t+2 are issued in phase 3 of K-tile t, the A pieces of K-tile t+1 in phase 0 of K-tile t, and
+// every wave waits for its own pieces of K-tile t+1 (vmcnt(4): only B(t+2) may stay in flight)
+// before phase 3's first barrier, which every reader of K-tile t+1 passes afterwards.
+__device__ __forceinline__ void rp_lgkm0() {
+  __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));
+}
+
+template <bool AK, bool BKM, typename TC, int MODE, int BNT>
+__global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int64_t K, const bf16* __restrict__ A,
+                                                       int64_t lda, const bf16* __restrict__ B, int64_t ldb,
+                                                       TC* __restrict__ Cout, int64_t ldc, float alpha, EpiDev ep,
+                                                       int64_t kchunk, float* __restrict__ bslab) {
+  static_assert(BNT == 256, "phased 256-row kernel: 256 x 256 tiles");
+  using G = G8<BNT, 64, 2>;
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int tiles_n = (int)((N + BNT - 1) / BNT);
+  const int tiles_m = (int)((M + 255) / 256);
+  int t, split;
+  tile_split<MODE>(tiles_m * tiles_n, ep.split_major, t, split);
+  const int64_t m0 = (int64_t)(t / tiles_n) * 256;
+  const int64_t n0 = (int64_t)(t % tiles_n) * BNT;
+  int64_t kbeg = 0, kend = K;
+  if (MODE == 1) {
+    kbeg = (int64_t)split * kchunk;
+    kend = kbeg + kchunk < K ? kbeg + kchunk : K;
+  }
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int bimg = wn >> 1, bcol = (wn & 1) * 64;
+  const int nk = kend > kbeg ? (int)((kend - kbeg) / 64) : 0;
+  const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
+  float bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  // A pieces (2 half images x 2) and B pieces of K-tile kt into slot kt & 1
+  auto fill_a = [&](int kt) {
+    char* buf = lds + (kt & 1) * G::SLOT;
+    const int64_t k0 = kbeg + (int64_t)kt * 64;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        glds_piece8<AK, 64>(A, lda, M, m0 + 128 * h, k0, buf + h * G::HB, wid * 2 + j, lane);
+  };
+  auto fill_b = [&](int kt) {
+    char* buf = lds + (kt & 1) * G::SLOT;
+    const int64_t k0 = kbeg + (int64_t)kt * 64;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        glds_piece8<BKM, 64>(B, ldb, N, n0 + 128 * h, k0, buf + (2 + h) * G::HB, wid * 2 + j, lane);
+  };
+  auto ra = [&](const char* img, int i, int kk) -> bf16x8 {
+    return AK ? frag_k_swz<64>(img, i * 16, kk, lane) : frag_m_swz(img, i * 16, kk, lane);
+  };
+  auto rb = [&](const char* img, int j, int kk) -> bf16x8 {
+    return BKM ? frag_k_swz<64>(img, bcol + j * 16, kk, lane) : frag_m_swz(img, bcol + j * 16, kk, lane);
+  };
+  if (nk > 0) {
+    fill_a(0);
+    fill_b(0);
+    if (nk > 1) {
+      fill_b(1);
+      rp_waitcnt<4, 15>();
+    } else {
+      rp_waitcnt<0, 15>();
+    }
+  }
+  rp_raw_barrier();
+  if (wm == 1) rp_raw_barrier();  // the second wave of each SIMD runs one barrier behind
+
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = lds + (kt & 1) * G::SLOT;
+    const char* ai = cur + wm * G::HB;
+    const char* bi = cur + (2 + bimg) * G::HB;
+    // ---- phase 0: A rows 0-63, B columns 0-31; A pieces of K-tile kt+1 ----
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = ra(ai, i, kk * 32);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb0[j][kk] = rb(bi, j, kk * 32);
+    if (kt + 1 < nk) fill_a(kt + 1);
+    rp_raw_barrier();
+    rp_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb0[j][kk], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    rp_raw_barrier();
+    // ---- phase 1: B columns 32-63 ----
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb1[j][kk] = rb(bi, 2 + j, kk * 32);
+    rp_raw_barrier();
+    rp_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb1[j][kk], acc[i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    rp_raw_barrier();
+    // ---- phase 2: A rows 64-127 ----
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = ra(ai, 4 + i, kk * 32);
+    rp_raw_barrier();
+    rp_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb1[j][kk], acc[4 + i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    rp_raw_barrier();
+    // ---- phase 3: no fragment reads; B pieces of K-tile kt+2; own pieces of K-tile kt+1 landed ----
+    if (want_bias) {  // wgrad bias: column sums of the staged m-major dY tile, 4 x 16 B per thread
+      const char* hi = cur + (tid >> 8) * G::HB;
+      const int cg = tid & 15;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = ((tid >> 4) & 15) + 16 * j;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(hi + k * 256 + mswz(k, cg) * 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bacc[e] += (float)v[e];
+      }
+      rp_lgkm0();  // retired before the barrier after which the next A pieces may overwrite them
+    }
+    if (kt + 2 < nk) {
+      fill_b(kt + 2);
+      rp_waitcnt<4, 15>();
+    } else {
+      rp_waitcnt<0, 15>();
+    }
+    rp_raw_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb0[j][kk], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    rp_raw_barrier();
+  }
+  if (wm == 0) rp_raw_barrier();  // match the lagging half's barrier count
+  __syncthreads();
+  gemm8_epilogue<TC, MODE, BNT>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
+  if (MODE == 1 && want_bias) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bacc[j];
+    __syncthreads();
+    if (tid < 256 && m0 + tid < M) {
+      const int h = tid >> 7, cg = (tid & 127) >> 3, e = tid & 7;
+      float sum = 0.f;
+      for (int r = 0; r < 16; ++r) sum += red[((h << 8) + cg + 16 * r) * 8 + e];
+      bslab[(int64_t)split * M + m0 + tid] = sum;
+    }
+  }
+}
+
+// 256-row phased path selection.  RP_GEMM8=0 disables it, RP_GEMM8=1 forces it wherever legal
+// (read per call: scripts/gemm_ab.py switches it between launches).  Default: the wide short-K
+// shapes with at least one 256 x 256 tile per CU (MI355X, M = 16384: linear1 forward 54.6 ->
+// 48.9 us, the K = 512 dgrad into d_ff 61.0 -> 50.1 us); N = 512 shapes have only 128 tiles, and
+// N = 1536 ones 1.5 tiles per CU.
+static int rp_gemm8_mode() {
+  const char* e = getenv("RP_GEMM8");
+  return e ? (e[0] == '0' ? 0 : (e[0] == '1' ? 1 : -1)) : -1;
+}
+static int rp_gemm8_bn(int64_t M, int64_t N, int64_t kext) {
+  if (kext % 64 != 0 || kext < 128 || M < 256 || N % 8 != 0) return 0;
+  const int mode = rp_gemm8_mode();
+  if (mode == 0) return 0;
+  if (mode == 1) return 256;
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  return (N >= 2048 && kext <= 1024 && tiles >= 256) ? 256 : 0;
 }
 
 // dst[i] (+)= sum_s slab[s][i] in fixed slab order (deterministic), for the weight slabs (n
@@ -617,6 +1013,30 @@ static bool rp_dma_enabled() {
   return v != 0;
 }
 
+template <typename TC>
+int launch_gemm8(int bn, int64_t M, int64_t N, int64_t K, const bf16* a, int64_t lda, int ak, const bf16* b,
+                 int64_t ldb, int bk, TC* c, int64_t ldc, float alpha, const EpiDev& ep, hipStream_t s, int splits,
+                 int64_t kchunk, float* bslab) {
+  const int64_t tiles = ((M + 255) / 256) * ((N + bn - 1) / bn);
+#define RP_G8_LAUNCH1(AKV, BKV, MODEV, BNV, GRID)                                                            \
+  hipLaunchKernelGGL((gemm8_kernel<AKV, BKV, TC, MODEV, 256>), GRID, dim3(NT8), 0, s, M, N, K, a, lda, b, ldb, c, \
+                     ldc, alpha, ep, kchunk, bslab)
+#define RP_G8_LAUNCH(AKV, BKV, MODEV, GRID) RP_G8_LAUNCH1(AKV, BKV, MODEV, 256, GRID)
+  if (splits == 0) {
+    dim3 grid((unsigned)tiles);
+    if (ak && bk) RP_G8_LAUNCH(true, true, 0, grid);
+    else if (ak && !bk) RP_G8_LAUNCH(true, false, 0, grid);
+    else if (!ak && !bk) RP_G8_LAUNCH(false, false, 0, grid);
+    else RP_G8_LAUNCH(false, true, 0, grid);
+  } else {
+    dim3 grid((unsigned)tiles, (unsigned)splits);
+    RP_G8_LAUNCH(false, false, 1, grid);  // split-K serves the wgrad layout only
+  }
+#undef RP_G8_LAUNCH
+#undef RP_G8_LAUNCH1
+  return rp_check_launch("rp_gemm");
+}
+
 template <typename T, typename TC>
 int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int ak, const void* B,
                   int64_t ldb, int bk, void* Cp, int64_t ldc, float alpha, const EpiDev& ep,
@@ -626,6 +1046,10 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
   const T* b = (const T*)B;
   TC* c = (TC*)Cp;
   if constexpr (std::is_same<T, bf16>::value) {
+    const int bn8 = splits == 0 ? rp_gemm8_bn(M, N, K) : 0;
+    if (bn8 > 0 && rp_dma_enabled())
+      return launch_gemm8<TC>(bn8, M, N, K, (const bf16*)A, lda, ak, (const bf16*)B, ldb, bk, c, ldc, alpha, ep, s,
+                              splits, kchunk, bslab);
     const bool full_k = K % 32 == 0 && (splits == 0 || kchunk % 32 == 0);
     if (full_k && rp_dma_enabled()) {
       const int cfg = rp_gemm_cfg(splits == 0 ? K : kchunk, N);
@@ -700,6 +1124,32 @@ void wgrad_plan(int64_t M, int64_t N, int64_t K, int bk, int& splits, int64_t& k
   if (splits < 1) splits = 1;
 }
 
+// the 256 x 256 phased kernel's wgrad plan (only under RP_GEMM8=1): ~one workgroup per CU
+// (RP_WGRAD8_BLOCKS overrides), splits of whole 64-deep K-tiles, at least 8 per split; returns 0
+// when the 128 x 128 kernel runs.  Measured (scripts/gemm_ab.py, M = 16384, split-major mapping on
+// both): 46.0 / 31.2 / 53.2 / 53.4 / 67.3 us for the qkv / out_proj / linear1 / linear2 / input
+// projection weight gradients against 40.9 / 23.9 / 49.2 / 47.5 / 68.1 us on the 128 x 128 kernel
+// at two workgroups per CU — the m-major x m-major fragment reads (two transposed reads each) and
+// the 16-32 x larger fp32 slabs per tile cost more than the tile's operand reuse gains.
+int wgrad8_plan(int64_t M, int64_t N, int64_t K, int& splits, int64_t& kchunk) {
+  const int mode = rp_gemm8_mode();
+  if (mode != 1 || K % 64 != 0 || K < 512 || M < 256) return 0;
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  static int target = -1;
+  if (target < 0) {
+    const char* e = getenv("RP_WGRAD8_BLOCKS");
+    target = e ? atoi(e) : 256;
+    if (target < 1) target = 256;
+  }
+  int64_t sp = target / tiles;
+  const int64_t maxsp = K / (8 * 64);
+  if (sp > maxsp) sp = maxsp;
+  if (sp < 1) sp = 1;
+  kchunk = ((K + sp - 1) / sp + 63) / 64 * 64;
+  splits = (int)((K + kchunk - 1) / kchunk);
+  return 256;
+}
+
 }  // namespace
 
 extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int a_kmajor,
@@ -761,6 +1211,7 @@ extern "C" int64_t rp_gemm_wgrad_workspace(int64_t M, int64_t N, int64_t K) {
   int64_t k2;
   wgrad_plan(M, N, K, GemmCfg<float>::BK, s2, k2);
   if (s2 > splits) splits = s2;
+  if (wgrad8_plan(M, N, K, s2, k2) && s2 > splits) splits = s2;
   return (int64_t)splits * (M * N + M) * 4;
 }
 
@@ -779,15 +1230,21 @@ extern "C" int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const v
   const int bk = dtype == RP_BF16 ? GemmCfg<bf16>::BK : GemmCfg<float>::BK;
   int splits;
   int64_t kchunk;
-  wgrad_plan(M, N, K, bk, splits, kchunk);
+  const int bn8 = (dtype == RP_BF16 && rp_dma_enabled()) ? wgrad8_plan(M, N, K, splits, kchunk) : 0;
+  if (!bn8) wgrad_plan(M, N, K, bk, splits, kchunk);
   RP_REQUIRE(ws_bytes >= (int64_t)splits * (M * N + M) * 4, "rp_gemm_wgrad: workspace too small");
   float* slab = (float*)workspace;
   float* bslab = db ? slab + (int64_t)splits * M * N : nullptr;
   hipStream_t s = (hipStream_t)stream;
   EpiDev e{};
   e.gate_scale = 1.f;
+  const char* sm = getenv("RP_WGRAD_SPLIT_MAJOR");  // read per call (A/B scripts); default on
+  e.split_major = !(sm && sm[0] == '0');
   int rc;
-  if (dtype == RP_BF16)
+  if (bn8)
+    rc = launch_gemm8<float>(bn8, M, N, K, (const bf16*)dY, ldy, 0, (const bf16*)X, ldx, 0, slab, N, 1.f, e, s, splits,
+                             kchunk, bslab);
+  else if (dtype == RP_BF16)
     rc = launch_gemm_t<bf16, float>(M, N, K, dY, ldy, 0, X, ldx, 0, slab, N, 1.f, e, s, splits, kchunk, bslab);
   else
     rc = launch_gemm_t<float, float>(M, N, K, dY, ldy, 0, X, ldx, 0, slab, N, 1.f, e, s, splits, kchunk, bslab);
