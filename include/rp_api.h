@@ -20,7 +20,7 @@
  *                         models/MMCTransformer.py:159-179
  *   rp_rowdot_*           final Linear(256->1 / 256->2) of cls/reg heads models/MMCTransformer.py:71-93
  *   rp_colsum             bias / LayerNorm-affine gradient reductions (autograd of the above)
- *   rp_adam_step          torch.optim.Adam(lr, weight_decay) step  main.py:190-191,369
+ *   rp_adam_step(_dev)    torch.optim.Adam(lr, weight_decay) step  main.py:190-191,369
  *   rp_infer_select       inference_single_video                 models/MMCTransformer.py:181-229
  *   rp_softnms            soft_nms_intervals_cpu                 models/softnms.py:3-38
  *   rp_mha_fwd/bwd        models/transformer.py:37-81 MultiHeadAttention core (self / cross)
@@ -303,6 +303,23 @@ int rp_rowdot_bwd_dx(const float* dout, int64_t ldd, int64_t rows, int K, const 
  * p_lp (optional): refreshed bf16 copy of the updated parameters. */
 int rp_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                  float beta2, float eps, float weight_decay, int step, void* p_lp, void* stream);
+/* The same update with its coefficients read from device memory when the kernel runs (a captured
+ * HIP graph replays one launch with the host's per-step values): coef_dev[6] = the output of
+ * rp_adam_coefficients {lr/(1-beta1^step), beta1, beta2, eps, weight_decay, sqrt(1-beta2^step)},
+ * computed on the host exactly as rp_adam_step computes them (bitwise identical updates). */
+int rp_adam_coefficients(float lr, float beta1, float beta2, float eps, float weight_decay, int step,
+                         float* coef);
+int rp_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* coef_dev,
+                     void* p_lp, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Graph-replayable dropout streams (the captured training step, repurpose_amd/graph.py).
+ * rp_set_seed_base(ptr): while ptr != NULL, every launch that draws dropout (rp_gemm epilogue,
+ * rp_layernorm_fwd/bwd, attention forward) records ptr in its kernel arguments and draws with the
+ * seed rp_hash(*ptr, seed) — *ptr read when the kernel RUNS — instead of `seed`, so one captured
+ * launch gives a fresh stream per replay once the host rewrites the word.  Process-wide (the
+ * autograd backward launches from another thread); NULL (the default) restores plain seeds. */
+int rp_set_seed_base(const uint32_t* dev_ptr);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Inference.  rp_infer_select: per video b (one workgroup), prob = sigmoid(logit)*mask,

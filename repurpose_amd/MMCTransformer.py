@@ -178,6 +178,13 @@ class MMCTransformer(nn.Module):
             o, shp = layout[n]
             p.data = flat[o:o + p.numel()].view(shp)
         self._flat = flat
+        # host-side parameter table (the per-step checks walk this list, not named_parameters():
+        # the module-tree walk costs ~0.6 ms per call at L = 16, several calls per step)
+        self._ptable = [(n, p, layout[n][0]) for n, p in params]
+        self._plist = [p for n, p in self.named_parameters()]
+        self._trained_params = [p for n, p, _ in self._ptable if not n.startswith("reg_head.")]
+        self._flat_dirty = False
+        self._bound_grads = None
         self._layout = layout
         self._trainable = layout[next(n for n, _ in params if n.startswith("reg_head."))][0] \
             if any(n.startswith("reg_head.") for n, _ in params) else off
@@ -187,10 +194,29 @@ class MMCTransformer(nn.Module):
         self._lp_version = None
         assert total <= off
 
+    def _apply(self, fn, *args, **kwargs):
+        # .to() / .cuda() / .float() rebind every Parameter's storage: repack on the next use
+        out = super()._apply(fn, *args, **kwargs)
+        self._flat_dirty = True
+        return out
+
     def _flat_ok(self):
         f = self._flat
-        if f is None:
-            return False
+        if f is None or self._flat_dirty:
+            if f is None or not self._flat_walk_ok():
+                return False
+            self._flat_dirty = False
+            return True
+        # fast path: the table's first and last Parameters still view the flat buffer (catches a
+        # direct ``p.data = ...`` on them; module conversions go through _apply above)
+        base = f.data_ptr()
+        for n, p, o in (self._ptable[0], self._ptable[-1]):
+            if p.data_ptr() != base + 4 * o:
+                return False
+        return True
+
+    def _flat_walk_ok(self):
+        f = self._flat
         base = f.data_ptr()
         for n, p in self.named_parameters():
             o, _ = self._layout[n]
@@ -214,21 +240,18 @@ class MMCTransformer(nn.Module):
         """Make every trained Parameter's .grad a view of the flat gradient buffer.  If the trainer
         set grads to None (optimizer.zero_grad()), the buffer is zeroed first (grad semantics)."""
         g = self.flat_grads()
-        rebind = False
-        for n, p in self.named_parameters():
-            if n.startswith("reg_head."):
-                continue
-            o, shp = self._layout[n]
-            if p.grad is None or p.grad.data_ptr() != g.data_ptr() + 4 * o:
-                rebind = True
-                break
+        bound = self._bound_grads
+        rebind = bound is None or bound[0] is not g or any(
+            p.grad is not v for p, v in zip(self._trained_params, bound[1]))
         if rebind:
             g.zero_()
-            for n, p in self.named_parameters():
+            views = []
+            for n, p, o in self._ptable:
                 if n.startswith("reg_head."):
                     continue
-                o, shp = self._layout[n]
-                p.grad = g[o:o + p.numel()].view(shp)
+                p.grad = g[o:o + p.numel()].view(p.shape)
+                views.append(p.grad)
+            self._bound_grads = (g, views)
         return g
 
     def trainable_numel(self):
@@ -256,7 +279,7 @@ class MMCTransformer(nn.Module):
         ``p.data = view``, which gives the Parameter a version counter of its own: in-place updates
         through the Parameters (torch.optim.Adam, ``load_state_dict``'s copy_) bump only those, writes
         through the flat buffer bump only ``flat._version`` — the key covers both."""
-        return (self._flat._version,) + tuple(p._version for p in self.parameters())
+        return (self._flat._version,) + tuple(p._version for p in self._plist)
 
     def lowp_weights(self):
         """bf16 operand copy of the flat weights, refreshed when the fp32 master changed."""
@@ -277,6 +300,8 @@ class MMCTransformer(nn.Module):
 
     @property
     def device(self):
+        if self._flat is not None and self._flat_ok():
+            return self._flat.device
         return list(set(p.device for p in self.parameters()))[0]
 
     # ---------------------------------------------------------------- forward -------------------
@@ -290,7 +315,7 @@ class MMCTransformer(nn.Module):
         if flat.device != v.device:
             raise RuntimeError(f"model on {flat.device}, batch on {v.device}")
         run = _Schedule(self, v, a, t, masks, train=self.training)
-        params = [p for n, p in self.named_parameters() if not n.startswith("reg_head.")]
+        params = self._trained_params
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
             logits, offsets, feats = _ModelFunction.apply(run, *params)
         else:
@@ -374,6 +399,7 @@ class _Schedule:
         self.scale_drop = 1.0 / (1.0 - self.p) if self.p > 0 else 1.0
         self.dt = model.compute_dtype
         self.base_seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if train else 0
+        self.device_seeds = K.seed_base_active()
         self.saved = None
 
     # ---- parameter access ----
@@ -395,7 +421,10 @@ class _Schedule:
         return self._g[o:o + n].view(shp)
 
     def seed(self, site):
-        return _mix(self.base_seed, site) if self.train else 0
+        if not self.train:
+            return 0
+        # graph-replayable mode (graph.py): the kernels mix the site with the device base word
+        return site if self.device_seeds else _mix(self.base_seed, site)
 
     # ---- forward ----
     def forward(self, save):
@@ -608,4 +637,4 @@ class _ModelFunction(torch.autograd.Function):
 
     @staticmethod
     def _nparams(run):
-        return sum(1 for n, _ in run.m.named_parameters() if not n.startswith("reg_head."))
+        return len(run.m._trained_params)

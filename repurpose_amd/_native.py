@@ -91,6 +91,9 @@ _SIGNATURES = {
     "rp_rowdot_bwd_dx": (c_i, [c_vp, c_i64, c_i64, c_i, c_vp, c_i, c_vp, c_i, c_i64, c_f, c_vp, c_i,
                                c_i64, c_vp]),
     "rp_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_f, c_f, c_f, c_i, c_vp, c_vp]),
+    "rp_adam_coefficients": (c_i, [c_f, c_f, c_f, c_f, c_f, c_i, c_vp]),
+    "rp_adam_step_dev": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "rp_set_seed_base": (c_i, [c_vp]),
     "rp_infer_select": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_f, c_i, c_f, c_f, c_vp, c_vp, c_vp, c_vp,
                               c_vp]),
     "rp_softnms_workspace": (c_i64, [c_i, c_i]),

@@ -78,6 +78,7 @@ struct MhaDev {
   int B, Tq, Tk, H;
   float scale;
   uint32_t drop_thresh; float drop_scale; uint32_t seed;
+  const uint32_t* seed_base;  // graph-replayable dropout (rp_set_seed_base), or null
   void* out; int64_t ldo;
   void* out_lo;  // bf16: O - bf16(O) rounded to bf16 (same layout as out), or null
   float* lse;
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   const T* Kg = (const T*)a.k + (int64_t)b * Tk * ldk + h * HD;
   const T* Vg = (const T*)a.v + (int64_t)b * Tk * ldv + h * HD;
   const int q0 = qb * QB + w * 16 * QT;  // this wave's first query
-  const uint32_t seed_bh = rp_hash(a.seed, (uint32_t)bh);
+  const uint32_t seed_bh = rp_hash(rp_seed_eff(a.seed_base, a.seed), (uint32_t)bh);
   const float c = scale * LOG2E;
   const int KT = mask_kt(Tk);
   const int64_t ldm = mask_ld(Tq);
@@ -1634,6 +1635,7 @@ int make_dev(const char* fn, int dtype, int qpre, const rp_mha_args* p, int phas
   a.q = p->q; a.k = p->k; a.v = p->v; a.ldq = p->ldq; a.ldk = p->ldk; a.ldv = p->ldv;
   a.kvalid = p->key_valid; a.B = p->B; a.Tq = p->Tq; a.Tk = p->Tk; a.H = p->H; a.scale = p->scale;
   a.drop_thresh = thr; a.drop_scale = p->dropout_p > 0.f ? 1.f / (1.f - p->dropout_p) : 1.f; a.seed = p->seed;
+  a.seed_base = thr ? g_rp_seed_base : nullptr;
   a.out = p->out; a.ldo = p->ldo; a.lse = p->lse; a.dmask = thr ? p->dropmask : nullptr;
   a.out_lo = dtype == RP_BF16 ? p->out_lo : nullptr;
   a.empty_uniform = p->empty_rows_uniform != 0;

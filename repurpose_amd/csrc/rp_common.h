@@ -92,6 +92,15 @@ __device__ __forceinline__ uint32_t rp_keep_bits(uint32_t seed, uint32_t idx0, u
   }
 }
 
+// Graph-replayable dropout streams (rp_set_seed_base): while the process-wide base pointer is set,
+// launchers copy it into their kernel arguments and the kernels draw with rp_hash(*base, seed), the
+// base word read on the device when the kernel runs (a captured HIP graph replays with whatever the
+// host last wrote there); with no base the seed argument is used as is.
+extern const uint32_t* g_rp_seed_base;
+__device__ __forceinline__ uint32_t rp_seed_eff(const uint32_t* base, uint32_t seed) {
+  return base ? rp_hash(*base, seed) : seed;
+}
+
 static inline uint32_t rp_dropout_thresh(float p) {
   if (p <= 0.f) return 0u;
   double t = (double)p * 65536.0 + 0.5;

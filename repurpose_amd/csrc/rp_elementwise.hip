@@ -246,18 +246,51 @@ __global__ void rowdot_bwd_kernel(const float* __restrict__ dout, int64_t ldd, i
 }
 
 // ---------------------------------------------------------------- Adam ---------------------
+// coef = {lr / bc1, beta1, beta2, eps, weight_decay, sqrt(bc2)} (rp_adam_coefficients)
+__device__ __forceinline__ void adam_elem(float& pi, float gi, float& mi, float& vi, const float (&c)[6]) {
+  if (c[4] != 0.f) gi = gi + c[4] * pi;
+  mi = mi + (1.f - c[1]) * (gi - mi);
+  vi = vi * c[2] + (1.f - c[2]) * gi * gi;
+  const float denom = sqrtf(vi) / c[5] + c[3];
+  pi = pi - c[0] * (mi / denom);
+}
+
+// 4 elements per thread (16-byte loads/stores); scalar tail.  DEV: the coefficients are read from
+// device memory when the kernel runs (graph replay), else taken from the arguments.
+template <bool DEV>
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, int64_t n, float lr_bc1, float beta1, float beta2, float eps,
-                            float wd, float sqrt_bc2, bf16* __restrict__ plp) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float pi = p[i];
-    float gi = g[i];
-    if (wd != 0.f) gi = gi + wd * pi;
-    float mi = m[i];
-    mi = mi + (1.f - beta1) * (gi - mi);
-    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
-    const float denom = sqrtf(vi) / sqrt_bc2 + eps;
-    pi = pi - lr_bc1 * (mi / denom);
+                            float* __restrict__ v, int64_t n, int vec, const float* __restrict__ coef_dev, float c0, float c1,
+                            float c2, float c3, float c4, float c5, bf16* __restrict__ plp) {
+  float c[6];
+  if (DEV) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) c[i] = coef_dev[i];
+  } else {
+    c[0] = c0; c[1] = c1; c[2] = c2; c[3] = c3; c[4] = c4; c[5] = c5;
+  }
+  const int64_t n4 = vec ? n / 4 : 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_elem(pp.x, gg.x, mm.x, vv.x, c);
+    adam_elem(pp.y, gg.y, mm.y, vv.y, c);
+    adam_elem(pp.z, gg.z, mm.z, vv.z, c);
+    adam_elem(pp.w, gg.w, mm.w, vv.w, c);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (plp) {
+      typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+      bf16x4v o = {(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
+      reinterpret_cast<bf16x4v*>(plp)[i] = o;
+    }
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    adam_elem(pi, g[i], mi, vi, c);
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
@@ -415,18 +448,51 @@ extern "C" int rp_rowdot_bwd_dx(const float* dout, int64_t ldd, int64_t rows, in
   return rp_check_launch("rp_rowdot_bwd_dx");
 }
 
+extern "C" int rp_adam_coefficients(float lr, float beta1, float beta2, float eps, float weight_decay, int step,
+                                    float* coef) {
+  RP_REQUIRE(step >= 1 && coef, "rp_adam_coefficients: bad step / null output");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  coef[0] = (float)(lr / bc1);
+  coef[1] = beta1;
+  coef[2] = beta2;
+  coef[3] = eps;
+  coef[4] = weight_decay;
+  coef[5] = (float)sqrt(bc2);
+  return RP_OK;
+}
+
+static int adam_launch(float* p, const float* g, float* m, float* v, int64_t n, const float* coef_dev,
+                       const float* c, void* p_lp, void* stream) {
+  if (n == 0) return RP_OK;
+  RP_REQUIRE(p && g && m && v, "rp_adam_step: null");
+  // 16-byte vectors when every operand allows them, else the scalar loop covers everything
+  const int vec = rp_aligned16(p) && rp_aligned16(g) && rp_aligned16(m) && rp_aligned16(v) &&
+                  (!p_lp || (((uintptr_t)p_lp) & 7u) == 0);
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  if (coef_dev)
+    hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, vec,
+                       coef_dev, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, (bf16*)p_lp);
+  else
+    hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, vec,
+                       nullptr, c[0], c[1], c[2], c[3], c[4], c[5], (bf16*)p_lp);
+  return rp_check_launch("rp_adam_step");
+}
+
 extern "C" int rp_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                             float eps, float weight_decay, int step, void* p_lp, void* stream) {
   RP_REQUIRE(n >= 0 && step >= 1, "rp_adam_step: bad n/step");
-  if (n == 0) return RP_OK;
-  RP_REQUIRE(p && g && m && v, "rp_adam_step: null");
-  const double bc1 = 1.0 - pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - pow((double)beta2, (double)step);
-  const float lr_bc1 = (float)(lr / bc1);
-  const float sqrt_bc2 = (float)sqrt(bc2);
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr_bc1, beta1,
-                     beta2, eps, weight_decay, sqrt_bc2, (bf16*)p_lp);
-  return rp_check_launch("rp_adam_step");
+  float c[6];
+  rp_adam_coefficients(lr, beta1, beta2, eps, weight_decay, step, c);
+  return adam_launch(p, g, m, v, n, nullptr, c, p_lp, stream);
+}
+
+extern "C" int rp_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* coef_dev,
+                                void* p_lp, void* stream) {
+  RP_REQUIRE(n >= 0 && coef_dev, "rp_adam_step_dev: bad n / null coef");
+  return adam_launch(p, g, m, v, n, coef_dev, nullptr, p_lp, stream);
 }
 
 extern "C" int rp_pad_rows(const void* src, int src_dtype, const int64_t* row_offsets, int B, int T, int D, float pad,

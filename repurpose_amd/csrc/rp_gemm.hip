@@ -39,6 +39,7 @@ struct EpiDev {
   uint32_t drop_thresh;
   float drop_scale;
   uint32_t drop_seed;
+  const uint32_t* seed_base;  // graph-replayable dropout (rp_set_seed_base), or null
   const float* residual;
   int64_t ldr;
   const void* gate;
@@ -219,6 +220,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* ld
   constexpr int OV = 16 / (int)sizeof(TC);
   constexpr int CPRO = BN / OV;
   TC* Cbase = Cout + (MODE == 1 ? (int64_t)split * M * ldc : 0);
+  const uint32_t dseed = (MODE == 0 && ep.drop_thresh) ? rp_seed_eff(ep.seed_base, ep.drop_seed) : 0u;
   constexpr int NH = HALVES ? 2 : 1;  // staging passes
   constexpr int HR = BM / NH;          // rows per pass
 #pragma unroll 1
@@ -262,7 +264,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* ld
         for (int e = 0; e < OV; ++e) v[e] = fmaxf(v[e], 0.f);
       }
       if (ep.drop_thresh) {
-        const uint32_t kb = rp_keep_bits<OV>(ep.drop_seed, (uint32_t)(m * N + n), ep.drop_thresh);
+        const uint32_t kb = rp_keep_bits<OV>(dseed, (uint32_t)(m * N + n), ep.drop_thresh);
 #pragma unroll
         for (int e = 0; e < OV; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * ep.drop_scale : 0.f;
       }
@@ -651,6 +653,7 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
   constexpr int OV = 16 / (int)sizeof(TC);
   constexpr int CPRO = BNT / OV;
   TC* Cbase = Cout + (MODE == 1 ? (int64_t)split * M * ldc : 0);
+  const uint32_t dseed = (MODE == 0 && ep.drop_thresh) ? rp_seed_eff(ep.seed_base, ep.drop_seed) : 0u;
   const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
@@ -692,7 +695,7 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
           for (int e = 0; e < OV; ++e) v[e] = fmaxf(v[e], 0.f);
         }
         if (ep.drop_thresh) {
-          const uint32_t kb = rp_keep_bits<OV>(ep.drop_seed, (uint32_t)(m * N + n), ep.drop_thresh);
+          const uint32_t kb = rp_keep_bits<OV>(dseed, (uint32_t)(m * N + n), ep.drop_thresh);
 #pragma unroll
           for (int e = 0; e < OV; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * ep.drop_scale : 0.f;
         }
@@ -1179,6 +1182,7 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
     e.drop_thresh = rp_dropout_thresh(ep->dropout_p);
     e.drop_scale = ep->dropout_p > 0.f ? 1.f / (1.f - ep->dropout_p) : 1.f;
     e.drop_seed = ep->dropout_seed;
+    e.seed_base = e.drop_thresh ? g_rp_seed_base : nullptr;
     e.residual = ep->residual;
     e.ldr = ep->ldr;
     e.gate = ep->gate;

@@ -93,6 +93,7 @@ struct LnFwdDev {
   const float* gamma; const float* beta; float eps;
   const float* pe; int64_t pe_period;
   int relu; uint32_t drop_thresh; float drop_scale; uint32_t drop_seed;
+  const uint32_t* seed_base;  // graph-replayable dropout (rp_set_seed_base), or null
   float* out_f32; int64_t ld_out_f32;
   void* out_lp; int out_lp_dtype; int64_t ld_out_lp;
   float* mean; float* rstd;
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(64 * LN_WAVES) void ln_fwd_kernel(int64_t rows, LnF
   }
   const float var = rp_wave_sum(q) * (1.f / D);
   const float rstd = rsqrtf(var + a.eps);
-  const uint32_t kb = a.drop_thresh ? rp_keep_bits<VPT>(a.drop_seed, (uint32_t)(row * D + c0), a.drop_thresh) : 0u;
+  const uint32_t kb = a.drop_thresh ? rp_keep_bits<VPT>(rp_seed_eff(a.seed_base, a.drop_seed), (uint32_t)(row * D + c0), a.drop_thresh) : 0u;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     float y = (v[i] - mean) * rstd * gm[i] + bt[i];
@@ -150,6 +151,7 @@ struct LnBwdDev {
   float* dx; int64_t lddx;
   void* dx_lp; int dx_lp_dtype; int64_t lddx_lp;
   uint32_t lp_thresh; float lp_scale; uint32_t lp_seed;
+  const uint32_t* seed_base;  // graph-replayable dropout (rp_set_seed_base), or null
   float* dgamma_part; float* dbeta_part; int64_t ld_part;
 };
 
@@ -163,6 +165,8 @@ __global__ __launch_bounds__(64 * LNB_WAVES) void ln_bwd_kernel(int64_t rows, Ln
   for (int i = 0; i < VPT; ++i) pg[i] = pb[i] = 0.f;
   float gam[VPT];
   load_row<VPT>(gam, a.gamma, RP_F32, c0);
+  const uint32_t dseed = a.drop_thresh ? rp_seed_eff(a.seed_base, a.drop_seed) : 0u;
+  const uint32_t lseed = a.lp_thresh ? rp_seed_eff(a.seed_base, a.lp_seed) : 0u;
 
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS_PER_BLOCK;
   for (int rr = w; rr < LN_ROWS_PER_BLOCK; rr += LNB_WAVES) {
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(64 * LNB_WAVES) void ln_bwd_kernel(int64_t rows, Ln
     float yv[VPT];
     if (a.y) load_row<VPT>(yv, a.y, a.y_dtype, row * a.ldy + c0);
     if (a.drop_thresh) {
-      const uint32_t kb = rp_keep_bits<VPT>(a.drop_seed, (uint32_t)(row * D + c0), a.drop_thresh);
+      const uint32_t kb = rp_keep_bits<VPT>(dseed, (uint32_t)(row * D + c0), a.drop_thresh);
 #pragma unroll
       for (int i = 0; i < VPT; ++i) g[i] = ((kb >> i) & 1u) ? g[i] * a.drop_scale : 0.f;
     }
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(64 * LNB_WAVES) void ln_bwd_kernel(int64_t rows, Ln
     if (a.dx) store_row<VPT>(dx, a.dx, RP_F32, row * a.lddx + c0);
     if (a.dx_lp) {
       if (a.lp_thresh) {
-        const uint32_t kb = rp_keep_bits<VPT>(a.lp_seed, (uint32_t)(row * D + c0), a.lp_thresh);
+        const uint32_t kb = rp_keep_bits<VPT>(lseed, (uint32_t)(row * D + c0), a.lp_thresh);
 #pragma unroll
         for (int i = 0; i < VPT; ++i) dx[i] = ((kb >> i) & 1u) ? dx[i] * a.lp_scale : 0.f;
       }
@@ -265,6 +269,7 @@ extern "C" int rp_layernorm_fwd(int64_t rows, int64_t D, const rp_ln_fwd_args* p
   a.drop_thresh = rp_dropout_thresh(p->dropout_p);
   a.drop_scale = p->dropout_p > 0.f ? 1.f / (1.f - p->dropout_p) : 1.f;
   a.drop_seed = p->dropout_seed;
+  a.seed_base = a.drop_thresh ? g_rp_seed_base : nullptr;
   a.out_f32 = p->out_f32; a.ld_out_f32 = p->ld_out_f32;
   a.out_lp = p->out_lp; a.out_lp_dtype = p->out_lp_dtype; a.ld_out_lp = p->ld_out_lp;
   a.mean = p->mean; a.rstd = p->rstd;
@@ -293,6 +298,7 @@ extern "C" int rp_layernorm_bwd(int64_t rows, int64_t D, const rp_ln_bwd_args* p
   a.lp_thresh = rp_dropout_thresh(p->dx_lp_dropout_p);
   a.lp_scale = p->dx_lp_dropout_p > 0.f ? 1.f / (1.f - p->dx_lp_dropout_p) : 1.f;
   a.lp_seed = p->dx_lp_seed;
+  a.seed_base = (a.drop_thresh || a.lp_thresh) ? g_rp_seed_base : nullptr;
   a.dgamma_part = p->dgamma_part; a.dbeta_part = p->dbeta_part;
   a.ld_part = p->ld_part ? p->ld_part : D;
   RP_REQUIRE(a.ld_part >= D, "rp_layernorm_bwd: ld_part < D");

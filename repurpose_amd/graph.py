@@ -1,0 +1,121 @@
+"""The training step captured once as a HIP graph and replayed (MI355X launch-overhead removal).
+
+One eager step of the reference trainer (``main.py:331-369``: ``optimizer.zero_grad()``,
+``model(batch)``, ``model.losses(...)``, ``loss.backward()``, ``optimizer.step()``) is ~450 kernel
+launches from Python.  ``CapturedTrainStep`` records exactly that sequence once with
+``torch.cuda.graph`` (hipStreamBeginCapture under the hood: every rp_* launch goes to torch's
+current stream, which is the capture stream) and replays it with one ``hipGraphLaunch`` per step.
+
+What changes per step without re-capture lives in one small device block that the host rewrites
+(pinned staging slot -> async H2D on the step's stream) before each replay:
+
+* word 0 — the dropout base (``rp_set_seed_base``): every dropout launch of the captured step
+  draws with ``rp_hash(base, site)``, so each replay has fresh dropout streams;
+* words 1..6 — the Adam coefficients ``rp_adam_coefficients(lr, betas, eps, wd, step)``
+  (``rp_adam_step_dev``), computed on the host from the optimizer's current ``param_groups`` and
+  step count, so LR schedulers and the bias correction behave exactly as in eager mode (the
+  updates are bitwise those of ``rp_adam_step`` with the same coefficients).
+
+The batch tensors given at construction are the graph's static inputs: ``load(batch)`` copies a new
+batch of the same shape into them.  Requirements: a ``FusedAdam`` optimizer, one device, no
+gradient all-reduce hooks inside the captured region (the DP path keeps the eager step).
+"""
+import numpy as np
+import torch
+
+from . import kernels as K
+from .optim import FusedAdam
+
+_SLOTS = 4  # pinned staging slots: the host runs at most this many steps ahead of the device
+
+
+class CapturedTrainStep:
+    def __init__(self, model, optimizer, batch, loss_fn=None, warmup=2, seed=None):
+        if not isinstance(optimizer, FusedAdam):
+            raise TypeError("CapturedTrainStep needs repurpose_amd.optim.FusedAdam (device-side coefficients)")
+        if model._grad_ready_hooks or model._grad_done_hooks:
+            raise RuntimeError("CapturedTrainStep: gradient all-reduce hooks are registered; the DP step stays "
+                               "eager (collectives are not captured)")
+        self.model, self.opt = model, optimizer
+        self.batch = batch
+        self.loss_fn = loss_fn or (lambda m, out: m.losses(*out)["cls_loss"] / out[1].shape[0])
+        self.warmup = int(warmup)
+        dev = model.flat_params().device
+        self.device = dev
+        self._dev = torch.zeros(8, device=dev, dtype=torch.int32)  # [seed, coef0..5, pad]
+        self._coef = self._dev[1:7].view(torch.float32)
+        self._host = [torch.zeros(8, dtype=torch.int32).pin_memory() for _ in range(_SLOTS)]
+        self._ev = [None] * _SLOTS
+        self._rng = np.random.default_rng(seed)
+        self._graph = None
+        self._loss = None
+        self.steps = 0
+
+    def load(self, batch):
+        """Copy a batch of the captured shapes into the static input tensors."""
+        for k, v in batch.items():
+            dst = self.batch.get(k)
+            if isinstance(dst, torch.Tensor):
+                if dst.shape != v.shape:
+                    raise ValueError(f"CapturedTrainStep.load: {k} shape {tuple(v.shape)} != captured {tuple(dst.shape)}")
+                dst.copy_(v, non_blocking=True)
+
+    def _eager(self):
+        self.opt.zero_grad()
+        out = self.model(self.batch)
+        loss = self.loss_fn(self.model, out)
+        loss.backward()
+        self.opt.step()
+        return loss
+
+    def _stage(self, stream):
+        """Write this step's seed and Adam coefficients and enqueue their upload on ``stream``."""
+        i = self.steps % _SLOTS
+        if self._ev[i] is not None:
+            self._ev[i].synchronize()  # the slot's previous upload has been consumed
+        grp = self.opt.param_groups[0]
+        b1, b2 = grp["betas"]
+        coef = K.adam_coefficients(grp["lr"], b1, b2, grp["eps"], grp["weight_decay"], self.opt._step + 1)
+        h = self._host[i].numpy()
+        h[0] = np.int32(np.uint32(self._rng.integers(0, 2 ** 32)).view(np.int32))
+        h[1:7] = np.asarray(coef, dtype=np.float32).view(np.int32)
+        with torch.cuda.stream(stream):
+            self._dev.copy_(self._host[i], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self._ev[i] = ev
+
+    def _capture(self):
+        stream = torch.cuda.current_stream(self.device)
+        self._stage(stream)
+        g = torch.cuda.CUDAGraph()
+        K.set_seed_base(self._dev[0:1])
+        self.opt._coef_dev = self._coef
+        step0 = self.opt._step
+        try:
+            # the pool is private to the graph; the eager warm-up steps ran on the caller's stream
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.graph(g):
+                self._loss = self._eager()
+        finally:
+            K.set_seed_base(None)
+            self.opt._coef_dev = None
+        self.opt._step = step0  # capture executed nothing; replay() counts the step
+        self._graph = g
+
+    def step(self):
+        """One training step (eager for the first ``warmup`` calls, then graph replays); returns the
+        loss tensor of this step (device scalar, valid until the next step)."""
+        if self.steps < self.warmup:
+            self.steps += 1
+            return self._eager()
+        if self._graph is None:
+            self._capture()
+        else:
+            self._stage(torch.cuda.current_stream(self.device))
+        self._graph.replay()
+        self.opt._step += 1
+        if self.opt._step_t is not None:
+            self.opt._step_t.fill_(float(self.opt._step))
+        self.steps += 1
+        return self._loss

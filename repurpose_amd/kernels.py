@@ -418,10 +418,42 @@ def rowdot_bwd_dx(dout, W, gate=None, gate_scale=1.0, out_dtype=torch.float32):
 
 
 # ------------------------------------------------------------------------------------- optimizer
-def adam_step(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, p_lp=None):
-    _gpu(p, g, m, v, p_lp)
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, p_lp=None, coef_dev=None):
+    """One Adam update; with ``coef_dev`` (fp32 device tensor of 6, see ``adam_coefficients``) the
+    kernel reads its coefficients from device memory when it runs (graph replay) and the host
+    hyper-parameters are not used."""
+    _gpu(p, g, m, v, p_lp, coef_dev)
+    if coef_dev is not None:
+        N.call("rp_adam_step_dev", _p(p), _p(g), _p(m), _p(v), p.numel(), _p(coef_dev), _p(p_lp), _stream(p))
+        return
     N.call("rp_adam_step", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
            float(eps), float(weight_decay), int(step), _p(p_lp), _stream(p))
+
+
+def adam_coefficients(lr, beta1, beta2, eps, weight_decay, step):
+    """The six fp32 kernel coefficients of an Adam step (computed by the library, as rp_adam_step does)."""
+    buf = (ctypes.c_float * 6)()
+    N.call("rp_adam_coefficients", float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(step),
+           ctypes.cast(buf, ctypes.c_void_p))
+    return list(buf)
+
+
+_seed_base = {"t": None}
+
+
+def set_seed_base(t):
+    """Graph-replayable dropout (rp_set_seed_base): while ``t`` (a uint32/int32 device word) is set,
+    dropout launches draw with rp_hash(*t, seed) read when the kernel runs; None restores plain seeds."""
+    if t is not None:
+        _gpu(t)
+        if t.dtype not in (torch.int32, torch.uint32) or t.numel() < 1:
+            raise TypeError("set_seed_base: needs an int32 device word")
+    N.call("rp_set_seed_base", _p(t))
+    _seed_base["t"] = t
+
+
+def seed_base_active():
+    return _seed_base["t"] is not None
 
 
 # ------------------------------------------------------------------------------------- inference

@@ -65,6 +65,7 @@ class FusedAdam(torch.optim.Optimizer):
         self._v = None
         self._step = 0
         self._step_t = None  # one shared CPU step tensor referenced by every trained param's state
+        self._coef_dev = None  # graph capture (graph.py): coefficients read from this device buffer
 
     # ---------------------------------------------------------------- state <-> flat moments
     def _trained(self):
@@ -146,7 +147,7 @@ class FusedAdam(torch.optim.Optimizer):
         if model.compute_dtype == torch.bfloat16:
             lp = model.lowp_weights()[:n]  # refreshes a stale copy first (e.g. after load_state_dict)
         K.adam_step(flat[:n], g[:n], self._m, self._v, grp["lr"], b1, b2, grp["eps"], grp["weight_decay"],
-                    self._step, p_lp=lp)
+                    self._step, p_lp=lp, coef_dev=self._coef_dev)
         if lp is not None:
             model.mark_lowp_fresh()
         return loss

@@ -1,0 +1,90 @@
+"""The captured training step (repurpose_amd/graph.py): a HIP-graph replay is the eager step.
+
+* with dropout off, N replays give bitwise the parameters, moments and losses of N eager steps
+  (same kernels; Adam reads the same coefficients from the device block), including new batches
+  copied in with load() and an LR change between steps (LR schedulers keep working);
+* with dropout on, every replay draws a fresh stream (device seed word rewritten per step), and two
+  runners with the same seed reproduce each other bit for bit.
+"""
+import numpy as np
+import pytest
+import torch
+
+from repurpose_amd.graph import CapturedTrainStep
+from repurpose_amd.MMCTransformer import MMCTransformer
+from repurpose_amd.optim import FusedAdam
+
+from .test_model_gpu import TRI, make_batch, to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(dev, dtype, dropout):
+    torch.manual_seed(0)
+    m = MMCTransformer(**TRI, compute_dtype=dtype).to(dev).train()
+    m.DROPOUT = dropout
+    return m, FusedAdam(m, lr=1e-3, weight_decay=1e-4)
+
+
+def _batches(dev, n, B=2, T=192):
+    return [{k: v for k, v in to_dev(make_batch(TRI, B, T, [T, 150], seed=20 + i), dev).items() if torch.is_tensor(v)}
+            for i in range(n)]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_replay_equals_eager_without_dropout(dev, dtype):
+    batches = _batches(dev, 5)
+    me, oe = _model(dev, dtype, 0.0)
+    eager_losses = []
+    for i, b in enumerate(batches):
+        if i == 3:
+            oe.param_groups[0]["lr"] = 5e-4
+        oe.zero_grad()
+        out = me(b)
+        loss = me.losses(*out)["cls_loss"] / 2
+        loss.backward()
+        oe.step()
+        eager_losses.append(loss.item())
+
+    mg, og = _model(dev, dtype, 0.0)
+    static = {k: v.clone() for k, v in batches[0].items()}
+    run = CapturedTrainStep(mg, og, static, warmup=1)
+    graph_losses = []
+    for i, b in enumerate(batches):
+        if i == 3:
+            og.param_groups[0]["lr"] = 5e-4
+        run.load(b)
+        graph_losses.append(run.step().item())
+    torch.cuda.synchronize()
+    assert run._graph is not None
+    assert graph_losses == eager_losses
+    n = me.trainable_numel()
+    assert torch.equal(mg.flat_params()[:n], me.flat_params()[:n])
+    assert torch.equal(og._m, oe._m) and torch.equal(og._v, oe._v)
+    assert og._step == oe._step == 5
+    if dtype == "bf16":
+        assert torch.equal(mg._lp[:n], mg.flat_params()[:n].to(torch.bfloat16))
+    # torch-Adam-layout state follows the replays
+    assert float(og.state_dict()["state"][0]["step"]) == 5.0
+
+
+def test_replays_draw_fresh_dropout_and_are_reproducible(dev):
+    b = _batches(dev, 1)[0]
+
+    def losses(seed, lr):
+        m, o = _model(dev, "bf16", 0.1)
+        o.param_groups[0]["lr"] = lr
+        run = CapturedTrainStep(m, o, {k: v.clone() for k, v in b.items()}, warmup=1, seed=seed)
+        out = [run.step().item() for _ in range(5)]
+        torch.cuda.synchronize()
+        return out, m.flat_params().clone()
+
+    frozen, p0 = losses(7, 0.0)  # lr 0 (no weight decay effect: lr scales the whole update)
+    # weights frozen: replays 2..5 differ only through their dropout streams
+    assert len(set(frozen[1:])) == 4, frozen
+    again, p1 = losses(7, 0.0)
+    assert again == frozen and torch.equal(p0, p1)
+    other, _ = losses(8, 0.0)
+    assert other[1:] != frozen[1:]
+    trained, _ = losses(7, 1e-3)
+    assert all(np.isfinite(trained))
