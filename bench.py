@@ -9,8 +9,10 @@ softmax and accumulators), dropout 0.1 active.  One step = forward + losses + ba
 all-reduce over RCCL (N > 1) + fused Adam (lr 1e-3, weight decay 1e-4).  Synthetic seeded inputs
 with the feature statistics of SURVEY §8d, random-init weights (seed 1234); inputs resident in HBM.
 
-Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel's achieved MFMA rate measured
-live with HIP events on the launch stream during the timed steps; `cpu_baseline` is the oracle
+Prints ONE JSON line (rank 0).  On one GPU the timed steps replay the step captured as a HIP graph
+(repurpose_amd/graph.py; the DP path, N > 1, runs eager).  `roofline` is the dominant kernel's
+achieved MFMA rate measured with HIP events on its launch stream over eager steps of the same
+workload right after the timed region; `cpu_baseline` is the oracle
 (stock torch CPU modules, fp32, the reference's own arithmetic) timed on this host.
 """
 import argparse
@@ -204,8 +206,6 @@ def main():
     for _ in range(max(args.warmup, 2 if use_graph else 0)):
         step()
     torch.cuda.synchronize()
-    if not use_graph:
-        K.timer_start(*KERNEL_FLOPS, "gemm_wgrad")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -217,15 +217,13 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     loss_val = float(loss.item())
-    if use_graph:
-        # a replay carries no per-launch events: the same kernels on the same data, timed with HIP
-        # events on their launch stream over eager steps right after the timed region
-        K.timer_start(*KERNEL_FLOPS, "gemm_wgrad")
-        for _ in range(min(args.steps, 5)):
-            eager_step()
-        kern_steps = min(args.steps, 5)
-    else:
-        kern_steps = args.steps
+    # per-kernel durations: the same kernels on the same data, timed with HIP events on their launch
+    # stream over eager steps right after the timed region (a graph replay carries no per-launch
+    # events, and ~100 event pairs per eager step would themselves add ~0.6 ms to the timed steps)
+    kern_steps = min(args.steps, 5)
+    K.timer_start(*KERNEL_FLOPS, "gemm_wgrad")
+    for _ in range(kern_steps):
+        eager_step()
     kern = K.timer_stop(detail=True)
     kern_ms = {n: v[0] for n, v in kern.items()}
     if world > 1:
@@ -278,8 +276,7 @@ def main():
                           "seq_len": T, "parallelism": f"dp{world}"},
                "loss": loss_val, "roofline": roof,
                "execution": "hip-graph replay of the captured step" if use_graph else "eager (per-launch)"}
-        roof["kernel_timing"] = ("HIP events on the launch stream over %d eager steps after the timed graph "
-                                 "replays" % kern_steps) if use_graph else "HIP events on the launch stream over the timed steps"
+        roof["kernel_timing"] = "HIP events on the launch stream over %d eager steps after the timed region" % kern_steps
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(T)
             res["speedup_vs_cpu"] = value / res["cpu_baseline"]["value"]

@@ -44,6 +44,11 @@ class LnBwdArgs(ctypes.Structure):
                 ("ld_part", c_i64)]
 
 
+class WgradItem(ctypes.Structure):
+    _fields_ = [("dY", c_vp), ("X", c_vp), ("dW", c_vp), ("db", c_vp), ("M", c_i64), ("N", c_i64), ("ldy", c_i64),
+                ("ldx", c_i64)]
+
+
 class MhaArgs(ctypes.Structure):
     _fields_ = [("q", c_vp), ("ldq", c_i64), ("k", c_vp), ("ldk", c_i64), ("v", c_vp), ("ldv", c_i64),
                 ("key_valid", c_vp), ("B", c_i), ("Tq", c_i), ("Tk", c_i), ("H", c_i), ("head_dim", c_i),
@@ -63,6 +68,7 @@ _SIGNATURES = {
                       c_f, ctypes.POINTER(GemmEpilogue), c_vp]),
     "rp_gemm_wgrad_workspace": (c_i64, [c_i64, c_i64, c_i64]),
     "rp_gemm_wgrad": (c_i, [c_i, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i, c_vp, c_i64, c_vp]),
+    "rp_gemm_wgrad_grouped": (c_i, [c_i64, c_vp, c_i, c_i, c_vp]),
     "rp_layernorm_fwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnFwdArgs), c_vp]),
     "rp_layernorm_bwd_blocks": (c_i64, [c_i64]),
     "rp_layernorm_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnBwdArgs), c_vp]),

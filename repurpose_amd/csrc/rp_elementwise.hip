@@ -470,7 +470,7 @@ static int adam_launch(float* p, const float* g, float* m, float* v, int64_t n, 
   const int vec = rp_aligned16(p) && rp_aligned16(g) && rp_aligned16(m) && rp_aligned16(v) &&
                   (!p_lp || (((uintptr_t)p_lp) & 7u) == 0);
   int64_t blocks = (n / 4 + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > 65536) blocks = 65536;
   if (blocks < 1) blocks = 1;
   if (coef_dev)
     hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, vec,

@@ -490,39 +490,16 @@ __device__ __forceinline__ bf16x8 frag_m_swz(const char* t, int rbase, int kbase
   return r;
 }
 
-template <bool AK, bool BKM, typename TC, int MODE, int CFG>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t N, int64_t K,
-                                                              const bf16* __restrict__ A, int64_t lda,
-                                                              const bf16* __restrict__ B, int64_t ldb,
-                                                              TC* __restrict__ Cout, int64_t ldc, float alpha,
-                                                              EpiDev ep, int64_t kchunk, float* __restrict__ bslab) {
+// main loop of the 128 x 128 LDS-DMA tile over the K range [kbeg, kend) (whole BK steps): acc gets
+// the tile's products; with want_bias, bacc the column sums of the staged m-major A tiles
+template <bool AK, bool BKM, int CFG>
+__device__ __forceinline__ void dma_mainloop(const bf16* __restrict__ A, int64_t lda, int64_t M,
+                                             const bf16* __restrict__ B, int64_t ldb, int64_t N, int64_t m0,
+                                             int64_t n0, int64_t kbeg, int64_t kend, bool want_bias,
+                                             f32x4 (&acc)[4][4], float (&bacc)[8], char* lds, int tid, int lane,
+                                             int wid, int wm, int wn) {
   using D = DmaCfg<CFG>;
   constexpr int BK = D::BK, GT = D::GT;
-  __shared__ __attribute__((aligned(16))) char lds[D::LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
-  const int tiles_n = (int)((N + BN - 1) / BN);
-  const int tiles_m = (int)((M + BM - 1) / BM);
-  int t, split;
-  tile_split<MODE>(tiles_m * tiles_n, ep.split_major, t, split);
-  const int64_t m0 = (int64_t)(t / tiles_n) * BM;
-  const int64_t n0 = (int64_t)(t % tiles_n) * BN;
-  int64_t kbeg = 0, kend = K;
-  if (MODE == 1) {
-    kbeg = (int64_t)split * kchunk;
-    kend = kbeg + kchunk < K ? kbeg + kchunk : K;
-  }
-  const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bacc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
-
   const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
   if (D::STAGES == 2 && nk > 0) {
     glds_tile<AK, BK>(A, lda, M, m0, kbeg, lds, wid, lane);
@@ -571,8 +548,109 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
     if (D::STAGES == 2) __syncthreads();
   }
   if (D::STAGES == 1) __syncthreads();
+}
+
+template <bool AK, bool BKM, typename TC, int MODE, int CFG>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t N, int64_t K,
+                                                              const bf16* __restrict__ A, int64_t lda,
+                                                              const bf16* __restrict__ B, int64_t ldb,
+                                                              TC* __restrict__ Cout, int64_t ldc, float alpha,
+                                                              EpiDev ep, int64_t kchunk, float* __restrict__ bslab) {
+  using D = DmaCfg<CFG>;
+  __shared__ __attribute__((aligned(16))) char lds[D::LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (int)((N + BN - 1) / BN);
+  const int tiles_m = (int)((M + BM - 1) / BM);
+  int t, split;
+  tile_split<MODE>(tiles_m * tiles_n, ep.split_major, t, split);
+  const int64_t m0 = (int64_t)(t / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(t % tiles_n) * BN;
+  int64_t kbeg = 0, kend = K;
+  if (MODE == 1) {
+    kbeg = (int64_t)split * kchunk;
+    kend = kbeg + kchunk < K ? kbeg + kchunk : K;
+  }
+  const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  dma_mainloop<AK, BKM, CFG>(A, lda, M, B, ldb, N, m0, n0, kbeg, kend, want_bias, acc, bacc, lds, tid, lane, wid, wm,
+                             wn);
   gemm_epilogue<TC, MODE, D::HALVES>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
   if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab, split);
+}
+
+// ============ grouped weight gradients: many (dY, X) pairs over the same token range ============
+// One launch computes up to WG_MAX weight gradients dW_i = dY_i^T X_i (+ db_i = colsum dY_i) that
+// share the token count K, every 128 x 128 output tile over the WHOLE K range (no split-K slabs,
+// no reduce pass).  The deferred per-layer weight gradients of the encoder (16 layers x {linear2,
+// linear1, out_proj, in_proj} = 192 tiles per layer, 8 layers per launch = 1536 tiles = exactly
+// three waves at two workgroups per CU) are the intended use: the XCD remap deals each XCD 192
+// consecutive tiles, i.e. one layer, whose operand panels its L2 then shares.
+constexpr int WG_MAX = 32;
+struct WgItem {
+  const bf16* dY;
+  const bf16* X;
+  float* dW;
+  float* db;
+  int M, N, ldy, ldx;
+};
+struct WgGroup {
+  int n, accumulate, tiles_total;
+  int64_t K;
+  int start[WG_MAX + 1];
+  WgItem it[WG_MAX];
+};
+
+__global__ __launch_bounds__(NT, 2) void wgrad_grouped_kernel(const WgGroup g) {
+  using D = DmaCfg<0>;
+  __shared__ __attribute__((aligned(16))) char lds[D::LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int t = rp_xcd_remap(blockIdx.x, g.tiles_total);
+  int k = 0;
+  while (k + 1 < g.n && t >= g.start[k + 1]) ++k;
+  const WgItem w = g.it[k];
+  const int local = t - g.start[k];
+  const int tiles_n = (w.N + BN - 1) / BN;
+  const int64_t m0 = (int64_t)(local / tiles_n) * BM;
+  const int64_t n0 = (int64_t)(local % tiles_n) * BN;
+  const bool want_bias = w.db != nullptr && n0 == 0;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  dma_mainloop<false, false, 0>(w.dY, w.ldy, w.M, w.X, w.ldx, w.N, m0, n0, 0, g.K, want_bias, acc, bacc, lds, tid,
+                                lane, wid, wm, wn);
+  EpiDev ep{};
+  ep.gate_scale = 1.f;
+  ep.accumulate = g.accumulate;
+  gemm_epilogue<float, 0, D::HALVES>(acc, lds, tid, lane, wm, wn, m0, n0, w.M, w.N, w.dW, w.N, 1.f, ep, 0);
+  if (want_bias) {  // the tile's rows' whole-K column sums: the bias gradient itself
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bacc[j];
+    __syncthreads();
+    if (tid < BM && m0 + tid < w.M) {
+      const int c = tid / 8, e = tid % 8;
+      float sum = 0.f;
+      for (int j = 0; j < NT / (BM / 8); ++j) sum += red[(c + (BM / 8) * j) * 8 + e];
+      w.db[m0 + tid] = g.accumulate ? w.db[m0 + tid] + sum : sum;
+    }
+  }
 }
 
 // ====================== 256-row tiles: 8 waves, whole-K-tile LDS-DMA ring =======================
@@ -1205,6 +1283,38 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
   }
   if (c_dtype == RP_BF16) return launch_gemm_t<float, bf16>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, e, s);
   return launch_gemm_t<float, float>(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, C, ldc, alpha, e, s);
+}
+
+extern "C" int rp_gemm_wgrad_grouped(int64_t K, const rp_wgrad_item* items, int n_items, int accumulate,
+                                     void* stream) {
+  RP_REQUIRE(n_items >= 0 && n_items <= WG_MAX, "rp_gemm_wgrad_grouped: 0..%d items per launch", WG_MAX);
+  RP_REQUIRE(K >= 0 && K % 64 == 0, "rp_gemm_wgrad_grouped: K=%lld must be a multiple of 64", (long long)K);
+  if (n_items == 0) return RP_OK;
+  RP_REQUIRE(items, "rp_gemm_wgrad_grouped: null items");
+  WgGroup g{};
+  g.n = n_items;
+  g.accumulate = accumulate;
+  g.K = K;
+  int64_t tiles = 0;
+  for (int i = 0; i < n_items; ++i) {
+    const rp_wgrad_item& it = items[i];
+    RP_REQUIRE(it.M > 0 && it.N > 0 && it.M % 8 == 0 && it.N % 8 == 0 && it.ldy % 8 == 0 && it.ldx % 8 == 0 &&
+                   it.ldy >= it.M && it.ldx >= it.N && it.M <= INT32_MAX && it.N <= INT32_MAX &&
+                   it.ldy <= INT32_MAX && it.ldx <= INT32_MAX,
+               "rp_gemm_wgrad_grouped: item %d: M, N, leading dims must be positive multiples of 8", i);
+    RP_REQUIRE(it.dW && (K == 0 || (it.dY && it.X)), "rp_gemm_wgrad_grouped: item %d: null operand", i);
+    RP_REQUIRE(rp_aligned16(it.dY) && rp_aligned16(it.X) && rp_aligned16(it.dW),
+               "rp_gemm_wgrad_grouped: item %d: 16-byte alignment required", i);
+    g.start[i] = (int)tiles;
+    g.it[i] = WgItem{(const bf16*)it.dY, (const bf16*)it.X, it.dW, it.db, (int)it.M, (int)it.N, (int)it.ldy,
+                     (int)it.ldx};
+    tiles += ((it.M + BM - 1) / BM) * ((it.N + BN - 1) / BN);
+  }
+  RP_REQUIRE(tiles < (1 << 30), "rp_gemm_wgrad_grouped: too many tiles");
+  g.start[n_items] = (int)tiles;
+  g.tiles_total = (int)tiles;
+  hipLaunchKernelGGL(wgrad_grouped_kernel, dim3((unsigned)tiles), dim3(NT), 0, (hipStream_t)stream, g);
+  return rp_check_launch("rp_gemm_wgrad_grouped");
 }
 
 extern "C" int64_t rp_gemm_wgrad_workspace(int64_t M, int64_t N, int64_t K) {

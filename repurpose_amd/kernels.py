@@ -166,6 +166,38 @@ def linear_wgrad(dy, x, dW, db=None, accumulate=True, ws=None):
     return dW
 
 
+WGRAD_GROUP_MAX = 32  # items per rp_gemm_wgrad_grouped launch
+
+
+def linear_wgrad_grouped(items, accumulate=True):
+    """dW_i (+)= dy_i^T x_i, db_i (+)= colsum(dy_i) for items [(dy, x, dW, db)], all bf16 operands over
+    the same token count T (a multiple of 64): whole-K tiles, no split-K workspace (rp_gemm_wgrad_grouped).
+    Launches ceil(len / 32) kernels."""
+    if not items:
+        return
+    T = items[0][0].shape[0]
+    for dy, x, dW, db in items:
+        _gpu(dy, x, dW, db)
+        if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+            raise TypeError("rp_gemm_wgrad_grouped: bf16 operands")
+        if dy.shape[0] != T or x.shape[0] != T:
+            raise ValueError("rp_gemm_wgrad_grouped: every item needs the same token count")
+        if dW.dtype != torch.float32 or not dW.is_contiguous() or tuple(dW.shape) != (dy.shape[1], x.shape[1]):
+            raise ValueError("rp_gemm_wgrad_grouped: dW must be fp32 contiguous [N_out, N_in]")
+    for c in range(0, len(items), WGRAD_GROUP_MAX):
+        chunk = items[c:c + WGRAD_GROUP_MAX]
+        arr = (N.WgradItem * len(chunk))()
+        fl = 0.0
+        for i, (dy, x, dW, db) in enumerate(chunk):
+            arr[i] = N.WgradItem(_p(dy).value, _p(x).value, _p(dW).value, _p(db).value, dy.shape[1], x.shape[1],
+                                 dy.stride(0), x.stride(0))
+            fl += 2.0 * dy.shape[1] * x.shape[1] * T
+        e0 = _tick("gemm_wgrad")
+        N.call("rp_gemm_wgrad_grouped", T, ctypes.cast(arr, ctypes.c_void_p), len(chunk), int(accumulate),
+               _stream(chunk[0][0]))
+        _tock(e0, fl)
+
+
 # ------------------------------------------------------------------------------------- LayerNorm
 def layernorm_fwd(x, gamma, beta, eps=1e-5, pe=None, pe_period=1, relu=False, dropout_p=0.0, seed=0,
                   out_f32=True, lp_dtype=None, save_stats=True):

@@ -465,6 +465,39 @@ def test_wgrad_splitk_with_bias(dev, dtype, T, Nn, Kd):
     close(dW2, ref - 0.25, atol=tol, what="wgrad overwrite")
 
 
+def test_wgrad_grouped_whole_k(dev):
+    """rp_gemm_wgrad_grouped: several (dY, X) pairs of different shapes over one token range in one
+    launch (whole-K tiles, bias from the staged dY tiles), strided dY views, items without a bias,
+    accumulate and overwrite modes, deterministic; 33 items -> two launches."""
+    T = 1216  # a multiple of 64, not of 128
+    shapes = [(512, 2048), (2048, 512), (512, 512), (1536, 512), (256, 136), (8, 64)]
+    items, refs = [], []
+    big = rnd(T, 1536 + 64, dev=dev, seed=40).to(torch.bfloat16)
+    for i, (n_out, n_in) in enumerate(shapes):
+        dy = big[:, 8:8 + n_out] if n_out <= 1536 else rnd(T, n_out, dev=dev, seed=41 + i).to(torch.bfloat16)
+        x = rnd(T, n_in, dev=dev, seed=60 + i).to(torch.bfloat16)
+        dW = torch.full((n_out, n_in), 0.5, device=dev)
+        db = torch.full((n_out,), -2.0, device=dev) if i != 2 else None
+        items.append((dy, x, dW, db))
+        refs.append((dy.double().T @ x.double() + 0.5, (dy.double().sum(0) - 2.0) if db is not None else None))
+    K.linear_wgrad_grouped(items, accumulate=True)
+    tol = 1e-3 * math.sqrt(T)
+    for (dy, x, dW, db), (rw, rb) in zip(items, refs):
+        close(dW, rw, atol=tol, what=f"grouped wgrad {tuple(dW.shape)}")
+        if db is not None:
+            close(db, rb, atol=tol, what=f"grouped bias {tuple(db.shape)}")
+    outs = []
+    for _ in range(2):
+        its = [(dy, x, torch.empty_like(dW), None) for dy, x, dW, _ in items] * 6  # 36 items: two launches
+        its = its[:33]
+        K.linear_wgrad_grouped(its, accumulate=False)
+        outs.append([w for _, _, w, _ in its])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    for (dy, x, dW, _), w in zip(its, outs[0]):
+        close(w, dy.double().T @ x.double(), atol=tol, what="grouped wgrad overwrite")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("qpre", [False, True])

@@ -215,3 +215,25 @@ def test_fused_adam_checkpoint_resume_bitwise(dev):
         step(m2, opt2, 100 + s)
     torch.cuda.synchronize()
     assert torch.equal(m2.flat_params(), want)
+
+
+def test_bf16_grouped_weight_gradients_match_per_layer(dev, monkeypatch):
+    """The deferred whole-K grouped weight gradients (bf16, one device) equal the per-layer split-K
+    path up to fp32 summation order, on every encoder parameter; the step is deterministic."""
+    cfg = dict(TRI, self_num_layers=3)
+    b = to_dev(make_batch(cfg, 2, 128, [128, 90], seed=9), dev)
+
+    def grads(grouped):
+        monkeypatch.setenv("RP_WGRAD_GROUPED", "1" if grouped else "0")
+        torch.manual_seed(0)
+        m = MMCTransformer(**cfg, compute_dtype="bf16").to(dev).train()
+        m.DROPOUT = 0.0
+        out = m(b)
+        (m.losses(*out)["cls_loss"] / 2).backward()
+        torch.cuda.synchronize()
+        return m.flat_grads()[:m.trainable_numel()].clone()
+
+    g0, g1, g1b = grads(False), grads(True), grads(True)
+    assert torch.equal(g1, g1b)
+    scale = g0.abs().max().item()
+    assert (g1 - g0).abs().max().item() < 1e-4 * scale + 1e-6
