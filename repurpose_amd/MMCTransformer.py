@@ -521,19 +521,26 @@ class _Schedule:
         side = _side_stream(dlogits.device)
         pending = []  # (event on the side stream, prefixes) not yet announced
 
-        # bf16 single-device training: the encoder layers' weight gradients are deferred and computed
-        # by grouped whole-K launches (8 layers x 4 GEMMs = 1536 tiles per launch: no split-K slabs and
-        # no reduce pass); with all-reduce hooks (DP) they stay per layer so the exchange overlaps
-        deferred = [] if (dt == torch.bfloat16 and side is None and not m._grad_ready_hooks and M % 64 == 0
+        # bf16 training: the encoder layers' weight gradients are deferred and computed by grouped
+        # whole-K launches (8 layers x 4 GEMMs = 1536 tiles = three full waves per launch: no split-K
+        # slabs and no reduce pass).  Under DP a layer's gradient range is announced to the all-reduce
+        # hooks once its group has been launched, so the first group's exchange overlaps the backward
+        # of the remaining eight layers.
+        deferred = [] if (dt == torch.bfloat16 and side is None and M % 64 == 0
                           and os.environ.get("RP_WGRAD_GROUPED", "1") != "0") else None
+        held = []  # layer prefixes whose gradients wait for their group launch
         per_launch = 4 * 8
+
+        def flush_group():
+            K.linear_wgrad_grouped(deferred)
+            deferred.clear()
+            for pf in held:
+                m._grads_ready(pf)
+            held.clear()
 
         def wgrad(dy, x, wname, bname):
             if deferred is not None and wname.startswith("multimodal_encoder."):
                 deferred.append((dy, x, G(wname), G(bname)))
-                if len(deferred) == per_launch:
-                    K.linear_wgrad_grouped(deferred)
-                    deferred.clear()
                 return
             if side is None:
                 K.linear_wgrad(dy, x, G(wname), db=G(bname), ws=wws)
@@ -545,6 +552,11 @@ class _Schedule:
             x.record_stream(side)
 
         def ready(prefixes, flush=False):
+            if deferred is not None and prefixes[0].startswith("multimodal_encoder."):
+                held.append(prefixes)
+                if len(deferred) >= per_launch:
+                    flush_group()
+                return
             if side is None:
                 m._grads_ready(prefixes)
                 return
@@ -612,8 +624,7 @@ class _Schedule:
                                      dgamma=G(pre + "norm1.weight"), dbeta=G(pre + "norm1.bias"), ws=ws)
             ready([pre])
         if deferred:
-            K.linear_wgrad_grouped(deferred)
-            deferred.clear()
+            flush_group()
         # input LayerNorm (+PE, no grad) and input projection (weight/bias grads only)
         _, dproj = K.layernorm_bwd(dx, S["proj"], S["mu0"], S["rs0"], self.P("input_norm.weight"), want_f32=False,
                                    lp_dtype=dt, dgamma=G("input_norm.weight"), dbeta=G("input_norm.bias"), ws=ws)

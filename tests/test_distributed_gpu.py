@@ -29,14 +29,14 @@ def _port():
 
 def _batch(seed=5):
     g = torch.Generator().manual_seed(seed)
-    B, T, lens = 2, 96, [96, 70]
+    B, T, lens = 2, 128, [128, 70]
     return {"visual_feats": torch.randn(B, T, 512, generator=g), "audio_feats": torch.relu(torch.randn(B, T, 2048, generator=g)),
             "text_feats": torch.randn(B, T, 384, generator=g),
             "masks": (torch.arange(T)[None] < torch.tensor(lens)[:, None]).unsqueeze(1),
             "labels": (torch.rand(B, T, generator=g) < 0.35).float(), "segments": torch.rand(B, T, 2, generator=g) * 10}
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, dtype="fp32"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
@@ -53,7 +53,10 @@ def _worker(rank, world, port, q):
 
         def fresh(seed):
             torch.manual_seed(seed)
-            m = MMCTransformer(**CFG, compute_dtype="fp32")
+            # bf16: 9 layers, so the deferred grouped weight gradients flush once mid-backward (8
+            # layers) and once at the end, each flush announcing its layers' ranges to the reducer
+            cfg = CFG if dtype == "fp32" else dict(CFG, self_num_layers=9)
+            m = MMCTransformer(**cfg, compute_dtype=dtype)
             m.DROPOUT = 0.0  # dropout off: the per-rank gradients are comparable bit for bit
             return m
 
@@ -115,11 +118,12 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_ddp_two_ranks_real_backward(dev):
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_ddp_two_ranks_real_backward(dev, dtype):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, dtype)) for r in range(2)]
     for p in procs:
         p.start()
     try:
