@@ -191,6 +191,19 @@ int64_t rp_colsum_workspace(int64_t rows, int64_t cols);
 int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, int64_t ldx, const float* w,
               float* out, int accumulate, float* workspace, void* stream);
 
+/* Many fp32 column sums in one launch (no weights): out_k[c] (+)= sum_r X_k[r*ldx_k + c] with the
+ * same fixed summation order as rp_colsum's single pass (so the results are bitwise those of
+ * per-item rp_colsum calls with rows <= 2048).  Used to reduce every LayerNorm's gamma / beta
+ * partials of a backward together (the LayerNorm affine gradients of models/MMCTransformer.py
+ * under loss.backward()).  At most 64 items per call. */
+typedef struct {
+  const float* X;
+  float* out;
+  int64_t rows, cols, ldx;
+  int accumulate;
+} rp_colsum_item;
+int rp_colsum_batched(const rp_colsum_item* items, int n_items, void* stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Flag or-ed into the dtype argument of every rp_attn_* / rp_mha_* entry point: the q operand
  * already holds Q * scale * log2(e), rounded to the operand dtype (rp_gemm's col_scale epilogue

@@ -531,9 +531,19 @@ class _Schedule:
         held = []  # layer prefixes whose gradients wait for their group launch
         per_launch = 4 * 8
 
+        # LayerNorm gamma / beta partials: reduced together by one rp_colsum_batched launch per flush
+        # (before the gradients they finish are announced, and at the end) instead of one per LayerNorm
+        cs = []
+
+        def flush_cs():
+            if cs:
+                K.colsum_batched(cs)
+                cs.clear()
+
         def flush_group():
             K.linear_wgrad_grouped(deferred)
             deferred.clear()
+            flush_cs()
             for pf in held:
                 m._grads_ready(pf)
             held.clear()
@@ -557,6 +567,8 @@ class _Schedule:
                 if len(deferred) >= per_launch:
                     flush_group()
                 return
+            if m._grad_ready_hooks:
+                flush_cs()
             if side is None:
                 m._grads_ready(prefixes)
                 return
@@ -582,17 +594,17 @@ class _Schedule:
         # cls_head[0] LayerNorm (+ any external gradient on feats)
         dres = dfeats.reshape(M, -1).contiguous().float() if dfeats is not None else None
         dfe, _ = K.layernorm_bwd(dc0, S["feats"], S["muC"], S["rsC"], self.P("cls_head.0.weight"), dres=dres,
-                                 dgamma=G("cls_head.0.weight"), dbeta=G("cls_head.0.bias"), ws=ws)
+                                 dgamma=G("cls_head.0.weight"), dbeta=G("cls_head.0.bias"), ws=ws, defer=cs)
         # feature_map: LN + ReLU + dropout, then Linear
         _, dz = K.layernorm_bwd(dfe, S["z"], S["muF"], S["rsF"], self.P("feature_map.1.weight"), y=S["feats"],
                                 dropout_p=p, seed=self.seed(1), want_f32=False, lp_dtype=dt,
-                                dgamma=G("feature_map.1.weight"), dbeta=G("feature_map.1.bias"), ws=ws)
+                                dgamma=G("feature_map.1.weight"), dbeta=G("feature_map.1.bias"), ws=ws, defer=cs)
         wgrad(dz, S["e"], "feature_map.0.weight", "feature_map.0.bias")
         de = K.linear_dgrad(dz, self.W("feature_map.0.weight"), out_dtype=_F32)
         # encoder_norm; emit the masked lp gradient for the last layer's dropout2
         dx, g2 = K.layernorm_bwd(de, S["xL"], S["muE"], S["rsE"], self.P("encoder_norm.weight"), lp_dtype=dt,
                                  lp_dropout_p=p, lp_seed=self.seed(103 + 4 * (L - 1)),
-                                 dgamma=G("encoder_norm.weight"), dbeta=G("encoder_norm.bias"), ws=ws)
+                                 dgamma=G("encoder_norm.weight"), dbeta=G("encoder_norm.bias"), ws=ws, defer=cs)
         ready(["encoder_norm.", "feature_map.", "cls_head."])
         for l in reversed(range(L)):
             pre = f"multimodal_encoder.layers.{l}."
@@ -606,7 +618,7 @@ class _Schedule:
             # norm2 + residual; masked lp gradient for dropout1
             dx1, g1 = K.layernorm_bwd(dh2, x1, mu2, rs2, self.P(pre + "norm2.weight"), dres=dx, lp_dtype=dt,
                                       lp_dropout_p=p, lp_seed=self.seed(101 + 4 * l),
-                                      dgamma=G(pre + "norm2.weight"), dbeta=G(pre + "norm2.bias"), ws=ws)
+                                      dgamma=G(pre + "norm2.weight"), dbeta=G(pre + "norm2.bias"), ws=ws, defer=cs)
             # out_proj
             wgrad(g1, o, pre + "self_attn.out_proj.weight", pre + "self_attn.out_proj.bias")
             do = K.linear_dgrad(g1, self.W(pre + "self_attn.out_proj.weight"), out_dtype=dt)
@@ -621,18 +633,19 @@ class _Schedule:
             dx, g2 = K.layernorm_bwd(dh1, x, mu1, rs1, self.P(pre + "norm1.weight"), dres=dx1,
                                      lp_dtype=None if last else dt, lp_dropout_p=0.0 if last else p,
                                      lp_seed=0 if last else self.seed(103 + 4 * (l - 1)),
-                                     dgamma=G(pre + "norm1.weight"), dbeta=G(pre + "norm1.bias"), ws=ws)
+                                     dgamma=G(pre + "norm1.weight"), dbeta=G(pre + "norm1.bias"), ws=ws, defer=cs)
             ready([pre])
         if deferred:
             flush_group()
         # input LayerNorm (+PE, no grad) and input projection (weight/bias grads only)
         _, dproj = K.layernorm_bwd(dx, S["proj"], S["mu0"], S["rs0"], self.P("input_norm.weight"), want_f32=False,
-                                   lp_dtype=dt, dgamma=G("input_norm.weight"), dbeta=G("input_norm.bias"), ws=ws)
+                                   lp_dtype=dt, dgamma=G("input_norm.weight"), dbeta=G("input_norm.bias"), ws=ws, defer=cs)
         wgrad(dproj, S["xin"], "input_projection.weight", "input_projection.bias")
         ready(["input_projection.", "input_norm."], flush=True)
         if side is not None:
             wws.record_stream(side)
             main.wait_stream(side)
+        flush_cs()
         for h in m._grad_done_hooks:
             h()
         self.saved = None

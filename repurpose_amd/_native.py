@@ -49,6 +49,10 @@ class WgradItem(ctypes.Structure):
                 ("ldx", c_i64)]
 
 
+class ColsumItem(ctypes.Structure):
+    _fields_ = [("X", c_vp), ("out", c_vp), ("rows", c_i64), ("cols", c_i64), ("ldx", c_i64), ("accumulate", c_i)]
+
+
 class MhaArgs(ctypes.Structure):
     _fields_ = [("q", c_vp), ("ldq", c_i64), ("k", c_vp), ("ldk", c_i64), ("v", c_vp), ("ldv", c_i64),
                 ("key_valid", c_vp), ("B", c_i), ("Tq", c_i), ("Tk", c_i), ("H", c_i), ("head_dim", c_i),
@@ -73,6 +77,7 @@ _SIGNATURES = {
     "rp_layernorm_bwd_blocks": (c_i64, [c_i64]),
     "rp_layernorm_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnBwdArgs), c_vp]),
     "rp_colsum_workspace": (c_i64, [c_i64, c_i64]),
+    "rp_colsum_batched": (c_i, [c_vp, c_i, c_vp]),
     "rp_colsum": (c_i, [c_vp, c_i, c_i64, c_i64, c_i64, c_vp, c_vp, c_i, c_vp, c_vp]),
     "rp_attn_dropmask_elems": (c_i64, [c_i, c_i, c_i]),
     "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -16,11 +16,11 @@ namespace {
 template <typename TO>
 __global__ void concat_kernel(const float* __restrict__ v, int dv, const float* __restrict__ a, int da,
                               const float* __restrict__ t, int dt, int64_t rows, TO* __restrict__ out) {
+  // one workgroup per row (no index division); 16-byte loads, one vector store per 4 elements
   const int D = dv + da + dt;
-  const int64_t n4 = rows * (int64_t)(D / 4);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / (D / 4);
-    const int c = (int)(i % (D / 4)) * 4;
+  const int64_t r = blockIdx.x;
+  TO* orow = out + r * D;
+  for (int c = threadIdx.x * 4; c < D; c += blockDim.x * 4) {
     float4 q;
     if (c < dv)
       q = *reinterpret_cast<const float4*>(v + r * dv + c);
@@ -28,11 +28,11 @@ __global__ void concat_kernel(const float* __restrict__ v, int dv, const float* 
       q = *reinterpret_cast<const float4*>(a + r * da + (c - dv));
     else
       q = *reinterpret_cast<const float4*>(t + r * dt + (c - dv - da));
-    TO* o = out + r * D + c;
-    rp_st(o + 0, q.x);
-    rp_st(o + 1, q.y);
-    rp_st(o + 2, q.z);
-    rp_st(o + 3, q.w);
+    if constexpr (std::is_same<TO, float>::value) {
+      *reinterpret_cast<float4*>(orow + c) = q;
+    } else {
+      *reinterpret_cast<bf16x4*>(orow + c) = bf16x4{(bf16)q.x, (bf16)q.y, (bf16)q.z, (bf16)q.w};
+    }
   }
 }
 
@@ -79,11 +79,11 @@ __global__ void colsum_pass1(const T* __restrict__ X, int64_t rows, int64_t cols
 // and 64 row groups; each thread sums its rows in order, the groups are added in order through LDS
 constexpr int CS1_MAX_ROWS = 2048;
 template <typename T>
-__global__ __launch_bounds__(1024) void colsum_onepass(const T* __restrict__ X, int64_t rows, int64_t cols,
-                                                       int64_t ldx, const float* __restrict__ w,
-                                                       float* __restrict__ out, int accumulate) {
+__device__ __forceinline__ void colsum_block(const T* __restrict__ X, int64_t rows, int64_t cols, int64_t ldx,
+                                             const float* __restrict__ w, float* __restrict__ out, int accumulate,
+                                             int64_t cblk) {
   const int ch = threadIdx.x & 15, rg = threadIdx.x >> 4;  // 16 column chunks x 64 row groups
-  const int64_t c = (int64_t)blockIdx.x * 64 + ch * 4;
+  const int64_t c = cblk * 64 + ch * 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < cols) {
     const bool vec = std::is_same<T, float>::value && c + 3 < cols && (ldx & 3) == 0;
@@ -137,6 +137,35 @@ __global__ __launch_bounds__(1024) void colsum_onepass(const T* __restrict__ X, 
     if (c + 2 < cols) out[c + 2] = accumulate ? out[c + 2] + t.z : t.z;
     if (c + 3 < cols) out[c + 3] = accumulate ? out[c + 3] + t.w : t.w;
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void colsum_onepass(const T* __restrict__ X, int64_t rows, int64_t cols,
+                                                       int64_t ldx, const float* __restrict__ w,
+                                                       float* __restrict__ out, int accumulate) {
+  colsum_block<T>(X, rows, cols, ldx, w, out, accumulate, blockIdx.x);
+}
+
+// many fp32 column sums in one launch (the LayerNorm gamma / beta partials of a whole backward):
+// item k owns blocks [start[k], start[k+1]), one 64-column slice each, same sums as colsum_onepass
+constexpr int CSB_MAX = 64;
+struct CsItem {
+  const float* X;
+  float* out;
+  int rows, cols, ldx, accumulate;
+};
+struct CsBatch {
+  int n;
+  int start[CSB_MAX + 1];
+  CsItem it[CSB_MAX];
+};
+
+__global__ __launch_bounds__(1024) void colsum_batched_kernel(const CsBatch bt) {
+  const int blk = blockIdx.x;
+  int k = 0;
+  while (k + 1 < bt.n && blk >= bt.start[k + 1]) ++k;
+  const CsItem c = bt.it[k];
+  colsum_block<float>(c.X, c.rows, c.cols, c.ldx, nullptr, c.out, c.accumulate, blk - bt.start[k]);
 }
 
 __global__ void colsum_pass2(const float* __restrict__ ws, int64_t nrb, int64_t cols, float* __restrict__ out,
@@ -255,11 +284,12 @@ __device__ __forceinline__ void adam_elem(float& pi, float gi, float& mi, float&
   pi = pi - c[0] * (mi / denom);
 }
 
-// 4 elements per thread (16-byte loads/stores); scalar tail.  DEV: the coefficients are read from
-// device memory when the kernel runs (graph replay), else taken from the arguments.
+// one element per thread-iteration (measured on MI355X: 243-246 us per step for 52.6 M parameters,
+// against 258-269 us for a float4 variant).  DEV: the coefficients are read from device memory when
+// the kernel runs (graph replay), else taken from the arguments.
 template <bool DEV>
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, int64_t n, int vec, const float* __restrict__ coef_dev, float c0, float c1,
+                            float* __restrict__ v, int64_t n, const float* __restrict__ coef_dev, float c0, float c1,
                             float c2, float c3, float c4, float c5, bf16* __restrict__ plp) {
   float c[6];
   if (DEV) {
@@ -268,27 +298,7 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   } else {
     c[0] = c0; c[1] = c1; c[2] = c2; c[3] = c3; c[4] = c4; c[5] = c5;
   }
-  const int64_t n4 = vec ? n / 4 : 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    const float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    adam_elem(pp.x, gg.x, mm.x, vv.x, c);
-    adam_elem(pp.y, gg.y, mm.y, vv.y, c);
-    adam_elem(pp.z, gg.z, mm.z, vv.z, c);
-    adam_elem(pp.w, gg.w, mm.w, vv.w, c);
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    if (plp) {
-      typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
-      bf16x4v o = {(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
-      reinterpret_cast<bf16x4v*>(plp)[i] = o;
-    }
-  }
-  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float pi = p[i], mi = m[i], vi = v[i];
     adam_elem(pi, g[i], mi, vi, c);
     p[i] = pi;
@@ -323,14 +333,17 @@ extern "C" int rp_concat_rows(const float* v, int dv, const float* a, int da, co
                               void* out, int out_dtype, void* stream) {
   RP_REQUIRE(dv >= 0 && da >= 0 && dt >= 0 && rows >= 0, "rp_concat_rows: negative size");
   RP_REQUIRE(dv % 4 == 0 && da % 4 == 0 && dt % 4 == 0, "rp_concat_rows: widths must be multiples of 4");
+  RP_REQUIRE(rows < (1ll << 31), "rp_concat_rows: too many rows");
   RP_REQUIRE((dv == 0 || v) && (da == 0 || a) && (dt == 0 || t) && out, "rp_concat_rows: null pointer");
+  RP_REQUIRE(rp_aligned16(out) && rp_aligned16(v) && rp_aligned16(a) && rp_aligned16(t),
+             "rp_concat_rows: 16-byte aligned buffers required");
   const int64_t n4 = rows * (int64_t)((dv + da + dt) / 4);
   if (n4 == 0) return RP_OK;
   hipStream_t s = (hipStream_t)stream;
   if (out_dtype == RP_BF16)
-    hipLaunchKernelGGL(concat_kernel<bf16>, dim3(grid_for(n4, 256)), dim3(256), 0, s, v, dv, a, da, t, dt, rows, (bf16*)out);
+    hipLaunchKernelGGL(concat_kernel<bf16>, dim3((unsigned)rows), dim3(256), 0, s, v, dv, a, da, t, dt, rows, (bf16*)out);
   else if (out_dtype == RP_F32)
-    hipLaunchKernelGGL(concat_kernel<float>, dim3(grid_for(n4, 256)), dim3(256), 0, s, v, dv, a, da, t, dt, rows, (float*)out);
+    hipLaunchKernelGGL(concat_kernel<float>, dim3((unsigned)rows), dim3(256), 0, s, v, dv, a, da, t, dt, rows, (float*)out);
   else {
     rp_set_error("rp_concat_rows: bad dtype");
     return RP_ERR_ARG;
@@ -344,6 +357,29 @@ extern "C" int rp_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void*
   RP_REQUIRE(src && dst, "rp_cast_f32_to_bf16: null");
   hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, src, (bf16*)dst, n);
   return rp_check_launch("rp_cast_f32_to_bf16");
+}
+
+extern "C" int rp_colsum_batched(const rp_colsum_item* items, int n_items, void* stream) {
+  RP_REQUIRE(n_items >= 0 && n_items <= CSB_MAX, "rp_colsum_batched: 0..%d items per launch", CSB_MAX);
+  if (n_items == 0) return RP_OK;
+  RP_REQUIRE(items, "rp_colsum_batched: null items");
+  CsBatch bt{};
+  bt.n = n_items;
+  int64_t blocks = 0;
+  for (int i = 0; i < n_items; ++i) {
+    const rp_colsum_item& c = items[i];
+    RP_REQUIRE(c.rows >= 0 && c.cols > 0 && c.ldx >= c.cols && c.rows <= INT32_MAX && c.ldx <= INT32_MAX &&
+                   c.cols <= INT32_MAX,
+               "rp_colsum_batched: item %d: bad shape", i);
+    RP_REQUIRE(c.out && (c.rows == 0 || c.X), "rp_colsum_batched: item %d: null pointer", i);
+    bt.start[i] = (int)blocks;
+    bt.it[i] = CsItem{c.X, c.out, (int)c.rows, (int)c.cols, (int)c.ldx, c.accumulate};
+    blocks += (c.cols + 63) / 64;
+  }
+  RP_REQUIRE(blocks < (1 << 30), "rp_colsum_batched: too many blocks");
+  bt.start[n_items] = (int)blocks;
+  hipLaunchKernelGGL(colsum_batched_kernel, dim3((unsigned)blocks), dim3(1024), 0, (hipStream_t)stream, bt);
+  return rp_check_launch("rp_colsum_batched");
 }
 
 extern "C" int64_t rp_colsum_workspace(int64_t rows, int64_t cols) {
@@ -466,18 +502,13 @@ static int adam_launch(float* p, const float* g, float* m, float* v, int64_t n, 
                        const float* c, void* p_lp, void* stream) {
   if (n == 0) return RP_OK;
   RP_REQUIRE(p && g && m && v, "rp_adam_step: null");
-  // 16-byte vectors when every operand allows them, else the scalar loop covers everything
-  const int vec = rp_aligned16(p) && rp_aligned16(g) && rp_aligned16(m) && rp_aligned16(v) &&
-                  (!p_lp || (((uintptr_t)p_lp) & 7u) == 0);
-  int64_t blocks = (n / 4 + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
-  if (blocks < 1) blocks = 1;
+  const dim3 grid(grid_for(n, 256));
   if (coef_dev)
-    hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, vec,
-                       coef_dev, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, (bf16*)p_lp);
+    hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, coef_dev, 0.f, 0.f,
+                       0.f, 0.f, 0.f, 0.f, (bf16*)p_lp);
   else
-    hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, vec,
-                       nullptr, c[0], c[1], c[2], c[3], c[4], c[5], (bf16*)p_lp);
+    hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, nullptr, c[0], c[1],
+                       c[2], c[3], c[4], c[5], (bf16*)p_lp);
   return rp_check_launch("rp_adam_step");
 }
 

@@ -216,8 +216,10 @@ def layernorm_fwd(x, gamma, beta, eps=1e-5, pe=None, pe_period=1, relu=False, dr
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, y=None, dropout_p=0.0, seed=0, dres=None, want_f32=True,
-                  lp_dtype=None, lp_dropout_p=0.0, lp_seed=0, dgamma=None, dbeta=None, ws=None):
-    """Returns (dx_f32, dx_lp); accumulates dgamma / dbeta (fp32 [D]) when given."""
+                  lp_dtype=None, lp_dropout_p=0.0, lp_seed=0, dgamma=None, dbeta=None, ws=None, defer=None):
+    """Returns (dx_f32, dx_lp); accumulates dgamma / dbeta (fp32 [D]) when given.  With ``defer`` (a
+    list), the gamma / beta partial reductions are appended to it as (partials, out) pairs for one
+    ``colsum_batched`` call later instead of being launched here."""
     _gpu(dy, x, mean, rstd, gamma, y, dres)
     rows, D = x.shape
     dev = x.device
@@ -243,14 +245,32 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, y=None, dropout_p=0.0, seed=0, dres=
                     _p(dxl).value, _dt(dxl) if dxl is not None else 0, D, float(lp_dropout_p),
                     int(lp_seed) & 0xFFFFFFFF, _p(pg).value, _p(pb).value, ld_part)
     N.call("rp_layernorm_bwd", rows, D, ctypes.byref(a), _stream(x))
-    if both:
-        colsum(part, out=dgamma.as_strided((2 * D,), (1,)), accumulate=True, ws=ws)
-        return dx, dxl
-    if dgamma is not None:
-        colsum(pg, out=dgamma, accumulate=True, ws=ws)
-    if dbeta is not None:
-        colsum(pb, out=dbeta, accumulate=True, ws=ws)
+    jobs = [(part, dgamma.as_strided((2 * D,), (1,)))] if both else \
+        [(p, o) for p, o in ((pg, dgamma), (pb, dbeta)) if o is not None]
+    if defer is not None:
+        defer.extend(jobs)
+    else:
+        for p, o in jobs:
+            colsum(p, out=o, accumulate=True, ws=ws)
     return dx, dxl
+
+
+COLSUM_BATCH_MAX = 64
+
+
+def colsum_batched(jobs, accumulate=True):
+    """out (+)= column sums of X for every (X fp32 [rows, cols] with unit column stride, out fp32 [cols])
+    in ``jobs``, ceil(len / 64) launches (rp_colsum_batched)."""
+    for c in range(0, len(jobs), COLSUM_BATCH_MAX):
+        chunk = jobs[c:c + COLSUM_BATCH_MAX]
+        arr = (N.ColsumItem * len(chunk))()
+        for i, (X, out) in enumerate(chunk):
+            _gpu(X, out)
+            if X.dtype != torch.float32 or out.dtype != torch.float32 or X.stride(1) != 1 or out.stride(0) != 1 \
+                    or out.shape[0] != X.shape[1]:
+                raise ValueError("colsum_batched: fp32 X with unit column stride and a matching fp32 out")
+            arr[i] = N.ColsumItem(_p(X).value, _p(out).value, X.shape[0], X.shape[1], X.stride(0), int(accumulate))
+        N.call("rp_colsum_batched", ctypes.cast(arr, ctypes.c_void_p), len(chunk), _stream(chunk[0][0]))
 
 
 # ------------------------------------------------------------------------------------- reductions

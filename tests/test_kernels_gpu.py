@@ -465,6 +465,26 @@ def test_wgrad_splitk_with_bias(dev, dtype, T, Nn, Kd):
     close(dW2, ref - 0.25, atol=tol, what="wgrad overwrite")
 
 
+def test_colsum_batched_equals_per_item(dev):
+    """rp_colsum_batched (every LayerNorm's gamma / beta partials of a backward in one launch) gives
+    bitwise the per-item rp_colsum results, accumulate and overwrite, ragged shapes, 70 items
+    (two launches), strided rows."""
+    items = []
+    for i in range(70):
+        rows, cols = [(512, 1024), (7, 512), (33, 12), (1, 4), (300, 260)][i % 5]
+        X = rnd(rows, cols + 4, dev=dev, seed=100 + i)[:, 2:2 + cols] if i % 3 == 0 else rnd(rows, cols, dev=dev, seed=100 + i)
+        items.append((X, rnd(cols, dev=dev, seed=300 + i)))
+    want = [o.clone() for _, o in items]
+    for (X, _), w in zip(items, want):
+        K.colsum(X, out=w, accumulate=True)
+    K.colsum_batched(items, accumulate=True)
+    for (_, o), w in zip(items, want):
+        assert torch.equal(o, w)
+    K.colsum_batched(items, accumulate=False)
+    for (X, o) in items:
+        assert torch.equal(o, K.colsum(X))
+
+
 def test_wgrad_grouped_whole_k(dev):
     """rp_gemm_wgrad_grouped: several (dY, X) pairs of different shapes over one token range in one
     launch (whole-K tiles, bias from the staged dY tiles), strided dY views, items without a bias,
