@@ -248,7 +248,7 @@ def main():
         # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
         # (scripts/pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE doubled per the gfx950 correction)
         try:
-            with open(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")) as f:
+            with open(os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")) as f:
                 traffic = {k: v["hbm_bytes"] for k, v in json.load(f).items()}
         except (OSError, ValueError, KeyError):
             traffic = {}

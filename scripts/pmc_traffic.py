@@ -9,7 +9,8 @@ import json
 import sys
 from collections import defaultdict
 
-SHORT = {"attn_bwd_kv_kernel": "attn_bwd_dkdv", "attn_bwd_q_kernel": "attn_bwd_dq", "attn_fwd_kernel": "attn_fwd",
+SHORT = {"attn_bwd_kv_dma_kernel": "attn_bwd_dkdv", "attn_bwd_kv_kernel": "attn_bwd_dkdv",
+         "wgrad_grouped_kernel": "wgrad_grouped", "gemm8_kernel": "gemm8", "colsum_batched_kernel": "colsum_batched", "attn_bwd_q_kernel": "attn_bwd_dq", "attn_fwd_kernel": "attn_fwd",
          "gemm_bf16_dma_kernel": "gemm_bf16", "ln_bwd_kernel": "ln_bwd", "ln_fwd_kernel": "ln_fwd",
          "splitk_reduce_kernel": "splitk_reduce", "adam_kernel": "adam"}
 

@@ -237,3 +237,30 @@ def test_bf16_grouped_weight_gradients_match_per_layer(dev, monkeypatch):
     assert torch.equal(g1, g1b)
     scale = g0.abs().max().item()
     assert (g1 - g0).abs().max().item() < 1e-4 * scale + 1e-6
+
+
+def test_bf16_training_tracks_fp32(dev):
+    """bf16 (bench mode) training follows fp32 (parity mode) training: same init, same batches,
+    dropout off, 8 FusedAdam steps; the per-step losses agree to 1 % (the L = 16, T = 1024, 40-step
+    run of scripts/bf16_vs_fp32.py stays within 0.4 %, profiles/r02_bf16_vs_fp32.json)."""
+    batches = [to_dev(make_batch(TRI, 2, 128, [128, 100], seed=70 + i), dev) for i in range(3)]
+
+    def run(dtype):
+        torch.manual_seed(0)
+        m = MMCTransformer(**TRI, compute_dtype=dtype).to(dev).train()
+        m.DROPOUT = 0.0
+        opt = FusedAdam(m, lr=3e-4, weight_decay=1e-4)
+        out = []
+        for s in range(8):
+            opt.zero_grad()
+            o = m(batches[s % 3])
+            loss = m.losses(*o)["cls_loss"] / 2
+            loss.backward()
+            opt.step()
+            out.append(loss.item())
+        return out
+
+    f32, b16 = run("fp32"), run("bf16")
+    assert f32[-1] < f32[0] and b16[-1] < b16[0]
+    for a, b in zip(f32, b16):
+        assert abs(a - b) <= 1e-2 * abs(a), (f32, b16)
