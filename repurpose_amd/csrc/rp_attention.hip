@@ -1498,6 +1498,264 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     }
 }
 
+// =================================================================================================
+// backward: dQ (+ the fused delta) — bf16, LDS-DMA staged variant (the default for bf16 with
+// 128-query blocks and Tk <= QD_TKMAX; RP_ATTN_DMA=0 selects the register-staged kernel above).
+// Same math and register layouts as attn_bwd_q_kernel<bf16, DROP, true, 2>; what changes is how
+// the key tiles reach LDS:
+//  * K and V tiles and this block's keep-bit words of a key tile arrive by LDS-DMA (the swizzled
+//    images of dma_rows64; the words as one 1 KB piece) in a three-slot ring two tiles ahead, one
+//    barrier per tile — the register-staged kernel has one tile of compute to hide the K / V loads
+//    and loads its keep-bit word from global memory inside the tile;
+//  * the sequence's key-valid bytes are staged in LDS once, with a per-tile "no masked key" flag;
+//    rows past Tk (clamped DMA sources) are invalid keys there, so they get P = 0.
+// =================================================================================================
+constexpr int QD_TKMAX = 8192;
+
+template <bool DROP>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
+  constexpr int QT = 2, QB = NW * 16 * QT;  // 128 queries per workgroup
+  using C = AttnCfg<bf16>;
+  constexpr int TILE = FW_KT * C::ROWB;  // one 64-key K or V image (8 KB)
+  constexpr int MASKB = 1024;            // keep bits of the tile: 4 lane groups x 128 queries x u16
+  constexpr int BUF = 2 * TILE + MASKB;
+  constexpr int NBUF = 3;
+  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
+  __shared__ __attribute__((aligned(16))) uint8_t kvl[QD_TKMAX];
+  __shared__ int kfull[QD_TKMAX / FW_KT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const float scale = a.scale, drop_scale = a.drop_scale;
+  const float* __restrict__ lse = a.lse;
+  const int nqb = (Tq + QB - 1) / QB;
+  const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
+  const int bh = L / nqb, qb = L % nqb;
+  const int b = bh / H, h = bh % H;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
+  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + h * HD;
+  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + h * HD;
+  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + h * HD;
+  const bf16* dOg = (const bf16*)a.dout + (int64_t)b * Tq * lddo + h * HD;
+  const int q0 = qb * QB + w * 16 * QT;
+  const float c = scale * LOG2E;
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
+  const uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
+
+  // ---- prologue: Q, dO fragments, lse, delta (= rowsum(dO * O), written for the dK/dV kernel) ----
+  bf16x8 qf[QT][2], df[QT][2];
+  float lq[QT], dq[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    const int q = q0 + qt * 16 + i;
+    lq[qt] = q < Tq ? lse[(int64_t)bh * Tq + q] * LOG2E - (DROP ? log2f(drop_scale) : 0.f) : INFINITY;
+    float part = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      qf[qt][s2] = row_frag_gmem(Qg, ldq, q0 + qt * 16, Tq, s2 * 32, lane);
+      df[qt][s2] = row_frag_gmem(dOg, lddo, q0 + qt * 16, Tq, s2 * 32, lane);
+      const bf16x8 of = row_frag_gmem((const bf16*)a.out + (int64_t)b * Tq * a.ldo + h * HD, a.ldo, q0 + qt * 16, Tq,
+                                      s2 * 32, lane);
+      if (a.out_lo) {  // O = hi + lo: delta from the unrounded output (exact rowsum(dO * O))
+        const bf16x8 ol = row_frag_gmem((const bf16*)a.out_lo + (int64_t)b * Tq * a.ldo + h * HD, a.ldo,
+                                        q0 + qt * 16, Tq, s2 * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += (float)df[qt][s2][j] * ((float)of[j] + (float)ol[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += (float)df[qt][s2][j] * (float)of[j];
+      }
+    }
+    const float dl = quad_sum(part);
+    dq[qt] = q < Tq ? -dl * (DROP ? 1.f / drop_scale : 1.f) : 0.f;
+    if (g == 0 && q < Tq) {  // delta and the dK/dV kernel's row constants (planes 1, 2)
+      const int64_t plane = (int64_t)B * H * Tq;
+      a.delta[(int64_t)bh * Tq + q] = dl;
+      a.delta[plane + (int64_t)bh * Tq + q] = dq[qt];
+      a.delta[2 * plane + (int64_t)bh * Tq + q] = -lq[qt];
+    }
+  }
+  if (seq_has_no_key(a, b, tid)) {  // empty_uniform: dQ = 0 (delta above is still written)
+    bf16* dQz = (bf16*)a.dq + (int64_t)b * Tq * a.lddq + h * HD;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = q0 + qt * 16 + 4 * g + r;
+        if (q >= Tq) continue;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) dQz[(int64_t)q * a.lddq + dt * 16 + i] = (bf16)0.f;
+      }
+    return;
+  }
+  float nlq[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    nlq[qt] = -lq[qt];
+    if (!a.qpre) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qt][s2][j] = (bf16)((float)qf[qt][s2][j] * c);
+    }
+  }
+  // key-valid bytes of the sequence (0 past Tk) and per-tile "no masked key" flags, staged once
+  const int nkt = (Tk + FW_KT - 1) / FW_KT;
+  for (int k = tid; k < nkt * FW_KT; k += NT) kvl[k] = k < Tk ? (a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
+  __syncthreads();
+  for (int t = tid; t < nkt; t += NT) {
+    int ok = 1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t v = reinterpret_cast<const uint32_t*>(kvl)[t * 16 + j];
+      ok &= ((v - 0x01010101u) & ~v & 0x80808080u) == 0u;  // no zero byte
+    }
+    kfull[t] = ok;
+  }
+  // consume Q / dO here, before the loop: otherwise their wait lands at the first use inside the
+  // loop as a full vmcnt(0) on every ring cycle
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) asm volatile("" ::"v"(qf[qt][s2]), "v"(df[qt][s2]));
+  __syncthreads();
+
+  f32x4 dqa[QT][4];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dqa[qt][dt] = zero4();
+
+  auto ring = [&](auto bi) -> char* {
+    constexpr int BI = decltype(bi)::value;
+    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
+  };
+  // LDS-DMA of key tile it into slot BI: K and V (two 1 KB pieces each per wave) and, with dropout,
+  // wave 1 the 4 x 128 keep-bit words of this query block (columns past ldm clamped: their queries
+  // are past Tq and never read)
+  auto issue = [&](int it, auto bi) {
+    char* buf = ring(bi);
+    const int k0 = it * FW_KT;
+    dma_rows64(Kg, ldk, k0, Tk, buf, w, lane);
+    dma_rows64(Vg, ldv, k0, Tk, buf + TILE, w, lane);
+    if (DROP && w == 1) {
+      int64_t col = (int64_t)qb * QB + (lane & 15) * 8;
+      col = col < ldm - 8 ? col : ldm - 8;
+      dma16(mrow + ((int64_t)it * 4 + (lane >> 4)) * ldm + col, lds_addr(buf + 2 * TILE));
+    }
+  };
+  auto wait_tile = [&](bool next) {
+    if (!next)
+      wait_vm<0>();
+    else if (DROP && w == 1)
+      wait_vm<5>();
+    else
+      wait_vm<4>();
+  };
+  issue(0, std::integral_constant<int, 0>());
+  if (nkt > 1) issue(1, std::integral_constant<int, 1>());
+
+  auto step = [&](auto bi, int it) {
+    constexpr int BI = decltype(bi)::value;
+    wait_tile(it + 1 < nkt);
+    raw_barrier();
+    if (it + 2 < nkt) issue(it + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    const char* Kl = ring(bi);
+    const char* Vl = Kl + TILE;
+    uint32_t kwd[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      kwd[qt] = 0u;
+      if constexpr (DROP)
+        kwd[qt] = reinterpret_cast<const uint16_t*>(Kl + 2 * TILE)[g * QB + w * 16 * QT + qt * 16 + i];
+    }
+    const bool full = kfull[it] != 0;
+    f32x4 s[4][QT], dp[4][QT];
+    {
+      f32x4 s0[QT], d0[QT];
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        s0[qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
+        d0[qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
+      }
+      RP_PRIO(1);
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 ka = row_frag_lds(Kl, kt * 16, ss * 32, lane);
+          const bf16x8 va = row_frag_lds(Vl, kt * 16, ss * 32, lane);
+#pragma unroll
+          for (int qt = 0; qt < QT; ++qt) {
+            s[kt][qt] = mfma_bf16(ka, qf[qt][ss], ss == 0 ? s0[qt] : s[kt][qt]);
+            dp[kt][qt] = mfma_bf16(va, df[qt][ss], ss == 0 ? d0[qt] : dp[kt][qt]);
+          }
+        }
+      RP_PRIO(0);
+    }
+    if (!full) {  // key bias 0 / -inf from the staged valid bytes of keys kt*16 + 4g + r
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const uint32_t vb = *reinterpret_cast<const uint32_t*>(kvl + it * FW_KT + kt * 16 + 4 * g);
+        f32x4 kb4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) kb4[r] = ((vb >> (8 * r)) & 0xFFu) ? 0.f : -INFINITY;
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) s[kt][qt] += kb4;
+      }
+    }
+    // dS^T = P^T (keep*ds*dP^T - delta) = P^T*ds*(keep ? acc : -delta/ds)
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = rp_exp2(s[kt][qt][r]);
+          if constexpr (DROP) {
+            const uint32_t km = keep_mask(kwd[qt], 4 * kt + r);
+            s[kt][qt][r] = p * bfi_select(km, dp[kt][qt][r], dq[qt]);
+          } else {
+            s[kt][qt][r] = p * dp[kt][qt][r];
+          }
+        }
+    RP_PRIO(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 sa[QT];
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) sa[qt] = pack8(s[2 * ks][qt], s[2 * ks + 1][qt]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 kb = col_frag_lds(Kl, ks * 32, dt * 16, lane);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) dqa[qt][dt] = mfma_bf16(sa[qt], kb, dqa[qt][dt]);
+      }
+    }
+    RP_PRIO(0);
+  };
+  for (int it = 0; it < nkt; it += NBUF) {
+    step(std::integral_constant<int, 0>(), it);
+    if (it + 1 < nkt) step(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < nkt) step(std::integral_constant<int, 2>(), it + 2);
+  }
+  // store: dqa[qt][dt][r] = dQ[q = q0 + qt*16 + 4g + r][dk = dt*16 + i]
+  bf16* dQ = (bf16*)a.dq + (int64_t)b * Tq * a.lddq + h * HD;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + qt * 16 + 4 * g + r;
+      if (q >= Tq) continue;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dQ[(int64_t)q * a.lddq + dt * 16 + i] = (bf16)(dqa[qt][dt][r] * scale);
+    }
+}
+
 // RP_ATTN_BLOCK=64 | 128 forces the workgroup block (queries for fwd / dQ, keys for dK/dV), for tuning
 static int attn_block_override() {
   static int v = -1;
@@ -1516,6 +1774,16 @@ static bool attn_dma_enabled() {
     v = (e && e[0] == '0') ? 0 : 1;
   }
   return v != 0;
+}
+
+// RP_ATTN_DMA_Q=0 selects the register-staged dQ kernel only (A/B tuning)
+static bool attn_dma_q_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_ATTN_DMA_Q");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0 && attn_dma_enabled();
 }
 
 template <typename T>
@@ -1567,10 +1835,18 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
                                            : (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H < 512;
   const bool fused = (phases & 5) == 5;
   if (fused) {
-    if (small)
+    if (small) {
       launch_bwd_q<T, 1>(true, a, s);
-    else
+    } else if (std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX && attn_dma_q_enabled()) {
+      // bf16, 128-query blocks: the LDS-DMA staged dQ kernel (RP_ATTN_DMA=0: register staged)
+      const dim3 grid((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
+      if (a.drop_thresh)
+        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true>), grid, dim3(NT), 0, s, a);
+      else
+        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false>), grid, dim3(NT), 0, s, a);
+    } else {
       launch_bwd_q<T, 2>(true, a, s);
+    }
   } else if (phases & 1) {
     hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
   }
