@@ -62,9 +62,11 @@ __device__ __forceinline__ int lds_off(int row, int byte) {
 }
 
 // keep-bit mask layout (the forward's register layout, so the forward and dQ kernels move one
-// 16-bit word per lane and key tile): [B*H][KT = ceil(T/64)][4 lane groups g][ldm = roundup(T,64)]
+// 16-bit word per lane and key tile): [B*H][KT = ceil(T/64)][4 lane groups g][ldm = roundup(T,128)]
+// (a row covers every query of the last 128-query block, so block-wide stores and DMA pieces of a
+// row never reach the next one)
 // uint16; bit (kt*4 + r) of word (bh, tile, g, q) = keep(q, key = 64*tile + 16*kt + 4*g + r)
-__host__ __device__ inline int64_t mask_ld(int T) { return ((int64_t)T + 63) / 64 * 64; }
+__host__ __device__ inline int64_t mask_ld(int T) { return ((int64_t)T + 127) / 128 * 128; }
 __host__ __device__ inline int mask_kt(int T) { return (T + 63) / 64; }
 
 // ----- problem description (device side of rp_mha_args) ------------------------------------------
@@ -1756,6 +1758,271 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
     }
 }
 
+// =================================================================================================
+// forward — bf16, LDS-DMA staged variant (the default for bf16 with 128-query blocks and
+// Tk <= FD_TKMAX; RP_ATTN_DMA_F=0 selects the register-staged kernel).  Same math, register layouts
+// and outputs as attn_fwd_kernel<bf16, DROP, 2>; the K / V tiles arrive by LDS-DMA in a three-slot
+// ring two tiles ahead (one barrier per tile) instead of registers one tile ahead, and the key-valid
+// bytes of the sequence are staged in LDS once with a per-tile "no masked key" flag.  The keep-bit
+// words are stored for every query of the block (the rows of the mask are padded to 128 queries), so
+// each step issues a fixed number of memory instructions and the counted waits below stay exact
+// (VMEM instructions of a wave complete in issue order).
+// =================================================================================================
+constexpr int FD_TKMAX = 4096;
+
+template <bool DROP>
+__global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
+  constexpr int QT = 2, QB = NW * 16 * QT;  // 128 queries per workgroup
+  using C = AttnCfg<bf16>;
+  constexpr int TILE = FW_KT * C::ROWB;  // 8 KB
+  constexpr int BUF = 2 * TILE;
+  constexpr int NBUF = 3;
+  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
+  __shared__ __attribute__((aligned(16))) uint8_t kvl[FD_TKMAX];
+  __shared__ int kfull[FD_TKMAX / FW_KT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const uint32_t drop_thresh = a.drop_thresh;
+  const float drop_scale = a.drop_scale;
+  const float scale = a.scale;
+  float* __restrict__ lse = a.lse;
+  const int nqb = (Tq + QB - 1) / QB;
+  const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
+  const int bh = L / nqb, qb = L % nqb;
+  const int b = bh / H, h = bh % H;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv;
+  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + h * HD;
+  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + h * HD;
+  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + h * HD;
+  const int q0 = qb * QB + w * 16 * QT;
+  const uint32_t seed_bh = rp_hash(rp_seed_eff(a.seed_base, a.seed), (uint32_t)bh);
+  const float c = scale * LOG2E;
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
+  uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
+  const bool novalid = seq_has_no_key(a, b, tid);
+
+  bf16x8 qf[QT][2];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) qf[qt][s2] = row_frag_gmem(Qg, ldq, q0 + qt * 16, Tq, s2 * 32, lane);
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    if (novalid) qf[qt][0] = qf[qt][1] = bf16x8{};
+    if (!a.qpre) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qt][s2][j] = (bf16)((float)qf[qt][s2][j] * c);
+    }
+  }
+  // key-valid bytes (every key < Tk when the sequence has none: masked_fill semantics) and flags
+  const int nkt = (Tk + FW_KT - 1) / FW_KT;
+  for (int k = tid; k < nkt * FW_KT; k += NT)
+    kvl[k] = k < Tk ? (novalid || a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
+  __syncthreads();
+  for (int t = tid; t < nkt; t += NT) {
+    int ok = 1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t v = reinterpret_cast<const uint32_t*>(kvl)[t * 16 + j];
+      ok &= ((v - 0x01010101u) & ~v & 0x80808080u) == 0u;  // no zero byte
+    }
+    kfull[t] = ok;
+  }
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) asm volatile("" ::"v"(qf[qt][s2]));
+  __syncthreads();
+
+  f32x4 o[QT][4];
+  float m[QT], lp[QT];
+  bool mset[QT];
+  uint32_t dst[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[qt][dt] = zero4();
+    m[qt] = 0.f;
+    lp[qt] = 0.f;
+    mset[qt] = false;
+    dst[qt] = DROP ? rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g) : 0u;
+  }
+
+  auto ring = [&](auto bi) -> char* {
+    constexpr int BI = decltype(bi)::value;
+    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
+  };
+  auto issue = [&](int it, auto bi) {  // K and V of key tile it: two 1 KB pieces each per wave
+    char* buf = ring(bi);
+    dma_rows64(Kg, ldk, it * FW_KT, Tk, buf, w, lane);
+    dma_rows64(Vg, ldv, it * FW_KT, Tk, buf + TILE, w, lane);
+  };
+  // step it waits for DMA(it).  Issued after it, in order: (it >= 2) the 2 keep-bit stores of step
+  // it - 2, DMA(it + 1) (4), the 2 stores of step it - 1 (it >= 1).
+  auto wait_tile = [&](int it) {
+    if (it + 1 >= nkt)
+      wait_vm<0>();
+    else if (!DROP || it == 0)
+      wait_vm<4>();
+    else if (it == 1)
+      wait_vm<6>();
+    else
+      wait_vm<8>();
+  };
+  issue(0, std::integral_constant<int, 0>());
+  if (nkt > 1) issue(1, std::integral_constant<int, 1>());
+
+  auto step = [&](auto bi, int kt_i) {
+    constexpr int BI = decltype(bi)::value;
+    wait_tile(kt_i);
+    raw_barrier();
+    if (kt_i + 2 < nkt) issue(kt_i + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    const char* Kl = ring(bi);
+    const char* Vl = Kl + TILE;
+    const bool full = kfull[kt_i] != 0;
+    // ---- S^T[key][q] = K (cQ)^T - m ----
+    f32x4 s[4][QT];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) s[kt][qt] = f32x4{-m[qt], -m[qt], -m[qt], -m[qt]};
+    RP_PRIO(1);
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 kf = row_frag_lds(Kl, kt * 16, ss * 32, lane);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) s[kt][qt] = mfma_bf16(kf, qf[qt][ss], s[kt][qt]);
+      }
+    RP_PRIO(0);
+    if (!full) {  // key bias 0 / -inf of keys kt*16 + 4g + r
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const uint32_t vb = *reinterpret_cast<const uint32_t*>(kvl + kt_i * FW_KT + kt * 16 + 4 * g);
+        f32x4 kb4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) kb4[r] = ((vb >> (8 * r)) & 0xFFu) ? 0.f : -INFINITY;
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) s[kt][qt] += kb4;
+      }
+    }
+    // ---- column max relative to the reference; deferred rescale (see attn_fwd_kernel) ----
+    float rel[QT];
+    bool grow = false;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      float mx = s[0][qt][0];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][qt][r]);
+      rel[qt] = quad_max(mx);
+      grow |= mset[qt] ? rel[qt] > RESCALE_LOG2 : rel[qt] > -INFINITY;
+    }
+    if (__any(grow)) {
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        const bool gq = mset[qt] ? rel[qt] > RESCALE_LOG2 : rel[qt] > -INFINITY;
+        const float alpha = gq ? (mset[qt] ? rp_exp2(-rel[qt]) : 0.f) : 1.f;
+        const float sub = gq ? rel[qt] : 0.f;
+        lp[qt] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+        m[qt] += sub;
+        mset[qt] = mset[qt] || gq;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) s[kt][qt] -= sub;
+      }
+    }
+    // ---- P = exp2(acc); per-lane partial row sums (before dropout), tree order ----
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      float t4[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[kt][qt][r] = rp_exp2(s[kt][qt][r]);
+        t4[kt] = (s[kt][qt][0] + s[kt][qt][1]) + (s[kt][qt][2] + s[kt][qt][3]);
+      }
+      lp[qt] += (t4[0] + t4[1]) + (t4[2] + t4[3]);
+    }
+    // ---- dropout masks; keep bits stored for every query of the block (padded rows) ----
+    uint32_t dm[QT][8];
+    if constexpr (DROP) {
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        const uint32_t word = drop_masks(dst[qt], drop_thresh, dm[qt]);
+        mrow[((int64_t)kt_i * 4 + g) * ldm + q0 + qt * 16 + i] = (uint16_t)word;
+      }
+    }
+    // ---- O^T[dk][q] += V^T P^T ----
+    bf16x8 pf[QT][2];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        pf[qt][ks] = pack8(s[2 * ks][qt], s[2 * ks + 1][qt]);
+        if constexpr (DROP) {
+          uint4 u = __builtin_bit_cast(uint4, pf[qt][ks]);
+          u.x &= ~dm[qt][4 * ks + 0];
+          u.y &= ~dm[qt][4 * ks + 1];
+          u.z &= ~dm[qt][4 * ks + 2];
+          u.w &= ~dm[qt][4 * ks + 3];
+          pf[qt][ks] = __builtin_bit_cast(bf16x8, u);
+        }
+      }
+    RP_PRIO(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 vf = col_frag_lds(Vl, ks * 32, dt * 16, lane);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) o[qt][dt] = mfma_bf16(vf, pf[qt][ks], o[qt][dt]);
+      }
+    RP_PRIO(0);
+  };
+  for (int it = 0; it < nkt; it += NBUF) {
+    step(std::integral_constant<int, 0>(), it);
+    if (it + 1 < nkt) step(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < nkt) step(std::integral_constant<int, 2>(), it + 2);
+  }
+
+  // ---- epilogue: O[q][dk] = O^T / l ; lse ----
+  const int64_t ldo = a.ldo;
+  bf16* __restrict__ out = (bf16*)a.out;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    const float l = quad_sum(lp[qt]);
+    const int q = q0 + qt * 16 + i;
+    if (q >= Tq) continue;
+    const float inv = drop_scale / l;
+    bf16* orow = out + ((int64_t)b * Tq + q) * ldo + h * HD;
+    bf16* lorow = a.out_lo ? (bf16*)a.out_lo + ((int64_t)b * Tq + q) * ldo + h * HD : nullptr;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x4 v, vl;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = o[qt][dt][r] * inv;
+        v[r] = (bf16)x;
+        vl[r] = (bf16)(x - (float)v[r]);
+      }
+      *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = v;
+      if (lorow) *reinterpret_cast<bf16x4*>(lorow + dt * 16 + 4 * g) = vl;
+    }
+    if (g == 0) lse[(int64_t)bh * Tq + q] = m[qt] * 0.6931471805599453f + logf(l);
+  }
+}
+
 // RP_ATTN_BLOCK=64 | 128 forces the workgroup block (queries for fwd / dQ, keys for dK/dV), for tuning
 static int attn_block_override() {
   static int v = -1;
@@ -1786,6 +2053,16 @@ static bool attn_dma_q_enabled() {
   return v != 0 && attn_dma_enabled();
 }
 
+// RP_ATTN_DMA_F=0 selects the register-staged forward kernel (A/B tuning)
+static bool attn_dma_f_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_ATTN_DMA_F");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0 && attn_dma_enabled();
+}
+
 template <typename T>
 int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
   // 128-query blocks unless that leaves fewer than two workgroups per CU (256 CUs): then 64
@@ -1799,6 +2076,11 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
       hipLaunchKernelGGL((attn_fwd_kernel<T, true, 1>), grid, dim3(NT), 0, s, a);
     else
       hipLaunchKernelGGL((attn_fwd_kernel<T, false, 1>), grid, dim3(NT), 0, s, a);
+  } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX && attn_dma_f_enabled()) {
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_fwd_dma_kernel<true>), grid, dim3(NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_dma_kernel<false>), grid, dim3(NT), 0, s, a);
   } else {
     if (a.drop_thresh)
       hipLaunchKernelGGL((attn_fwd_kernel<T, true, 2>), grid, dim3(NT), 0, s, a);
