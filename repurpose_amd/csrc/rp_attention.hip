@@ -990,7 +990,7 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool DROP, int KTW>
+template <bool DROP, int KTW, bool PIPE>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
   constexpr int KB = NW * 16 * KTW;  // keys per workgroup
   using C = AttnCfg<bf16>;
@@ -1103,9 +1103,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
     const float* drow = lrow + KV_QT;
     const uint16_t* mw = reinterpret_cast<const uint16_t*>(cur + 2 * TILE + 2 * KV_QT * 4);
 
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      f32x4 s[2][KTW], dp[2][KTW], ndq[2], nl[2];
+    // one half = 32 queries: S / dP products (16 MFMAs), the probability / dS VALU, then the dV / dK
+    // products (16 MFMAs) that consume both 16-query rows of the half
+    auto sdp = [&](int hf, f32x4 (&s)[2][KTW], f32x4 (&dp)[2][KTW], f32x4 (&ndq)[2]) {
+      f32x4 nl[2];
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
         const int r0 = (2 * hf + qq) * 16 + 4 * g;
@@ -1126,6 +1127,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
           }
         }
       RP_PRIO(0);
+    };
+    auto prob = [&](int hf, f32x4 (&s)[2][KTW], f32x4 (&dp)[2][KTW], const f32x4 (&ndq)[2], bf16x8 (&pa)[KTW],
+                    bf16x8 (&sa)[KTW]) {
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
         const int qrow = (2 * hf + qq) * 16 + 4 * g;
@@ -1152,12 +1156,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
           }
         }
       }
-      bf16x8 pa[KTW], sa[KTW];
 #pragma unroll
       for (int kt = 0; kt < KTW; ++kt) {
         pa[kt] = pack8(s[0][kt], s[1][kt]);
         sa[kt] = pack8(dp[0][kt], dp[1][kt]);
       }
+    };
+    auto dvdk = [&](int hf, const bf16x8 (&pa)[KTW], const bf16x8 (&sa)[KTW]) {
       RP_PRIO(1);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -1170,6 +1175,27 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
         }
       }
       RP_PRIO(0);
+    };
+    if constexpr (PIPE) {
+      // both halves' S / dP products are issued before the first half's VALU, so the VALU of half 0
+      // runs beside the MFMAs of half 1 and the VALU of half 1 beside the dV / dK MFMAs of half 0
+      f32x4 s0[2][KTW], dp0[2][KTW], nd0[2], s1[2][KTW], dp1[2][KTW], nd1[2];
+      bf16x8 pa0[KTW], sa0[KTW], pa1[KTW], sa1[KTW];
+      sdp(0, s0, dp0, nd0);
+      sdp(1, s1, dp1, nd1);
+      prob(0, s0, dp0, nd0, pa0, sa0);
+      dvdk(0, pa0, sa0);
+      prob(1, s1, dp1, nd1, pa1, sa1);
+      dvdk(1, pa1, sa1);
+    } else {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        f32x4 s[2][KTW], dp[2][KTW], ndq[2];
+        bf16x8 pa[KTW], sa[KTW];
+        sdp(hf, s, dp, ndq);
+        prob(hf, s, dp, ndq, pa, sa);
+        dvdk(hf, pa, sa);
+      }
     }
   };
   for (int it = 0; it < nqt; it += NBUF) {
@@ -2053,6 +2079,17 @@ static bool attn_dma_q_enabled() {
   return v != 0 && attn_dma_enabled();
 }
 
+// RP_ATTN_PIPE=0: the dK/dV kernel processes its two 32-query halves one after the other instead of
+// issuing both halves' S / dP products ahead of the VALU (A/B tuning)
+static bool attn_pipe_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_ATTN_PIPE");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
+
 // RP_ATTN_DMA_F=0 selects the register-staged forward kernel (A/B tuning)
 static bool attn_dma_f_enabled() {
   static int v = -1;
@@ -2138,17 +2175,20 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     const dim3 grid(small_kv ? (unsigned)((a.Tk + NW * 16 - 1) / (NW * 16) * a.B * a.H) : (unsigned)(nkb * a.B * a.H));
     // bf16 with the producer's Q prescale: the LDS-DMA staged kernel (RP_ATTN_DMA=0: register staged)
     if (std::is_same<T, bf16>::value && a.qpre && !a.empty_uniform && attn_dma_enabled()) {
+      const bool pipe = attn_pipe_enabled();
+#define RP_KVD(DROPV, KTWV)                                                                        \
+  do {                                                                                             \
+    if (pipe)                                                                                      \
+      hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<DROPV, KTWV, true>), grid, dim3(NT), 0, s, a);  \
+    else                                                                                           \
+      hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<DROPV, KTWV, false>), grid, dim3(NT), 0, s, a); \
+  } while (0)
       if (small_kv) {
-        if (a.drop_thresh)
-          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<true, 1>), grid, dim3(NT), 0, s, a);
-        else
-          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<false, 1>), grid, dim3(NT), 0, s, a);
+        if (a.drop_thresh) RP_KVD(true, 1); else RP_KVD(false, 1);
       } else {
-        if (a.drop_thresh)
-          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<true, 2>), grid, dim3(NT), 0, s, a);
-        else
-          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<false, 2>), grid, dim3(NT), 0, s, a);
+        if (a.drop_thresh) RP_KVD(true, 2); else RP_KVD(false, 2);
       }
+#undef RP_KVD
     } else if (small_kv) {
       if (a.drop_thresh)
         hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true, 1>), grid, dim3(NT), 0, s, a);
