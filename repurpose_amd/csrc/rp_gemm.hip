@@ -413,10 +413,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64
 // co-resident workgroups hide each other's load latency (qkv fwd 43.1 -> 41.3 us, linear1 fwd
 // 54.3 -> 50.5, K = 512 dgrad into d_ff 64.3 -> 52.8), deeper K on CFG 0 (linear2 fwd 39.5 vs 43.0);
 // CFG 2 lost to CFG 1 everywhere and serves only K % 64 == 32.  In the whole training step, though,
-// CFG 1 on the K = 512, N >= 1536 shapes (RP_GEMM_POLICY=1) measured 20.30 vs 20.15 ms per step
-// (same box, interleaved runs) although each of those kernels ran faster in the kernel trace: the
-// denser 4-workgroup residency costs more in the rest of the step (clock under load) than it saves,
-// so the default policy keeps CFG 0.
+// CFG 1 on the K = 512, N >= 1536 shapes (RP_GEMM_POLICY=1) measured 20.30 vs 20.15 ms per step in
+// round 1 (eager step, per-kernel events inside the timed region); in the graph-replayed step of
+// round 2 it measures 16.03 vs 16.21 ms (three interleaved pairs, one box), so it is the default
+// now (RP_GEMM_POLICY=0 restores CFG 0).  CFG 1 on every short-K shape (N = 512 too) measured the
+// same as on the wide ones only; CFG 1 everywhere (RP_GEMM_CFG=1) 16.52 ms.
 // Rows past M/N are clamped to the last valid row (their outputs are discarded), so the path needs
 // whole BK-deep K steps.
 typedef __attribute__((address_space(3))) void lds_void;
@@ -1078,7 +1079,7 @@ static int rp_gemm_cfg(int64_t kext, int64_t n) {
     const char* e = getenv("RP_GEMM_CFG");
     forced = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
     const char* pe = getenv("RP_GEMM_POLICY");
-    policy = pe ? atoi(pe) : 0;
+    policy = pe ? atoi(pe) : 1;
   }
   if (forced >= 0) return (forced == 2 || kext % 64 == 0) ? forced : 2;
   if (kext % 64 != 0) return 2;
