@@ -1,5 +1,6 @@
 #!/bin/bash
-# round-2 record: full GPU suite, smoke, full bench (with the CPU baseline), rocprof kernel stats
+# Record run: full GPU suite, smoke, full bench (with the CPU baseline), rocprof kernel stats and the
+# per-kernel breakdown of one graph-replayed step.  usage: scripts/gpu_check.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
