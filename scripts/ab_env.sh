@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: scripts/r2_ab_multi.sh ROUNDS STEPS "ENV1" "ENV2" ... : interleaved bench runs per env setting
+# usage: scripts/ab_env.sh ROUNDS STEPS "ENV1" "ENV2" ... : interleaved bench runs per env setting
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 R=$1; ST=$2; shift 2
