@@ -343,8 +343,44 @@ class MMCTransformer(nn.Module):
     @torch.no_grad()
     def inference_(self, batch, inference_settings):
         """Reference ``:231-275``: forward, then per-video selection + Soft-NMS — here one batched
-        launch each (rp_infer_select, rp_softnms) and a single device->host copy of the counts."""
+        launch each (rp_infer_select, rp_softnms) and a single device->host copy of the counts.
+
+        Length buckets: a batch padded to its longest video (the collate of ``main.py`` / config 5)
+        runs as up to four sub-batches of similar valid length, each cut to its own longest video
+        (``RP_INFER_BUCKETS``, default 4; 1 = one padded forward).  Every video's valid frames see the
+        same computation either way (row-wise GEMMs / LayerNorm, key-padding-masked attention, the
+        positional table indexed by the frame), so the proposals are those of the padded forward;
+        the padded frames' work is what is skipped."""
         cfg = inference_settings
+        out = [None] * batch["visual_feats"].shape[0]
+        for rows, tg in self._length_groups(batch["masks"]):
+            sub = batch if rows is None else _sub_batch(batch, rows, tg)
+            res = self._infer_batch(sub, cfg)
+            for j, b in enumerate(rows if rows is not None else range(len(out))):
+                out[b] = res[j]
+        return out
+
+    def _length_groups(self, masks):
+        """[(row indices or None for the whole batch, padded length)] of the inference buckets."""
+        B = masks.shape[0]
+        T = masks.shape[-1]
+        nb = int(os.environ.get("RP_INFER_BUCKETS", "4"))
+        if nb <= 1 or B < 2 * nb:
+            return [(None, T)]
+        mk = masks.reshape(B, T) != 0
+        pos = torch.arange(1, T + 1, device=mk.device)
+        lens = (mk * pos).amax(1).cpu().tolist()  # last valid frame + 1 (0: no valid frame)
+        if min(lens) * 10 >= T * 9:
+            return [(None, T)]
+        order = sorted(range(B), key=lambda b: lens[b])
+        groups = []
+        for g in range(nb):
+            rows = order[g * B // nb:(g + 1) * B // nb]
+            tg = min(T, max(16, (max(lens[b] for b in rows) + 15) // 16 * 16))
+            groups.append((rows, tg))
+        return groups
+
+    def _infer_batch(self, batch, cfg):
         masks, logits, offsets, _, _, _ = self.forward(batch)
         B, T = logits.shape[0], logits.shape[1]
         lg = logits.reshape(B, T)
@@ -361,6 +397,27 @@ class MMCTransformer(nn.Module):
             out.append({"segments": seg[b].index_select(0, sel), "scores": score[b].index_select(0, sel),
                         "labels": idx[b].index_select(0, sel), "video_id": vid, "duration": vlen})
         return out
+
+
+def _sub_batch(batch, rows, tg):
+    """Rows ``rows`` of a padded batch, its frame axis cut to ``tg``: tensors whose first dim is the
+    batch are row-selected (and cut on the axis that has the padded length), lists are picked."""
+    B = batch["visual_feats"].shape[0]
+    T = batch["visual_feats"].shape[1]
+    out = {}
+    for k, v in batch.items():
+        if torch.is_tensor(v) and v.dim() >= 1 and v.shape[0] == B:
+            v = v.index_select(0, torch.tensor(rows, device=v.device))
+            if v.dim() >= 2 and v.shape[1] == T:
+                v = v[:, :tg]
+            elif v.dim() >= 3 and v.shape[2] == T:
+                v = v[:, :, :tg]
+            out[k] = v.contiguous()
+        elif isinstance(v, (list, tuple)) and len(v) == B:
+            out[k] = [v[b] for b in rows]
+        else:
+            out[k] = v
+    return out
 
 
 _SIDE = {}

@@ -68,18 +68,28 @@ def main():
     for dt in ("fp32", "bf16"):
         torch.manual_seed(1234)
         m = exercise_heads(MMCTransformer(**MODEL_CFG, compute_dtype=dt)).to(dev).eval()
-        with torch.no_grad():
-            out = m.inference_(batch, CFG)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(args.reps):
+        outs = {}
+        for nb in os.environ.get("BENCH_INFER_BUCKETS", "1,4").split(","):  # padded forward, then buckets
+            os.environ["RP_INFER_BUCKETS"] = nb
+            with torch.no_grad():
                 out = m.inference_(batch, CFG)
-            torch.cuda.synchronize()
-        dt_s = (time.perf_counter() - t0) / args.reps
-        res[f"gpu_{dt}"] = {"value": args.videos / dt_s, "ms_per_batch": dt_s * 1e3,
-                            "proposals": int(sum(len(o["segments"]) for o in out))}
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(args.reps):
+                    out = m.inference_(batch, CFG)
+                torch.cuda.synchronize()
+            dt_s = (time.perf_counter() - t0) / args.reps
+            key = {"1": f"gpu_{dt}_padded", "4": f"gpu_{dt}"}.get(nb, f"gpu_{dt}_buckets{nb}")
+            res[key] = {"value": args.videos / dt_s, "ms_per_batch": dt_s * 1e3,
+                        "proposals": int(sum(len(o["segments"]) for o in out))}
+            outs[nb] = out
+        os.environ.pop("RP_INFER_BUCKETS")
+        res[f"gpu_{dt}"]["buckets"] = 4
+        res[f"gpu_{dt}"]["identical_to_padded"] = all(
+            torch.equal(a["labels"], b["labels"]) and torch.equal(a["segments"], b["segments"])
+            and torch.equal(a["scores"], b["scores"]) for a, b in zip(outs["1"], outs["4"]))
         if dt == "fp32":
-            gpu_fp32_out = out
+            gpu_fp32_out = outs["4"]
     # CPU restatement on a bounded sample of the same videos
     from oracle.mmct_oracle import MMCTransformer as Oracle
     from bench import host_threads

@@ -52,6 +52,7 @@ def test_test_cfg_is_what_the_gpu_tests_run(cfg):
     assert test_infer_gpu.CFG == cfg["test_cfg"]
     assert val_atiou.CFG == cfg["test_cfg"]
     # every key inference_ / inference_single_video read is in the file
-    src = inspect.getsource(MMCTransformer.inference_) + inspect.getsource(MMCTransformer.inference_single_video)
+    src = "".join(inspect.getsource(f) for f in (MMCTransformer.inference_, MMCTransformer._infer_batch,
+                                                  MMCTransformer.inference_single_video))
     for k in cfg["test_cfg"]:
         assert f'"{k}"' in src, k

@@ -153,3 +153,43 @@ def test_val_split_atiou_matches_cpu_reference(dev):
     assert r["identical_proposals"], r
     assert r["abs_diff"] < 1e-12, r
     assert r["proposals_gpu"] > 0 and r["gt_segments"] > 0
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_length_buckets_give_the_padded_forward_proposals(dev, monkeypatch, dtype):
+    """inference_ on a padded batch of ragged videos runs length buckets (RP_INFER_BUCKETS, default 4):
+    every video's proposals are bit-identical to one padded forward (RP_INFER_BUCKETS=1)."""
+    from repurpose_amd.MMCTransformer import MMCTransformer
+    cfg = dict(vis_dim=512, aud_dim=2048, text_dim=384, d_model=512, self_num_layers=2, text_num_layers=3,
+               cross_num_layers=3, num_heads=8)
+    torch.manual_seed(0)
+    m = MMCTransformer(**cfg, compute_dtype=dtype).to(dev).eval()
+    sd = m.state_dict()
+    with torch.no_grad():
+        sd["cls_head.7.bias"].fill_(0.02)
+        sd["reg_head.7.bias"].fill_(15.0)
+    m.load_state_dict(sd)
+    g = torch.Generator().manual_seed(5)
+    lens = [900, 61, 333, 700, 128, 899, 64, 450, 17, 640]
+    B, T = len(lens), max(lens)
+    mask = (torch.arange(T)[None] < torch.tensor(lens)[:, None]).unsqueeze(1)
+    batch = {"visual_feats": torch.randn(B, T, 512, generator=g), "audio_feats": torch.randn(B, T, 2048, generator=g),
+             "text_feats": torch.randn(B, T, 384, generator=g), "masks": mask, "labels": torch.zeros(B, T),
+             "segments": torch.zeros(B, T, 2)}
+    batch = {k: v.to(dev) for k, v in batch.items()}
+    batch["video_id"] = [f"v{i}" for i in range(B)]
+    batch["duration"] = lens
+    monkeypatch.setenv("RP_INFER_BUCKETS", "1")
+    assert m._length_groups(batch["masks"]) == [(None, T)]
+    ref = m.inference_(batch, CFG)
+    monkeypatch.setenv("RP_INFER_BUCKETS", "4")
+    groups = m._length_groups(batch["masks"])
+    assert len(groups) == 4 and sorted(b for r, _ in groups for b in r) == list(range(B))
+    assert all(tg < T for _, tg in groups[:-1])
+    res = m.inference_(batch, CFG)
+    assert sum(len(r["labels"]) for r in ref) > 0
+    for r, e in zip(res, ref):
+        assert r["video_id"] == e["video_id"] and r["duration"] == e["duration"]
+        assert torch.equal(r["labels"], e["labels"])
+        assert torch.equal(r["segments"], e["segments"])
+        assert torch.equal(r["scores"], e["scores"])
