@@ -204,6 +204,17 @@ typedef struct {
 } rp_colsum_item;
 int rp_colsum_batched(const rp_colsum_item* items, int n_items, void* stream);
 
+/* Sums of squares of many fp32 vectors in one launch: *out_k = sum_i x_k[i]^2, accumulated in fp64
+ * in a fixed order.  Replaces the per-tensor `.grad.norm().item()` host syncs of the trainer's
+ * gradient-norm logging (main.py:345-367); repurpose_amd.gradnorm.grad_norms copies every result
+ * to the host at once.  At most 64 items per call. */
+typedef struct {
+  const float* x;
+  int64_t n;
+  double* out;
+} rp_sumsq_item;
+int rp_sumsq_batched(const rp_sumsq_item* items, int n_items, void* stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Flag or-ed into the dtype argument of every rp_attn_* / rp_mha_* entry point: the q operand
  * already holds Q * scale * log2(e), rounded to the operand dtype (rp_gemm's col_scale epilogue

@@ -49,6 +49,10 @@ class WgradItem(ctypes.Structure):
                 ("ldx", c_i64)]
 
 
+class SumsqItem(ctypes.Structure):
+    _fields_ = [("x", c_vp), ("n", c_i64), ("out", c_vp)]
+
+
 class ColsumItem(ctypes.Structure):
     _fields_ = [("X", c_vp), ("out", c_vp), ("rows", c_i64), ("cols", c_i64), ("ldx", c_i64), ("accumulate", c_i)]
 
@@ -78,6 +82,7 @@ _SIGNATURES = {
     "rp_layernorm_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnBwdArgs), c_vp]),
     "rp_colsum_workspace": (c_i64, [c_i64, c_i64]),
     "rp_colsum_batched": (c_i, [c_vp, c_i, c_vp]),
+    "rp_sumsq_batched": (c_i, [c_vp, c_i, c_vp]),
     "rp_colsum": (c_i, [c_vp, c_i, c_i64, c_i64, c_i64, c_vp, c_vp, c_i, c_vp, c_vp]),
     "rp_attn_dropmask_elems": (c_i64, [c_i, c_i, c_i]),
     "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -273,6 +273,27 @@ def colsum_batched(jobs, accumulate=True):
         N.call("rp_colsum_batched", ctypes.cast(arr, ctypes.c_void_p), len(chunk), _stream(chunk[0][0]))
 
 
+SUMSQ_BATCH_MAX = 64
+
+
+def sumsq_batched(tensors):
+    """fp64 device tensor [len(tensors)]: the sum of squares of every (contiguous fp32) tensor,
+    ceil(len / 64) launches (rp_sumsq_batched); no host synchronisation."""
+    if not tensors:
+        return torch.zeros(0, dtype=torch.float64)
+    _gpu(*tensors)
+    out = torch.empty(len(tensors), dtype=torch.float64, device=tensors[0].device)
+    for c in range(0, len(tensors), SUMSQ_BATCH_MAX):
+        chunk = tensors[c:c + SUMSQ_BATCH_MAX]
+        arr = (N.SumsqItem * len(chunk))()
+        for i, t in enumerate(chunk):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != out.device:
+                raise ValueError("sumsq_batched: contiguous fp32 tensors on one device")
+            arr[i] = N.SumsqItem(_p(t).value, t.numel(), out.data_ptr() + 8 * (c + i))
+        N.call("rp_sumsq_batched", ctypes.cast(arr, ctypes.c_void_p), len(chunk), _stream(chunk[0]))
+    return out
+
+
 # ------------------------------------------------------------------------------------- reductions
 def colsum(X, w=None, out=None, accumulate=False, ws=None):
     """out[c] (+)= sum_r w[r] X[r, c] (deterministic)."""
