@@ -193,3 +193,16 @@ def test_length_buckets_give_the_padded_forward_proposals(dev, monkeypatch, dtyp
         assert torch.equal(r["labels"], e["labels"])
         assert torch.equal(r["segments"], e["segments"])
         assert torch.equal(r["scores"], e["scores"])
+
+
+def test_val_split_atiou_spread_heads_matches_cpu_reference(dev):
+    """The same check with the heads spread (scripts/val_atiou.py heads='spread'): scores straddle
+    the 0.5 threshold (about 4 % of the frames within 0.02 of it) and durations straddle the 10 s
+    filter, so selection, duration filtering and Soft-NMS decide many near-boundary cases."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import val_atiou
+    r = val_atiou.run(videos=24, layers=2, threads=8, heads="spread")
+    assert r["identical_proposals"], r
+    assert r["abs_diff"] < 1e-12, r
+    assert r["proposals_gpu"] > 0
