@@ -161,14 +161,17 @@ def main():
     # device) exist only to rehearse the multi-process path on a one-GPU box
     ndev = max(1, torch.cuda.device_count())
     gpu = local % ndev
-    if world > 1:
+    # RP_BENCH_DP=1 runs the DP path (process group, all-reduce hooks, barriers) even at one rank:
+    # a one-GPU rehearsal of what the driver's N > 1 runs execute over RCCL
+    dp = world > 1 or os.environ.get("RP_BENCH_DP") == "1"
+    if dp:
         torch.cuda.set_device(gpu)
         backend = os.environ.get("RP_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
-    dev = torch.device("cuda", gpu if world > 1 else 0)
+    dev = torch.device("cuda", gpu if dp else 0)
 
     from repurpose_amd import kernels as K
     from repurpose_amd.MMCTransformer import MMCTransformer
@@ -178,7 +181,7 @@ def main():
     torch.manual_seed(1234)
     model = MMCTransformer(**MODEL_CFG, compute_dtype=args.dtype).to(dev).train()
     opt = FusedAdam(model, lr=1e-3, weight_decay=1e-4)
-    reducer = GradAllReducer(model) if world > 1 else None
+    reducer = GradAllReducer(model) if dp else None
     B, T = args.batch, args.seq_len
     batch = synth_batch(B, T, dev, 1000 + rank)
 
@@ -195,7 +198,7 @@ def main():
     # one GPU: the whole step is captured once as a HIP graph and replayed (repurpose_amd/graph.py;
     # fresh dropout streams and the Adam step / LR per replay through a device parameter block); the
     # DP path (N > 1) keeps the eager step, whose all-reduce hooks overlap the backward
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    use_graph = args.graph == "on" or (args.graph == "auto" and not dp)
     if use_graph:
         from repurpose_amd.graph import CapturedTrainStep
         runner = CapturedTrainStep(model, opt, batch, warmup=1, seed=1000 + rank)
@@ -206,14 +209,14 @@ def main():
     for _ in range(max(args.warmup, 2 if use_graph else 0)):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     loss_val = float(loss.item())
@@ -226,7 +229,7 @@ def main():
         eager_step()
     kern = K.timer_stop(detail=True)
     kern_ms = {n: v[0] for n, v in kern.items()}
-    if world > 1:
+    if dp:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
@@ -281,7 +284,7 @@ def main():
             res["cpu_baseline"] = cpu_baseline(T)
             res["speedup_vs_cpu"] = value / res["cpu_baseline"]["value"]
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 
