@@ -50,6 +50,7 @@ struct EpiDev {
   int64_t col_scale_n;  // columns n < col_scale_n are multiplied by col_scale after the bias
   float col_scale;
   int split_major;  // split-K: deal the (split, tile) work items split-major over the XCDs (see tile_split)
+  int prefetch_gate;  // 256-row kernel: touch the tile's bf16 gate lines one K-tile before the epilogue
 };
 
 // Work item of a workgroup: output tile t (XCD-aware: consecutive tiles share an XCD's L2) and, for
@@ -862,6 +863,8 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
 
   const int bimg = wn >> 1, bcol = (wn & 1) * 64;
   const int nk = kend > kbeg ? (int)((kend - kbeg) / 64) : 0;
+  const bool pf = MODE == 0 && ep.prefetch_gate && ep.gate && ep.gate_bf16 && nk >= 2;
+  uint16_t pfd[2] = {0, 0};
   const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
   float bacc[8];
 #pragma unroll
@@ -919,6 +922,19 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) fb0[j][kk] = rb(bi, j, kk * 32);
     if (kt + 1 < nk) fill_a(kt + 1);
+    if (pf && kt == nk - 2) {
+      // the gate (the forward's saved activation, cold by now) read by the epilogue: one 2-byte load
+      // per 128-byte line of the 256 x 256 bf16 tile, two lines per thread, issued after the last
+      // LDS-DMA fill so the counted waits below can leave them in flight into the epilogue
+      const bf16* gb = (const bf16*)ep.gate;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int L = tid * 2 + j, row = L >> 2;
+        const int64_t m = m0 + row < M ? m0 + row : M - 1;
+        const int64_t n = n0 + (L & 3) * 64 < N ? n0 + (L & 3) * 64 : n0;
+        pfd[j] = *(const __attribute__((address_space(1))) uint16_t*)(uintptr_t)(gb + m * ep.ldg + n);
+      }
+    }
     rp_raw_barrier();
     rp_lgkm0();
     __builtin_amdgcn_s_setprio(1);
@@ -980,6 +996,8 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
     if (kt + 2 < nk) {
       fill_b(kt + 2);
       rp_waitcnt<4, 15>();
+    } else if (pf) {
+      rp_waitcnt<2, 15>();  // every fill landed; the two gate loads may stay in flight
     } else {
       rp_waitcnt<0, 15>();
     }
@@ -998,6 +1016,7 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
   if (wm == 0) rp_raw_barrier();  // match the lagging half's barrier count
   __syncthreads();
   gemm8_epilogue<TC, MODE, BNT>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
+  if (pf) asm volatile("" ::"v"(pfd[0]), "v"(pfd[1]));
   if (MODE == 1 && want_bias) {
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);
@@ -1084,6 +1103,16 @@ static int rp_gemm_cfg(int64_t kext, int64_t n) {
   if (forced >= 0) return (forced == 2 || kext % 64 == 0) ? forced : 2;
   if (kext % 64 != 0) return 2;
   return (kext <= 1024 && n >= 1536 && policy == 1) ? 1 : 0;
+}
+
+// RP_GEMM_PF=0 disables the gate-line prefetch of the 256-row kernel (A/B tuning)
+static int rp_gemm_prefetch_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_GEMM_PF");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v;
 }
 
 static bool rp_dma_enabled() {
@@ -1271,6 +1300,7 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
     e.accumulate = ep->accumulate;
     e.col_scale_n = ep->col_scale_n;
     e.col_scale = ep->col_scale;
+    e.prefetch_gate = rp_gemm_prefetch_enabled();
     RP_REQUIRE(e.col_scale_n >= 0 && e.col_scale_n % 8 == 0, "rp_gemm: col_scale_n must be a multiple of 8");
     RP_REQUIRE(!e.accumulate || c_dtype == RP_F32, "rp_gemm: accumulate needs an fp32 C");
     RP_REQUIRE(!e.drop_thresh || M * N < (int64_t)UINT32_MAX, "rp_gemm: dropout index overflow");
