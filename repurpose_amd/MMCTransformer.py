@@ -579,14 +579,16 @@ class _Schedule:
         pending = []  # (event on the side stream, prefixes) not yet announced
 
         # bf16 training: the encoder layers' weight gradients are deferred and computed by grouped
-        # whole-K launches (8 layers x 4 GEMMs = 1536 tiles = three full waves per launch: no split-K
+        # whole-K launches (all 16 layers x 4 GEMMs = 768 256x256 tiles, three per CU: no split-K
         # slabs and no reduce pass).  Under DP a layer's gradient range is announced to the all-reduce
         # hooks once its group has been launched, so the first group's exchange overlaps the backward
         # of the remaining eight layers.
         deferred = [] if (dt == torch.bfloat16 and side is None and M % 64 == 0
                           and os.environ.get("RP_WGRAD_GROUPED", "1") != "0") else None
         held = []  # layer prefixes whose gradients wait for their group launch
-        per_launch = 4 * 8
+        # one launch for the whole encoder on one GPU; groups of 8 layers when gradient hooks (DP
+        # all-reduce) wait for them, so the first group's exchange overlaps the rest of the backward
+        per_launch = 4 * int(os.environ.get("RP_WGRAD_GROUP_LAYERS", "8" if m._grad_ready_hooks else "16"))
 
         # LayerNorm gamma / beta partials: reduced together by one rp_colsum_batched launch per flush
         # (before the gradients they finish are announced, and at the end) instead of one per LayerNorm

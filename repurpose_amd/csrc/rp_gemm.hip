@@ -591,12 +591,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
 
 // ============ grouped weight gradients: many (dY, X) pairs over the same token range ============
 // One launch computes up to WG_MAX weight gradients dW_i = dY_i^T X_i (+ db_i = colsum dY_i) that
-// share the token count K, every 128 x 128 output tile over the WHOLE K range (no split-K slabs,
-// no reduce pass).  The deferred per-layer weight gradients of the encoder (16 layers x {linear2,
-// linear1, out_proj, in_proj} = 192 tiles per layer, 8 layers per launch = 1536 tiles = exactly
-// three waves at two workgroups per CU) are the intended use: the XCD remap deals each XCD 192
-// consecutive tiles, i.e. one layer, whose operand panels its L2 then shares.
-constexpr int WG_MAX = 32;
+// share the token count K, every output tile over the WHOLE K range (no split-K slabs, no reduce
+// pass).  The deferred per-layer weight gradients of the encoder (16 layers x {linear2, linear1,
+// out_proj, in_proj}) are the intended use: by default on 256 x 256 tiles (wgrad8_grouped_kernel
+// below, 48 tiles per layer, all 16 layers = 768 tiles = three per CU), here on 128 x 128 tiles
+// (RP_WGRAD8=0: 192 tiles per layer, 8 layers = 1536 tiles = three waves at two workgroups per CU);
+// the XCD remap deals each XCD consecutive tiles, i.e. whole layers, whose operand panels its L2
+// then shares.
+constexpr int WG_MAX = 64;
 struct WgItem {
   const bf16* dY;
   const bf16* X;
@@ -833,28 +835,19 @@ __device__ __forceinline__ void rp_lgkm0() {
   __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));
 }
 
+// One 256 x BNT output tile over the K range [kbeg, kend): the phased main loop, the epilogue and
+// (bias_dst != null, m-major A) the tile rows' column sums of the staged A: bias_dst[m0 + r] (+)=.
 template <bool AK, bool BKM, typename TC, int MODE, int BNT>
-__global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int64_t K, const bf16* __restrict__ A,
-                                                       int64_t lda, const bf16* __restrict__ B, int64_t ldb,
-                                                       TC* __restrict__ Cout, int64_t ldc, float alpha, EpiDev ep,
-                                                       int64_t kchunk, float* __restrict__ bslab) {
+__device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __restrict__ A, int64_t lda,
+                                           const bf16* __restrict__ B, int64_t ldb, TC* __restrict__ Cout,
+                                           int64_t ldc, float alpha, const EpiDev& ep, int64_t kbeg, int64_t kend,
+                                           int64_t m0, int64_t n0, int split, float* __restrict__ bias_dst,
+                                           int bias_acc, char* lds) {
   static_assert(BNT == 256, "phased 256-row kernel: 256 x 256 tiles");
   using G = G8<BNT, 64, 2>;
-  __shared__ __attribute__((aligned(16))) char lds[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 2, wn = wid & 3;
-  const int tiles_n = (int)((N + BNT - 1) / BNT);
-  const int tiles_m = (int)((M + 255) / 256);
-  int t, split;
-  tile_split<MODE>(tiles_m * tiles_n, ep.split_major, t, split);
-  const int64_t m0 = (int64_t)(t / tiles_n) * 256;
-  const int64_t n0 = (int64_t)(t % tiles_n) * BNT;
-  int64_t kbeg = 0, kend = K;
-  if (MODE == 1) {
-    kbeg = (int64_t)split * kchunk;
-    kend = kbeg + kchunk < K ? kbeg + kchunk : K;
-  }
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -865,7 +858,7 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
   const int nk = kend > kbeg ? (int)((kend - kbeg) / 64) : 0;
   const bool pf = MODE == 0 && ep.prefetch_gate && ep.gate && ep.gate_bf16 && nk >= 2;
   uint16_t pfd[2] = {0, 0};
-  const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
+  const bool want_bias = !AK && bias_dst != nullptr;
   float bacc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
@@ -1017,7 +1010,7 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
   __syncthreads();
   gemm8_epilogue<TC, MODE, BNT>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
   if (pf) asm volatile("" ::"v"(pfd[0]), "v"(pfd[1]));
-  if (MODE == 1 && want_bias) {
+  if (want_bias) {
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);
 #pragma unroll
@@ -1027,9 +1020,51 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
       const int h = tid >> 7, cg = (tid & 127) >> 3, e = tid & 7;
       float sum = 0.f;
       for (int r = 0; r < 16; ++r) sum += red[((h << 8) + cg + 16 * r) * 8 + e];
-      bslab[(int64_t)split * M + m0 + tid] = sum;
+      bias_dst[m0 + tid] = bias_acc ? bias_dst[m0 + tid] + sum : sum;
     }
   }
+}
+
+template <bool AK, bool BKM, typename TC, int MODE, int BNT>
+__global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int64_t K, const bf16* __restrict__ A,
+                                                       int64_t lda, const bf16* __restrict__ B, int64_t ldb,
+                                                       TC* __restrict__ Cout, int64_t ldc, float alpha, EpiDev ep,
+                                                       int64_t kchunk, float* __restrict__ bslab) {
+  __shared__ __attribute__((aligned(16))) char lds[G8<BNT, 64, 2>::LDS];
+  const int tiles_n = (int)((N + BNT - 1) / BNT);
+  const int tiles_m = (int)((M + 255) / 256);
+  int t, split;
+  tile_split<MODE>(tiles_m * tiles_n, ep.split_major, t, split);
+  const int64_t m0 = (int64_t)(t / tiles_n) * 256;
+  const int64_t n0 = (int64_t)(t % tiles_n) * BNT;
+  int64_t kbeg = 0, kend = K;
+  if (MODE == 1) {
+    kbeg = (int64_t)split * kchunk;
+    kend = kbeg + kchunk < K ? kbeg + kchunk : K;
+  }
+  float* bias_dst = (MODE == 1 && bslab != nullptr && n0 == 0) ? bslab + (int64_t)split * M : nullptr;
+  gemm8_tile<AK, BKM, TC, MODE, BNT>(M, N, A, lda, B, ldb, Cout, ldc, alpha, ep, kbeg, kend, m0, n0, split, bias_dst, 0,
+                                     lds);
+}
+
+// grouped weight gradients on 256 x 256 tiles (the WgGroup of wgrad_grouped_kernel, whole K): twice
+// the MFMA work per staged operand byte of the 128 x 128 tile, which the whole-K L2 -> LDS stream of
+// the grouped launch is bound by; one workgroup of 8 waves per CU
+__global__ __launch_bounds__(NT8, 1) void wgrad8_grouped_kernel(const WgGroup g) {
+  __shared__ __attribute__((aligned(16))) char lds[G8<256, 64, 2>::LDS];
+  const int t = rp_xcd_remap(blockIdx.x, g.tiles_total);
+  int k = 0;
+  while (k + 1 < g.n && t >= g.start[k + 1]) ++k;
+  const WgItem w = g.it[k];
+  const int local = t - g.start[k];
+  const int tiles_n = (w.N + 255) / 256;
+  const int64_t m0 = (int64_t)(local / tiles_n) * 256;
+  const int64_t n0 = (int64_t)(local % tiles_n) * 256;
+  EpiDev ep{};
+  ep.gate_scale = 1.f;
+  ep.accumulate = g.accumulate;
+  gemm8_tile<false, false, float, 0, 256>(w.M, w.N, w.dY, w.ldy, w.X, w.ldx, w.dW, w.N, 1.f, ep, 0, g.K, m0, n0, 0,
+                                          n0 == 0 ? w.db : nullptr, g.accumulate, lds);
 }
 
 // 256-row phased path selection.  RP_GEMM8=0 disables it, RP_GEMM8=1 forces it wherever legal
@@ -1103,6 +1138,16 @@ static int rp_gemm_cfg(int64_t kext, int64_t n) {
   if (forced >= 0) return (forced == 2 || kext % 64 == 0) ? forced : 2;
   if (kext % 64 != 0) return 2;
   return (kext <= 1024 && n >= 1536 && policy == 1) ? 1 : 0;
+}
+
+// RP_WGRAD8=0: the grouped weight gradients on 128 x 128 tiles instead of 256 x 256 (A/B tuning)
+static bool rp_wgrad8_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_WGRAD8");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
 }
 
 // RP_GEMM_PF=0 disables the gate-line prefetch of the 256-row kernel (A/B tuning)
@@ -1327,6 +1372,7 @@ extern "C" int rp_gemm_wgrad_grouped(int64_t K, const rp_wgrad_item* items, int 
   g.accumulate = accumulate;
   g.K = K;
   int64_t tiles = 0;
+  const bool big = rp_wgrad8_enabled();  // 256 x 256 tiles (wgrad8_grouped_kernel)
   for (int i = 0; i < n_items; ++i) {
     const rp_wgrad_item& it = items[i];
     RP_REQUIRE(it.M > 0 && it.N > 0 && it.M % 8 == 0 && it.N % 8 == 0 && it.ldy % 8 == 0 && it.ldx % 8 == 0 &&
@@ -1339,12 +1385,15 @@ extern "C" int rp_gemm_wgrad_grouped(int64_t K, const rp_wgrad_item* items, int 
     g.start[i] = (int)tiles;
     g.it[i] = WgItem{(const bf16*)it.dY, (const bf16*)it.X, it.dW, it.db, (int)it.M, (int)it.N, (int)it.ldy,
                      (int)it.ldx};
-    tiles += ((it.M + BM - 1) / BM) * ((it.N + BN - 1) / BN);
+    tiles += big ? ((it.M + 255) / 256) * ((it.N + 255) / 256) : ((it.M + BM - 1) / BM) * ((it.N + BN - 1) / BN);
   }
   RP_REQUIRE(tiles < (1 << 30), "rp_gemm_wgrad_grouped: too many tiles");
   g.start[n_items] = (int)tiles;
   g.tiles_total = (int)tiles;
-  hipLaunchKernelGGL(wgrad_grouped_kernel, dim3((unsigned)tiles), dim3(NT), 0, (hipStream_t)stream, g);
+  if (big)
+    hipLaunchKernelGGL(wgrad8_grouped_kernel, dim3((unsigned)tiles), dim3(NT8), 0, (hipStream_t)stream, g);
+  else
+    hipLaunchKernelGGL(wgrad_grouped_kernel, dim3((unsigned)tiles), dim3(NT), 0, (hipStream_t)stream, g);
   return rp_check_launch("rp_gemm_wgrad_grouped");
 }
 

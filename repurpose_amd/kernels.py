@@ -166,13 +166,13 @@ def linear_wgrad(dy, x, dW, db=None, accumulate=True, ws=None):
     return dW
 
 
-WGRAD_GROUP_MAX = 32  # items per rp_gemm_wgrad_grouped launch
+WGRAD_GROUP_MAX = 64  # items per rp_gemm_wgrad_grouped launch
 
 
 def linear_wgrad_grouped(items, accumulate=True):
     """dW_i (+)= dy_i^T x_i, db_i (+)= colsum(dy_i) for items [(dy, x, dW, db)], all bf16 operands over
     the same token count T (a multiple of 64): whole-K tiles, no split-K workspace (rp_gemm_wgrad_grouped).
-    Launches ceil(len / 32) kernels."""
+    Launches ceil(len / 64) kernels."""
     if not items:
         return
     T = items[0][0].shape[0]

@@ -488,7 +488,7 @@ def test_colsum_batched_equals_per_item(dev):
 def test_wgrad_grouped_whole_k(dev):
     """rp_gemm_wgrad_grouped: several (dY, X) pairs of different shapes over one token range in one
     launch (whole-K tiles, bias from the staged dY tiles), strided dY views, items without a bias,
-    accumulate and overwrite modes, deterministic; 33 items -> two launches."""
+    accumulate and overwrite modes, deterministic; 70 items -> two launches (64 per launch)."""
     T = 1216  # a multiple of 64, not of 128
     shapes = [(512, 2048), (2048, 512), (512, 512), (1536, 512), (256, 136), (8, 64)]
     items, refs = [], []
@@ -508,8 +508,8 @@ def test_wgrad_grouped_whole_k(dev):
             close(db, rb, atol=tol, what=f"grouped bias {tuple(db.shape)}")
     outs = []
     for _ in range(2):
-        its = [(dy, x, torch.empty_like(dW), None) for dy, x, dW, _ in items] * 6  # 36 items: two launches
-        its = its[:33]
+        its = [(dy, x, torch.empty_like(dW), None) for dy, x, dW, _ in items] * 12  # 72 items
+        its = its[:70]
         K.linear_wgrad_grouped(its, accumulate=False)
         outs.append([w for _, _, w, _ in its])
     for a, b in zip(*outs):
