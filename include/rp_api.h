@@ -229,7 +229,8 @@ enum { RP_ATTN_Q_PRESCALED = 0x100 };
 /* Multi-head self attention, flash-style (no T x T materialisation).
  * qkv: [B*T, 3*H*dk] rows = (q heads | k heads | v heads), dk == 64.
  * key_valid: [B, T] uint8 (0 -> key masked with -inf, torch key_padding_mask semantics).
- * out: [B*T, H*dk];  lse: [B, H, T] fp32 (natural-log sum-exp of scaled scores).
+ * out: [B*T, H*dk];  lse: [B, H, T] fp32 (natural-log sum-exp of scaled scores; bf16 with dropout
+ * sums the bf16-rounded probabilities the P.V product uses, on the matrix core).
  * out_lo (bf16, optional): bf16(O - bf16(O)), the rounding residual of out, for the backward's
  * delta = rowsum(dout * O) (pass the same pointer to the backward; NULL: delta from out alone).
  * Dropout on the attention probabilities with probability p: for query q and group g one stream
