@@ -399,6 +399,14 @@ class MMCTransformer(nn.Module):
         return out
 
 
+def _mask_u8(masks, B, T):
+    """[B, T] uint8 key-valid bytes of a [B, 1, T] mask: a zero-copy view of a contiguous bool mask
+    (torch stores bool as 0 / 1 bytes), otherwise one conversion."""
+    if masks.dtype == torch.bool and masks.is_contiguous():
+        return masks.reshape(B, T).view(torch.uint8)
+    return (masks.reshape(B, T) != 0).to(torch.uint8).contiguous()
+
+
 def _sub_batch(batch, rows, tg):
     """Rows ``rows`` of a padded batch, its frame axis cut to ``tg``: tensors whose first dim is the
     batch are row-selected (and cut on the axis that has the padded length), lists are picked."""
@@ -492,7 +500,7 @@ class _Schedule:
             raise ValueError(f"sequence length {T} exceeds the positional table "
                              f"({m.positional_encoding.pe.shape[1]})")
         self._lp = m.lowp_weights() if dt != _F32 else None
-        kv = (self.masks.reshape(B, T) != 0).to(torch.uint8).contiguous()
+        kv = _mask_u8(self.masks, B, T)
         self.kv = kv
         scale = 1.0 / math.sqrt(d // H)
         self.scale = scale

@@ -32,7 +32,10 @@ def focal_loss_masked_sum(out_cls_logits, gt_cls_labels, masks, alpha=0.7, gamma
     """sum_{b,t} masks[b,0,t] * sigmoid_focal_loss(logits[b,t,0], labels[b,t])."""
     B = out_cls_logits.shape[0]
     T = out_cls_logits.shape[1]
-    m = (masks.reshape(B, T) != 0).to(torch.uint8).reshape(-1)
+    if masks.dtype == torch.bool and masks.is_contiguous():
+        m = masks.reshape(-1).view(torch.uint8)  # zero-copy: bool is stored as 0 / 1 bytes
+    else:
+        m = (masks.reshape(B, T) != 0).to(torch.uint8).reshape(-1)
     return _FocalMaskedSum.apply(out_cls_logits, gt_cls_labels.float(), m, alpha, gamma)
 
 
