@@ -973,7 +973,7 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
           acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb1[j][kk], acc[4 + i][2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     rp_raw_barrier();
-    // ---- phase 3: no fragment reads; B pieces of K-tile kt+2; own pieces of K-tile kt+1 landed ----
+    // ---- phase 3: no fragment reads; B pieces of K-tile kt+2; own pieces of K-tile kt+1 landed by its end ----
     if (want_bias) {  // wgrad bias: column sums of the staged m-major dY tile, 4 x 16 B per thread
       const char* hi = cur + (tid >> 8) * G::HB;
       const int cg = tid & 15;
@@ -986,14 +986,7 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
       }
       rp_lgkm0();  // retired before the barrier after which the next A pieces may overwrite them
     }
-    if (kt + 2 < nk) {
-      fill_b(kt + 2);
-      rp_waitcnt<4, 15>();
-    } else if (pf) {
-      rp_waitcnt<2, 15>();  // every fill landed; the two gate loads may stay in flight
-    } else {
-      rp_waitcnt<0, 15>();
-    }
+    if (kt + 2 < nk) fill_b(kt + 2);
     rp_raw_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1004,6 +997,15 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
         for (int j = 0; j < 2; ++j)
           acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb0[j][kk], acc[4 + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+    // the wave's own pieces of K-tile kt+1 landed before the last barrier of the K-tile, after which
+    // K-tile kt+1 is read (waiting here rather than before this phase's first barrier gives the fills
+    // the phase's MFMA segment as well)
+    if (kt + 2 < nk)
+      rp_waitcnt<4, 15>();  // only B(kt+2) may stay in flight
+    else if (pf)
+      rp_waitcnt<2, 15>();  // every fill landed; the two gate loads may stay in flight
+    else
+      rp_waitcnt<0, 15>();
     rp_raw_barrier();
   }
   if (wm == 0) rp_raw_barrier();  // match the lagging half's barrier count
