@@ -496,11 +496,13 @@ def adam_step(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, p_lp=None, 
     kernel reads its coefficients from device memory when it runs (graph replay) and the host
     hyper-parameters are not used."""
     _gpu(p, g, m, v, p_lp, coef_dev)
+    e0 = _tick("adam")
     if coef_dev is not None:
         N.call("rp_adam_step_dev", _p(p), _p(g), _p(m), _p(v), p.numel(), _p(coef_dev), _p(p_lp), _stream(p))
-        return
-    N.call("rp_adam_step", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
-           float(eps), float(weight_decay), int(step), _p(p_lp), _stream(p))
+    else:
+        N.call("rp_adam_step", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
+               float(eps), float(weight_decay), int(step), _p(p_lp), _stream(p))
+    _tock(e0)
 
 
 def adam_coefficients(lr, beta1, beta2, eps, weight_decay, step):
