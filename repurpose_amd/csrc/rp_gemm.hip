@@ -987,6 +987,19 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
       rp_lgkm0();  // retired before the barrier after which the next A pieces may overwrite them
     }
     if (kt + 2 < nk) fill_b(kt + 2);
+    // every wave's pieces of K-tile kt+1 must have landed by barrier event 8kt+8 (G0's clock), after
+    // which the leading half reads K-tile kt+1.  That event is the leading half's LAST barrier of
+    // this K-tile but the lagging half's FIRST barrier of this phase: the lagging half waits here,
+    // the leading half after this phase's MFMA segment (which gives its fills that segment too)
+    auto wait_next = [&]() {
+      if (kt + 2 < nk)
+        rp_waitcnt<4, 15>();  // only B(kt+2) may stay in flight
+      else if (pf)
+        rp_waitcnt<2, 15>();  // every fill landed; the two gate loads may stay in flight
+      else
+        rp_waitcnt<0, 15>();
+    };
+    if (wm == 1) wait_next();
     rp_raw_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -997,15 +1010,7 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
         for (int j = 0; j < 2; ++j)
           acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb0[j][kk], acc[4 + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
-    // the wave's own pieces of K-tile kt+1 landed before the last barrier of the K-tile, after which
-    // K-tile kt+1 is read (waiting here rather than before this phase's first barrier gives the fills
-    // the phase's MFMA segment as well)
-    if (kt + 2 < nk)
-      rp_waitcnt<4, 15>();  // only B(kt+2) may stay in flight
-    else if (pf)
-      rp_waitcnt<2, 15>();  // every fill landed; the two gate loads may stay in flight
-    else
-      rp_waitcnt<0, 15>();
+    if (wm == 0) wait_next();
     rp_raw_barrier();
   }
   if (wm == 0) rp_raw_barrier();  // match the lagging half's barrier count

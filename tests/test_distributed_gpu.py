@@ -133,5 +133,5 @@ def test_ddp_two_ranks_real_backward(dev, dtype):
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    for rank, msg in sorted(res):
-        assert msg == "ok", f"rank {rank}: {msg}"
+    bad = [f"rank {rank}: {msg}" for rank, msg in sorted(res) if msg != "ok"]
+    assert not bad, "\n".join(bad)
