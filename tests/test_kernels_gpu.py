@@ -612,24 +612,28 @@ def test_attention_metric_shape_bf16_dropout(dev):
         assert torch.count_nonzero(dk[bb, hh][~valid]) == 0 and torch.count_nonzero(dv[bb, hh][~valid]) == 0
 
 
-def test_wgrad_grouped_repeat_bitwise(dev):
+@pytest.mark.parametrize("T", [128, 192, 4096])
+def test_wgrad_grouped_repeat_bitwise(dev, T):
     """Race guard for the 256-row kernel's LDS-DMA pipeline: the grouped weight gradients of the
-    encoder's four shapes over a long token range (K = 4096, 64 K-tiles per tile), relaunched eight
-    times, are bitwise identical every time (a fill read before it lands shows up as a differing
-    launch) and match fp64."""
-    T = 4096
+    encoder's four shapes, relaunched eight times, are bitwise identical every time and every launch
+    matches fp64 (a K-tile read before its fills land gives O(1) errors).  Short token ranges (two and
+    three K-tiles, the DDP test's T = 128) leave the fills the least time to land."""
     shapes = [(512, 2048), (2048, 512), (512, 512), (1536, 512)] * 2
     items = []
     for i, (n_out, n_in) in enumerate(shapes):
         dy = rnd(T, n_out, dev=dev, seed=300 + i).to(torch.bfloat16)
         x = rnd(T, n_in, dev=dev, seed=400 + i).to(torch.bfloat16)
         items.append((dy, x, torch.empty(n_out, n_in, device=dev), torch.empty(n_out, device=dev)))
-    runs = []
+    refs = [(dy.double().T @ x.double(), dy.double().sum(0)) for dy, x, _, _ in items]
+    first = None
     for _ in range(8):
         K.linear_wgrad_grouped(items, accumulate=False)
-        runs.append([torch.cat([w.reshape(-1), b]) for _, _, w, b in items])
-    for r in runs[1:]:
-        for a, b in zip(runs[0], r):
-            assert torch.equal(a, b)
-    dy, x, w, b = items[0]
-    close(w, dy.double().T @ x.double(), atol=1e-3 * math.sqrt(T), what="grouped wgrad K=4096")
+        got = [torch.cat([w.reshape(-1), b]) for _, _, w, b in items]
+        for (_, _, w, b), (rw, rb) in zip(items, refs):
+            close(w, rw, atol=1e-3 * math.sqrt(T), what=f"grouped wgrad T={T}")
+            close(b, rb, atol=1e-3 * math.sqrt(T), what=f"grouped bias T={T}")
+        if first is None:
+            first = got
+        else:
+            for a, c in zip(first, got):
+                assert torch.equal(a, c)
