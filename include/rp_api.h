@@ -86,6 +86,8 @@ typedef struct rp_gemm_epilogue {
   int64_t col_scale_n; /* multiple of 8; 0 = off.  The Q columns of the QKV projection use it to emit
                           Q * scale * log2(e) for the attention kernels (RP_ATTN_Q_PRESCALED) */
   float col_scale;
+  const uint32_t* seed_base; /* optional device word: dropout draws with rp_hash(*seed_base, dropout_seed)
+                                (see "Graph-replayable dropout" below); NULL: dropout_seed as is */
 } rp_gemm_epilogue;
 
 int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int a_kmajor,
@@ -143,6 +145,7 @@ typedef struct rp_ln_fwd_args {
   int64_t ld_out_lp;
   float* mean;
   float* rstd;
+  const uint32_t* seed_base; /* optional, as rp_gemm_epilogue.seed_base */
 } rp_ln_fwd_args;
 
 int rp_layernorm_fwd(int64_t rows, int64_t D, const rp_ln_fwd_args* a, void* stream);
@@ -181,6 +184,7 @@ typedef struct rp_ln_bwd_args {
   float* dgamma_part;
   float* dbeta_part;
   int64_t ld_part;
+  const uint32_t* seed_base; /* optional, as rp_gemm_epilogue.seed_base (both dropout_seed and dx_lp_seed) */
 } rp_ln_bwd_args;
 
 int64_t rp_layernorm_bwd_blocks(int64_t rows);
@@ -285,6 +289,7 @@ typedef struct rp_mha_args {
   int empty_rows_uniform;  /* a sequence with no valid key attends uniformly to ALL its keys (output =
                               mean of V, dq = dk = 0): models/transformer.py's masked_fill(-1e9) semantics.
                               0 = torch key_padding_mask semantics (-inf: such rows are NaN) */
+  const uint32_t* seed_base; /* optional, as rp_gemm_epilogue.seed_base (forward dropout stream seed) */
 } rp_mha_args;
 
 int64_t rp_mha_dropmask_elems(int B, int Tq, int Tk, int H);
@@ -293,8 +298,8 @@ int rp_mha_fwd(int dtype, const rp_mha_args* args, void* stream);
  * dQ kernel, which then runs before dK/dV (7 = all: fused dQ + delta, then dK/dV). */
 int rp_mha_bwd(int dtype, const rp_mha_args* args, int phases, void* stream);
 int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk,
-                float scale, float dropout_p, uint32_t seed, void* out, void* out_lo, float* lse,
-                uint16_t* dropmask, void* stream);
+                float scale, float dropout_p, uint32_t seed, const uint32_t* seed_base, void* out, void* out_lo,
+                float* lse, uint16_t* dropmask, void* stream);
 /* Backward; dqkv: [B*T, 3*H*dk] (fully overwritten); delta_ws: [3, B, H, T] fp32 workspace (plane 0:
  * delta = rowsum(dout * O); planes 1, 2: the dK/dV kernel's row constants -delta/(1/(1-p)) and
  * -lse*log2(e) + log2(1/(1-p)), written by whichever call formed delta).
@@ -355,12 +360,12 @@ int rp_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, co
 
 /* ---------------------------------------------------------------------------------------- */
 /* Graph-replayable dropout streams (the captured training step, repurpose_amd/graph.py).
- * rp_set_seed_base(ptr): while ptr != NULL, every launch that draws dropout (rp_gemm epilogue,
- * rp_layernorm_fwd/bwd, attention forward) records ptr in its kernel arguments and draws with the
- * seed rp_hash(*ptr, seed) — *ptr read when the kernel RUNS — instead of `seed`, so one captured
- * launch gives a fresh stream per replay once the host rewrites the word.  Process-wide (the
- * autograd backward launches from another thread); NULL (the default) restores plain seeds. */
-int rp_set_seed_base(const uint32_t* dev_ptr);
+ * Every launch that draws dropout (rp_gemm epilogue, rp_layernorm_fwd/bwd, rp_attn_fwd / rp_mha_fwd)
+ * takes an optional device word `seed_base` in its own arguments: when it is non-NULL the kernel
+ * draws with the seed rp_hash(*seed_base, seed) — *seed_base read when the kernel RUNS — instead of
+ * `seed`, so one captured launch gives a fresh stream per replay once the host rewrites the word.
+ * The pointer travels per call: the library keeps no process-wide dropout state (two models, or an
+ * eager step beside a captured one, never share a stream).  4-byte aligned. */
 
 /* ---------------------------------------------------------------------------------------- */
 /* Inference.  rp_infer_select: per video b (one workgroup), prob = sigmoid(logit)*mask,

@@ -135,6 +135,7 @@ class MMCTransformer(nn.Module):
         self._layout = None
         self._grad_ready_hooks = []   # called with (lo, hi) flat ranges whose gradients are final
         self._grad_done_hooks = []    # called once at the end of backward
+        self._seed_base = None        # int32 device word while a step is captured (graph.py), else None
         self._build_flat()
         for p in self.parameters():
             _OWNERS[id(p)] = self
@@ -464,7 +465,8 @@ class _Schedule:
         self.scale_drop = 1.0 / (1.0 - self.p) if self.p > 0 else 1.0
         self.dt = model.compute_dtype
         self.base_seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if train else 0
-        self.device_seeds = K.seed_base_active()
+        # graph capture (graph.py): the model's device seed word, passed to every dropout launch
+        self.sb = model._seed_base
         self.saved = None
 
     # ---- parameter access ----
@@ -489,7 +491,7 @@ class _Schedule:
         if not self.train:
             return 0
         # graph-replayable mode (graph.py): the kernels mix the site with the device base word
-        return site if self.device_seeds else _mix(self.base_seed, site)
+        return site if self.sb is not None else _mix(self.base_seed, site)
 
     # ---- forward ----
     def forward(self, save):
@@ -523,16 +525,16 @@ class _Schedule:
             # bf16 training: the output's rounding residual too, so the backward's rowsum(dO * O) is
             # that of the unrounded output
             olo = torch.empty(M, d, device=qkv.device, dtype=dt) if (save and dt != _F32) else None
-            o, lse, dmask = K.attn_fwd(qkv, kv, B, T, H, scale, p, self.seed(100 + 4 * l), q_prescaled=True,
+            o, lse, dmask = K.attn_fwd(qkv, kv, B, T, H, scale, p, self.seed(100 + 4 * l), seed_base=self.sb, q_prescaled=True,
                                        out_lo=olo)
             x1 = K.linear_fwd(o, self.W(pre + "self_attn.out_proj.weight"), self.P(pre + "self_attn.out_proj.bias"),
-                              out_dtype=_F32, dropout_p=p, seed=self.seed(101 + 4 * l), residual=x)
+                              out_dtype=_F32, dropout_p=p, seed=self.seed(101 + 4 * l), seed_base=self.sb, residual=x)
             _, h2, mu2, rs2 = K.layernorm_fwd(x1, self.P(pre + "norm2.weight"), self.P(pre + "norm2.bias"),
                                               out_f32=False, lp_dtype=dt, save_stats=save)
             f = K.linear_fwd(h2, self.W(pre + "linear1.weight"), self.P(pre + "linear1.bias"), relu=True,
-                             dropout_p=p, seed=self.seed(102 + 4 * l))
+                             dropout_p=p, seed=self.seed(102 + 4 * l), seed_base=self.sb)
             x2 = K.linear_fwd(f, self.W(pre + "linear2.weight"), self.P(pre + "linear2.bias"), out_dtype=_F32,
-                              dropout_p=p, seed=self.seed(103 + 4 * l), residual=x1)
+                              dropout_p=p, seed=self.seed(103 + 4 * l), seed_base=self.sb, residual=x1)
             if save:
                 layers.append((x, h1, mu1, rs1, qkv, o, olo, lse, dmask, x1, h2, mu2, rs2, f))
             x = x2
@@ -540,22 +542,22 @@ class _Schedule:
                                          out_f32=False, lp_dtype=dt, save_stats=save)
         z = K.linear_fwd(e, self.W("feature_map.0.weight"), self.P("feature_map.0.bias"), out_dtype=_F32)
         feats, _, muF, rsF = K.layernorm_fwd(z, self.P("feature_map.1.weight"), self.P("feature_map.1.bias"),
-                                             relu=True, dropout_p=p, seed=self.seed(1), save_stats=save)
+                                             relu=True, dropout_p=p, seed=self.seed(1), seed_base=self.sb, save_stats=save)
         # cls head
         _, c0, muC, rsC = K.layernorm_fwd(feats, self.P("cls_head.0.weight"), self.P("cls_head.0.bias"),
                                           out_f32=False, lp_dtype=dt, save_stats=save)
         c1 = K.linear_fwd(c0, self.W("cls_head.1.weight"), self.P("cls_head.1.bias"), relu=True, dropout_p=p,
-                          seed=self.seed(2))
+                          seed=self.seed(2), seed_base=self.sb)
         c2 = K.linear_fwd(c1, self.W("cls_head.4.weight"), self.P("cls_head.4.bias"), relu=True, dropout_p=p,
-                          seed=self.seed(3))
+                          seed=self.seed(3), seed_base=self.sb)
         logits = K.rowdot_fwd(c2, self.P("cls_head.7.weight"), self.P("cls_head.7.bias"))
         # reg head (forward only: no loss reaches it in the reference trainer)
         _, r0, _, _ = K.layernorm_fwd(feats, self.P("reg_head.0.weight"), self.P("reg_head.0.bias"),
                                       out_f32=False, lp_dtype=dt, save_stats=False)
         r1 = K.linear_fwd(r0, self.W("reg_head.1.weight"), self.P("reg_head.1.bias"), relu=True, dropout_p=p,
-                          seed=self.seed(4))
+                          seed=self.seed(4), seed_base=self.sb)
         r2 = K.linear_fwd(r1, self.W("reg_head.4.weight"), self.P("reg_head.4.bias"), relu=True, dropout_p=p,
-                          seed=self.seed(5))
+                          seed=self.seed(5), seed_base=self.sb)
         offsets = K.rowdot_fwd(r2, self.P("reg_head.7.weight"), self.P("reg_head.7.bias"), relu=True)
         if save:
             self.saved = dict(xin=xin, proj=proj, mu0=mu0, rs0=rs0, layers=layers, xL=x, e=e, muE=muE, rsE=rsE,
@@ -664,13 +666,13 @@ class _Schedule:
                                  dgamma=G("cls_head.0.weight"), dbeta=G("cls_head.0.bias"), ws=ws, defer=cs)
         # feature_map: LN + ReLU + dropout, then Linear
         _, dz = K.layernorm_bwd(dfe, S["z"], S["muF"], S["rsF"], self.P("feature_map.1.weight"), y=S["feats"],
-                                dropout_p=p, seed=self.seed(1), want_f32=False, lp_dtype=dt,
+                                dropout_p=p, seed=self.seed(1), seed_base=self.sb, want_f32=False, lp_dtype=dt,
                                 dgamma=G("feature_map.1.weight"), dbeta=G("feature_map.1.bias"), ws=ws, defer=cs)
         wgrad(dz, S["e"], "feature_map.0.weight", "feature_map.0.bias")
         de = K.linear_dgrad(dz, self.W("feature_map.0.weight"), out_dtype=_F32)
         # encoder_norm; emit the masked lp gradient for the last layer's dropout2
         dx, g2 = K.layernorm_bwd(de, S["xL"], S["muE"], S["rsE"], self.P("encoder_norm.weight"), lp_dtype=dt,
-                                 lp_dropout_p=p, lp_seed=self.seed(103 + 4 * (L - 1)),
+                                 lp_dropout_p=p, lp_seed=self.seed(103 + 4 * (L - 1)), seed_base=self.sb,
                                  dgamma=G("encoder_norm.weight"), dbeta=G("encoder_norm.bias"), ws=ws, defer=cs)
         ready(["encoder_norm.", "feature_map.", "cls_head."])
         for l in reversed(range(L)):
@@ -684,7 +686,7 @@ class _Schedule:
             dh2 = K.linear_dgrad(dzf, self.W(pre + "linear1.weight"), out_dtype=_F32)
             # norm2 + residual; masked lp gradient for dropout1
             dx1, g1 = K.layernorm_bwd(dh2, x1, mu2, rs2, self.P(pre + "norm2.weight"), dres=dx, lp_dtype=dt,
-                                      lp_dropout_p=p, lp_seed=self.seed(101 + 4 * l),
+                                      lp_dropout_p=p, lp_seed=self.seed(101 + 4 * l), seed_base=self.sb,
                                       dgamma=G(pre + "norm2.weight"), dbeta=G(pre + "norm2.bias"), ws=ws, defer=cs)
             # out_proj
             wgrad(g1, o, pre + "self_attn.out_proj.weight", pre + "self_attn.out_proj.bias")
@@ -699,7 +701,7 @@ class _Schedule:
             last = l == 0
             dx, g2 = K.layernorm_bwd(dh1, x, mu1, rs1, self.P(pre + "norm1.weight"), dres=dx1,
                                      lp_dtype=None if last else dt, lp_dropout_p=0.0 if last else p,
-                                     lp_seed=0 if last else self.seed(103 + 4 * (l - 1)),
+                                     lp_seed=0 if last else self.seed(103 + 4 * (l - 1)), seed_base=self.sb,
                                      dgamma=G(pre + "norm1.weight"), dbeta=G(pre + "norm1.bias"), ws=ws, defer=cs)
             ready([pre])
         if deferred:

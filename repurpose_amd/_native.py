@@ -24,14 +24,14 @@ class GemmEpilogue(ctypes.Structure):
     _fields_ = [("bias", c_vp), ("relu", c_i), ("dropout_p", c_f), ("dropout_seed", c_u32),
                 ("residual", c_vp), ("ldr", c_i64), ("gate", c_vp), ("gate_dtype", c_i),
                 ("ldg", c_i64), ("gate_scale", c_f), ("accumulate", c_i), ("col_scale_n", c_i64),
-                ("col_scale", c_f)]
+                ("col_scale", c_f), ("seed_base", c_vp)]
 
 
 class LnFwdArgs(ctypes.Structure):
     _fields_ = [("x", c_vp), ("x_dtype", c_i), ("ldx", c_i64), ("gamma", c_vp), ("beta", c_vp),
                 ("eps", c_f), ("pe", c_vp), ("pe_period", c_i64), ("relu", c_i), ("dropout_p", c_f),
                 ("dropout_seed", c_u32), ("out_f32", c_vp), ("ld_out_f32", c_i64), ("out_lp", c_vp),
-                ("out_lp_dtype", c_i), ("ld_out_lp", c_i64), ("mean", c_vp), ("rstd", c_vp)]
+                ("out_lp_dtype", c_i), ("ld_out_lp", c_i64), ("mean", c_vp), ("rstd", c_vp), ("seed_base", c_vp)]
 
 
 class LnBwdArgs(ctypes.Structure):
@@ -41,7 +41,7 @@ class LnBwdArgs(ctypes.Structure):
                 ("dres", c_vp), ("lddres", c_i64), ("dx_f32", c_vp), ("lddx", c_i64), ("dx_lp", c_vp),
                 ("dx_lp_dtype", c_i), ("lddx_lp", c_i64), ("dx_lp_dropout_p", c_f),
                 ("dx_lp_seed", c_u32), ("dgamma_part", c_vp), ("dbeta_part", c_vp),
-                ("ld_part", c_i64)]
+                ("ld_part", c_i64), ("seed_base", c_vp)]
 
 
 class WgradItem(ctypes.Structure):
@@ -63,7 +63,7 @@ class MhaArgs(ctypes.Structure):
                 ("scale", c_f), ("dropout_p", c_f), ("seed", c_u32), ("out", c_vp), ("ldo", c_i64), ("lse", c_vp),
                 ("dropmask", c_vp), ("dout", c_vp), ("lddo", c_i64), ("dq", c_vp), ("lddq", c_i64), ("dk", c_vp),
                 ("lddk", c_i64), ("dv", c_vp), ("lddv", c_i64), ("delta_ws", c_vp), ("out_lo", c_vp),
-                ("empty_rows_uniform", c_i)]
+                ("empty_rows_uniform", c_i), ("seed_base", c_vp)]
 
 
 # name -> (restype, argtypes); mirrors include/rp_api.h one to one
@@ -85,7 +85,7 @@ _SIGNATURES = {
     "rp_sumsq_batched": (c_i, [c_vp, c_i, c_vp]),
     "rp_colsum": (c_i, [c_vp, c_i, c_i64, c_i64, c_i64, c_vp, c_vp, c_i, c_vp, c_vp]),
     "rp_attn_dropmask_elems": (c_i64, [c_i, c_i, c_i]),
-    "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rp_attn_bwd": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp,
                           c_vp, c_vp, c_vp]),
     "rp_attn_bwd_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_vp, c_vp]),
@@ -109,7 +109,6 @@ _SIGNATURES = {
     "rp_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_f, c_f, c_f, c_i, c_vp, c_vp]),
     "rp_adam_coefficients": (c_i, [c_f, c_f, c_f, c_f, c_f, c_i, c_vp]),
     "rp_adam_step_dev": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
-    "rp_set_seed_base": (c_i, [c_vp]),
     "rp_infer_select": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_f, c_i, c_f, c_f, c_vp, c_vp, c_vp, c_vp,
                               c_vp]),
     "rp_softnms_workspace": (c_i64, [c_i, c_i]),

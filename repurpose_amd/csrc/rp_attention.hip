@@ -80,7 +80,7 @@ struct MhaDev {
   int B, Tq, Tk, H;
   float scale;
   uint32_t drop_thresh; float drop_scale; uint32_t seed;
-  const uint32_t* seed_base;  // graph-replayable dropout (rp_set_seed_base), or null
+  const uint32_t* seed_base;  // graph-replayable dropout base word (the launch's seed_base argument), or null
   void* out; int64_t ldo;
   void* out_lo;  // bf16: O - bf16(O) rounded to bf16 (same layout as out), or null
   float* lse;
@@ -2247,7 +2247,8 @@ int make_dev(const char* fn, int dtype, int qpre, const rp_mha_args* p, int phas
   a.q = p->q; a.k = p->k; a.v = p->v; a.ldq = p->ldq; a.ldk = p->ldk; a.ldv = p->ldv;
   a.kvalid = p->key_valid; a.B = p->B; a.Tq = p->Tq; a.Tk = p->Tk; a.H = p->H; a.scale = p->scale;
   a.drop_thresh = thr; a.drop_scale = p->dropout_p > 0.f ? 1.f / (1.f - p->dropout_p) : 1.f; a.seed = p->seed;
-  a.seed_base = thr ? g_rp_seed_base : nullptr;
+  a.seed_base = thr ? p->seed_base : nullptr;
+  RP_REQUIRE(!a.seed_base || ((uintptr_t)a.seed_base & 3u) == 0, "%s: misaligned seed_base", fn);
   a.out = p->out; a.ldo = p->ldo; a.lse = p->lse; a.dmask = thr ? p->dropmask : nullptr;
   a.out_lo = dtype == RP_BF16 ? p->out_lo : nullptr;
   a.empty_uniform = p->empty_rows_uniform != 0;
@@ -2298,12 +2299,13 @@ int mha_bwd_entry(int flagged, const rp_mha_args* p, int phases, void* stream) {
 
 // packed self-attention (qkv [B*T, 3*H*dk]) -> general description
 rp_mha_args packed(const void* qkv, const uint8_t* kv, int B, int T, int H, int dk, float scale, float p, uint32_t seed,
-                   const void* out, const void* out_lo, float* lse, const uint16_t* dmask, const void* dout, void* dqkv,
+                   const uint32_t* seed_base, const void* out, const void* out_lo, float* lse, const uint16_t* dmask, const void* dout, void* dqkv,
                    float* delta) {
   rp_mha_args a{};
   const int64_t ld = 3LL * H * dk, lo = (int64_t)H * dk;
   a.q = qkv; a.k = qkv; a.v = qkv; a.ldq = a.ldk = a.ldv = ld;
   a.key_valid = kv; a.B = B; a.Tq = T; a.Tk = T; a.H = H; a.head_dim = dk; a.scale = scale; a.dropout_p = p; a.seed = seed;
+  a.seed_base = seed_base;
   a.out = const_cast<void*>(out); a.ldo = lo; a.lse = lse; a.dropmask = const_cast<uint16_t*>(dmask);
   a.out_lo = const_cast<void*>(out_lo);
   a.dout = dout; a.lddo = lo; a.delta_ws = delta;
@@ -2338,11 +2340,11 @@ extern "C" int rp_mha_bwd(int dtype, const rp_mha_args* args, int phases, void* 
 }
 
 extern "C" int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
-                           float dropout_p, uint32_t seed, void* out, void* out_lo, float* lse, uint16_t* dropmask,
-                           void* stream) {
+                           float dropout_p, uint32_t seed, const uint32_t* seed_base, void* out, void* out_lo,
+                           float* lse, uint16_t* dropmask, void* stream) {
   RP_REQUIRE(dk == HD, "rp_attn_fwd: head dim %d unsupported (64)", dk);
   RP_REQUIRE(qkv, "rp_attn_fwd: null qkv");
-  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, seed, out, out_lo, lse, dropmask, nullptr,
+  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, seed, seed_base, out, out_lo, lse, dropmask, nullptr,
                          nullptr, nullptr);
   packed_offsets(a, attn_dtype(dtype));
   return mha_fwd_entry(dtype, &a, stream);
@@ -2353,7 +2355,7 @@ static int attn_bwd_packed(int phases, int dtype, const void* qkv, const void* o
                            float dropout_p, const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream) {
   RP_REQUIRE(dk == HD, "rp_attn_bwd: head dim %d unsupported (64)", dk);
   RP_REQUIRE(qkv && dqkv, "rp_attn_bwd: null qkv / dqkv");
-  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, 0, out, out_lo, const_cast<float*>(lse),
+  rp_mha_args a = packed(qkv, key_valid, B, T, H, dk, scale, dropout_p, 0, nullptr, out, out_lo, const_cast<float*>(lse),
                          dropmask, dout, dqkv, delta_ws);
   packed_offsets(a, attn_dtype(dtype));
   return mha_bwd_entry(dtype, &a, phases, stream);

@@ -92,11 +92,10 @@ __device__ __forceinline__ uint32_t rp_keep_bits(uint32_t seed, uint32_t idx0, u
   }
 }
 
-// Graph-replayable dropout streams (rp_set_seed_base): while the process-wide base pointer is set,
-// launchers copy it into their kernel arguments and the kernels draw with rp_hash(*base, seed), the
-// base word read on the device when the kernel runs (a captured HIP graph replays with whatever the
-// host last wrote there); with no base the seed argument is used as is.
-extern const uint32_t* g_rp_seed_base;
+// Graph-replayable dropout streams: a launch's optional seed_base argument (per call, never process
+// state) goes into its kernel arguments and the kernels draw with rp_hash(*base, seed), the base word
+// read on the device when the kernel runs (a captured HIP graph replays with whatever the host last
+// wrote there); with no base the seed argument is used as is.
 __device__ __forceinline__ uint32_t rp_seed_eff(const uint32_t* base, uint32_t seed) {
   return base ? rp_hash(*base, seed) : seed;
 }

@@ -39,7 +39,7 @@ struct EpiDev {
   uint32_t drop_thresh;
   float drop_scale;
   uint32_t drop_seed;
-  const uint32_t* seed_base;  // graph-replayable dropout (rp_set_seed_base), or null
+  const uint32_t* seed_base;  // graph-replayable dropout base word (the launch's seed_base argument), or null
   const float* residual;
   int64_t ldr;
   const void* gate;
@@ -828,9 +828,14 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
 // 64-127, phase 3 nothing.  Two LDS slots of one K-tile (A 2 x 16 KiB + B 2 x 16 KiB).
 // Slot reuse (barrier b(8t + j) = the j-th barrier of K-tile t's phases, G0's clock): the B
 // images of K-tile t are dead after b(8t+4), the A images after b(8t+6); the B pieces of K-tile
-// t+2 are issued in phase 3 of K-tile t, the A pieces of K-tile t+1 in phase 0 of K-tile t, and
-// every wave waits for its own pieces of K-tile t+1 (vmcnt(4): only B(t+2) may stay in flight)
-// before phase 3's first barrier, which every reader of K-tile t+1 passes afterwards.
+// t+2 are issued in phase 3 of K-tile t, the A pieces of K-tile t+1 in phase 0 of K-tile t.
+// INVARIANT (cross-wave: each wave's wait covers only its OWN fills): every fill piece of K-tile
+// t+1 has landed by G0-clock barrier b(8t+8), the first barrier any wave passes before reading
+// K-tile t+1.  b(8t+8) is the LEADING half's last barrier of K-tile t and the LAGGING half's first
+// barrier of phase 3, so the lagging half (waves 4-7) waits (vmcnt(4): only B(t+2) may stay in
+// flight) before its phase-3 first barrier and the leading half (waves 0-3) before its phase-3
+// SECOND barrier — both are event b(8t+8).  Moving either wait later lets a wave read K-tile t+1
+// before another wave's pieces land (the round-2 race, caught by the wgrad/dgrad relaunch tests).
 __device__ __forceinline__ void rp_lgkm0() {
   __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));
 }
@@ -1342,7 +1347,7 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
     e.drop_thresh = rp_dropout_thresh(ep->dropout_p);
     e.drop_scale = ep->dropout_p > 0.f ? 1.f / (1.f - ep->dropout_p) : 1.f;
     e.drop_seed = ep->dropout_seed;
-    e.seed_base = e.drop_thresh ? g_rp_seed_base : nullptr;
+    e.seed_base = e.drop_thresh ? ep->seed_base : nullptr;
     e.residual = ep->residual;
     e.ldr = ep->ldr;
     e.gate = ep->gate;

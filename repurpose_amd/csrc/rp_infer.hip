@@ -301,6 +301,13 @@ extern "C" int rp_softnms(const float* scores, const float* segs, const int* cou
   hipStream_t st = (hipStream_t)stream;
   if (cap <= NMS_LDS_CAP) {
     const size_t lds = (size_t)5 * (cap > 0 ? cap : 1) * sizeof(float);
+    if (lds > 65536) {  // above 64 KiB of dynamic LDS (up to 120 KiB of the CU's 160): opt the kernel in
+      static const hipError_t opt = hipFuncSetAttribute((const void*)softnms_kernel<false>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        (int)(5 * NMS_LDS_CAP * sizeof(float)));
+      RP_REQUIRE(opt == hipSuccess, "rp_softnms: cannot enable %zu bytes of dynamic LDS: %s", lds,
+                 hipGetErrorString(opt));
+    }
     hipLaunchKernelGGL(softnms_kernel<false>, dim3(B), dim3(NMS_THREADS), lds, st, scores, segs, count, cap, sigma,
                        thresh, max_seg, keep, keep_count, final_scores, (float*)nullptr);
   } else {

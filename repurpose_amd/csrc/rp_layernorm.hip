@@ -93,7 +93,7 @@ struct LnFwdDev {
   const float* gamma; const float* beta; float eps;
   const float* pe; int64_t pe_period;
   int relu; uint32_t drop_thresh; float drop_scale; uint32_t drop_seed;
-  const uint32_t* seed_base;  // graph-replayable dropout (rp_set_seed_base), or null
+  const uint32_t* seed_base;  // graph-replayable dropout base word (the launch's seed_base argument), or null
   float* out_f32; int64_t ld_out_f32;
   void* out_lp; int out_lp_dtype; int64_t ld_out_lp;
   float* mean; float* rstd;
@@ -151,7 +151,7 @@ struct LnBwdDev {
   float* dx; int64_t lddx;
   void* dx_lp; int dx_lp_dtype; int64_t lddx_lp;
   uint32_t lp_thresh; float lp_scale; uint32_t lp_seed;
-  const uint32_t* seed_base;  // graph-replayable dropout (rp_set_seed_base), or null
+  const uint32_t* seed_base;  // graph-replayable dropout base word (the launch's seed_base argument), or null
   float* dgamma_part; float* dbeta_part; int64_t ld_part;
 };
 
@@ -269,7 +269,7 @@ extern "C" int rp_layernorm_fwd(int64_t rows, int64_t D, const rp_ln_fwd_args* p
   a.drop_thresh = rp_dropout_thresh(p->dropout_p);
   a.drop_scale = p->dropout_p > 0.f ? 1.f / (1.f - p->dropout_p) : 1.f;
   a.drop_seed = p->dropout_seed;
-  a.seed_base = a.drop_thresh ? g_rp_seed_base : nullptr;
+  a.seed_base = a.drop_thresh ? p->seed_base : nullptr;
   a.out_f32 = p->out_f32; a.ld_out_f32 = p->ld_out_f32;
   a.out_lp = p->out_lp; a.out_lp_dtype = p->out_lp_dtype; a.ld_out_lp = p->ld_out_lp;
   a.mean = p->mean; a.rstd = p->rstd;
@@ -298,7 +298,7 @@ extern "C" int rp_layernorm_bwd(int64_t rows, int64_t D, const rp_ln_bwd_args* p
   a.lp_thresh = rp_dropout_thresh(p->dx_lp_dropout_p);
   a.lp_scale = p->dx_lp_dropout_p > 0.f ? 1.f / (1.f - p->dx_lp_dropout_p) : 1.f;
   a.lp_seed = p->dx_lp_seed;
-  a.seed_base = (a.drop_thresh || a.lp_thresh) ? g_rp_seed_base : nullptr;
+  a.seed_base = (a.drop_thresh || a.lp_thresh) ? p->seed_base : nullptr;
   a.dgamma_part = p->dgamma_part; a.dbeta_part = p->dbeta_part;
   a.ld_part = p->ld_part ? p->ld_part : D;
   RP_REQUIRE(a.ld_part >= D, "rp_layernorm_bwd: ld_part < D");

@@ -24,14 +24,6 @@ int rp_check_launch(const char* what) {
 
 extern "C" int rp_version(void) { return 1; }
 
-const uint32_t* g_rp_seed_base = nullptr;
-
-extern "C" int rp_set_seed_base(const uint32_t* dev_ptr) {
-  RP_REQUIRE(dev_ptr == nullptr || (((uintptr_t)dev_ptr) & 3u) == 0, "rp_set_seed_base: misaligned pointer");
-  g_rp_seed_base = dev_ptr;
-  return RP_OK;
-}
-
 extern "C" int rp_last_error(char* buf, size_t n) {
   if (!buf || n == 0) return RP_ERR_ARG;
   strncpy(buf, g_err, n - 1);

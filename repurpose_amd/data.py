@@ -28,6 +28,7 @@ from . import kernels as K
 
 _NP_DT = {np.dtype(np.float16): N.RP_F16, np.dtype(np.float32): N.RP_F32, np.dtype(np.float64): N.RP_F64,
           np.dtype(np.int64): N.RP_I64}
+_TORCH_DT = {torch.float16: N.RP_F16, torch.float32: N.RP_F32, torch.float64: N.RP_F64, torch.int64: N.RP_I64}
 
 
 def load_features(path):
@@ -104,31 +105,49 @@ class RaggedBatch:
     offsets: dict                   # name -> np.ndarray int64 [B+1]
     extra: dict = field(default_factory=dict)
 
+    def pin(self):
+        """This batch with every row array in page-locked host memory (what a DataLoader's pin_memory
+        thread does off the training loop); ``to_device`` then issues the H2D copies straight away."""
+        rows = {k: (v if torch.is_tensor(v) and v.is_pinned() else torch.from_numpy(np.ascontiguousarray(v)).pin_memory())
+                for k, v in self.rows.items()}
+        offs = {k: (v if torch.is_tensor(v) and v.is_pinned() else torch.from_numpy(np.asarray(v, dtype=np.int64)).pin_memory())
+                for k, v in self.offsets.items()}
+        return RaggedBatch(self.video_id, self.duration, rows, offs, dict(self.extra))
+
     def to_device(self, device, padding_val=0.0):
         """collate_fn's dict with every tensor on ``device``: one pinned H2D copy per modality, then
-        rp_pad_rows pads and converts on the GPU."""
+        rp_pad_rows pads and converts on the GPU (all enqueued on the current stream)."""
         if not torch.device(device).type == "cuda":
             raise RuntimeError("RaggedBatch.to_device: the device path needs a ROCm device (use collate_fn on CPU)")
         B = len(self.video_id)
-        vlens = np.diff(self.offsets["visual"])
+        host_offs = {k: (v.numpy() if torch.is_tensor(v) else np.asarray(v)) for k, v in self.offsets.items()}
+        vlens = np.diff(host_offs["visual"])
         T = int(vlens.max()) if B else 0
         if T == 0:
             raise ValueError("All sequences in the batch have zero length")
-        if int(np.diff(self.offsets["segments"]).max()) == 0:
+        if int(np.diff(host_offs["segments"]).max()) == 0:
             raise ValueError("All segments in the batch have zero length")
         out = {"video_id": self.video_id, "duration": self.duration}
         names = {"visual": "visual_feats", "audio": "audio_feats", "text": "text_feats", "labels": "labels",
                  "segments": "segments"}
         for name, key in names.items():
-            rows = np.ascontiguousarray(self.rows[name])
-            offs = self.offsets[name]
+            rows = self.rows[name]
+            offs = host_offs[name]
             if np.any(np.diff(offs) > T):
                 raise ValueError(f"{name}: a sequence is longer than the visual padding length {T}")
+            if torch.is_tensor(rows) and rows.is_pinned():
+                hsrc, code = rows, _TORCH_DT[rows.dtype]
+            else:
+                rows = np.ascontiguousarray(rows)
+                hsrc, code = torch.from_numpy(rows).pin_memory(), _NP_DT[rows.dtype]
+            hoff = self.offsets[name]
+            if not (torch.is_tensor(hoff) and hoff.is_pinned()):
+                hoff = torch.from_numpy(offs.astype(np.int64)).pin_memory()
             D = rows.shape[1] if rows.ndim > 1 else 1
-            src = torch.from_numpy(rows).pin_memory().to(device, non_blocking=True)
-            off = torch.from_numpy(offs.astype(np.int64)).pin_memory().to(device, non_blocking=True)
+            src = hsrc.to(device, non_blocking=True)
+            off = hoff.to(device, non_blocking=True)
             dst = torch.empty(B, T, D, device=device, dtype=torch.float32)
-            N.call("rp_pad_rows", ctypes.c_void_p(src.data_ptr()), _NP_DT[rows.dtype], ctypes.c_void_p(off.data_ptr()),
+            N.call("rp_pad_rows", ctypes.c_void_p(src.data_ptr()), code, ctypes.c_void_p(off.data_ptr()),
                    B, T, D, float(padding_val), ctypes.c_void_p(dst.data_ptr()), K._stream(dst))
             out[key] = dst.view(B, T) if name == "labels" else dst
         lens_dev = torch.from_numpy(vlens.astype(np.int64)).to(device, non_blocking=True)

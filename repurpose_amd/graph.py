@@ -9,16 +9,27 @@ current stream, which is the capture stream) and replays it with one ``hipGraphL
 What changes per step without re-capture lives in one small device block that the host rewrites
 (pinned staging slot -> async H2D on the step's stream) before each replay:
 
-* word 0 — the dropout base (``rp_set_seed_base``): every dropout launch of the captured step
-  draws with ``rp_hash(base, site)``, so each replay has fresh dropout streams;
+* word 0 — the dropout base: while the step is captured the model hands this word to every dropout
+  launch as its ``seed_base`` argument (per call: the library keeps no dropout state, so another
+  model in the process, or an eager step between replays, keeps its own streams), and each captured
+  launch draws with ``rp_hash(base, site)`` — each replay has fresh dropout streams;
 * words 1..6 — the Adam coefficients ``rp_adam_coefficients(lr, betas, eps, wd, step)``
   (``rp_adam_step_dev``), computed on the host from the optimizer's current ``param_groups`` and
   step count, so LR schedulers and the bias correction behave exactly as in eager mode (the
   updates are bitwise those of ``rp_adam_step`` with the same coefficients).
 
 The batch tensors given at construction are the graph's static inputs: ``load(batch)`` copies a new
-batch of the same shape into them.  Requirements: a ``FusedAdam`` optimizer, one device, no
-gradient all-reduce hooks inside the captured region (the DP path keeps the eager step).
+batch of the same shape into them.  Requirements: a ``FusedAdam`` optimizer, one device, at least
+one eager warm-up step (it allocates the Adam moments and binds the gradient views outside the
+capture: allocations or fills captured into the graph would re-run on every replay).
+
+Data parallel (``capture_collectives=True``): the gradient all-reduce hooks of a
+``distributed.GradAllReducer`` over RCCL (``backend="nccl"``) are captured with the rest of the
+step — every bucket's ``ncclAllReduce`` becomes a graph node on RCCL's stream, forked from and
+joined back into the step's stream at the points the eager backward issues and waits for it — so
+an N-rank step is one ``hipGraphLaunch`` per rank, the same execution mode as one GPU.  The
+warm-up steps run the collectives eagerly first (communicator set-up is not capturable).  A gloo
+reducer (CPU collectives) cannot be captured: it raises.
 """
 import numpy as np
 import torch
@@ -30,12 +41,22 @@ _SLOTS = 4  # pinned staging slots: the host runs at most this many steps ahead 
 
 
 class CapturedTrainStep:
-    def __init__(self, model, optimizer, batch, loss_fn=None, warmup=2, seed=None):
+    def __init__(self, model, optimizer, batch, loss_fn=None, warmup=2, seed=None, capture_collectives=False):
         if not isinstance(optimizer, FusedAdam):
             raise TypeError("CapturedTrainStep needs repurpose_amd.optim.FusedAdam (device-side coefficients)")
-        if model._grad_ready_hooks or model._grad_done_hooks:
-            raise RuntimeError("CapturedTrainStep: gradient all-reduce hooks are registered; the DP step stays "
-                               "eager (collectives are not captured)")
+        if int(warmup) < 1:
+            raise ValueError("CapturedTrainStep: warmup must be >= 1 (the first step allocates the Adam moments "
+                             "and binds the gradient buffer; captured allocations would re-run every replay)")
+        hooks = list(model._grad_ready_hooks) + list(model._grad_done_hooks)
+        if hooks:
+            if not capture_collectives:
+                raise RuntimeError("CapturedTrainStep: gradient all-reduce hooks are registered; pass "
+                                   "capture_collectives=True to capture the RCCL all-reduces with the step")
+            for h in hooks:
+                owner = getattr(h, "__self__", None)
+                if getattr(owner, "backend", None) != "nccl":
+                    raise RuntimeError("CapturedTrainStep: only RCCL (backend 'nccl') gradient all-reduces can be "
+                                       f"captured; got hook {h!r} (backend {getattr(owner, 'backend', None)!r})")
         self.model, self.opt = model, optimizer
         self.batch = batch
         self.loss_fn = loss_fn or (lambda m, out: m.losses(*out)["cls_loss"] / out[1].shape[0])
@@ -89,16 +110,19 @@ class CapturedTrainStep:
         stream = torch.cuda.current_stream(self.device)
         self._stage(stream)
         g = torch.cuda.CUDAGraph()
-        K.set_seed_base(self._dev[0:1])
+        self.model._seed_base = self._dev[0:1]
         self.opt._coef_dev = self._coef
         step0 = self.opt._step
         try:
             # the pool is private to the graph; the eager warm-up steps ran on the caller's stream
             torch.cuda.synchronize(self.device)
-            with torch.cuda.graph(g):
+            # with RCCL hooks: thread-local capture mode, so the process group's watchdog thread may
+            # keep querying its own (uncaptured) events while this thread captures
+            mode = "thread_local" if self.model._grad_ready_hooks else "global"
+            with torch.cuda.graph(g, capture_error_mode=mode):
                 self._loss = self._eager()
         finally:
-            K.set_seed_base(None)
+            self.model._seed_base = None
             self.opt._coef_dev = None
         self.opt._step = step0  # capture executed nothing; replay() counts the step
         self._graph = g

@@ -113,22 +113,24 @@ def cast_bf16(src, dst):
 # ------------------------------------------------------------------------------------- GEMM
 def gemm(A, B, C, M, Nn, K, lda, a_kmajor, ldb, b_kmajor, ldc, alpha=1.0, bias=None, relu=False,
          dropout_p=0.0, seed=0, residual=None, ldr=0, gate=None, ldg=0, gate_scale=1.0,
-         accumulate=False, col_scale_n=0, col_scale=1.0):
-    """Raw rp_gemm (see include/rp_api.h for the operand conventions)."""
+         accumulate=False, col_scale_n=0, col_scale=1.0, seed_base=None):
+    """Raw rp_gemm (see include/rp_api.h for the operand conventions).  ``seed_base``: optional int32
+    device word; the dropout then draws with rp_hash(*seed_base, seed), read when the kernel runs."""
     _gpu(A, B, C, bias, residual, gate)
+    _seed_word(seed_base)
     if A.dtype != B.dtype:
         raise TypeError("rp_gemm: A and B must share a dtype")
     ep = N.GemmEpilogue(_p(bias).value, int(relu), float(dropout_p), int(seed) & 0xFFFFFFFF,
                         _p(residual).value, int(ldr), _p(gate).value,
                         _dt(gate) if gate is not None else 0, int(ldg), float(gate_scale),
-                        int(accumulate), int(col_scale_n), float(col_scale))
+                        int(accumulate), int(col_scale_n), float(col_scale), _p(seed_base).value)
     N.call("rp_gemm", _dt(A), int(M), int(Nn), int(K), _p(A), int(lda), int(a_kmajor), _p(B), int(ldb),
            int(b_kmajor), _p(C), int(ldc), _dt(C), float(alpha), ctypes.byref(ep), _stream(A))
     return C
 
 
 def linear_fwd(x, W, b=None, out_dtype=None, relu=False, dropout_p=0.0, seed=0, residual=None, tag=None,
-               col_scale_n=0, col_scale=1.0):
+               col_scale_n=0, col_scale=1.0, seed_base=None):
     """y = epilogue(x W^T + b); x [M, K], W [N, K] (same dtype), residual fp32 [M, N]; columns
     < col_scale_n are multiplied by col_scale after the bias (the attention's Q prescale)."""
     M, K = x.shape
@@ -136,7 +138,7 @@ def linear_fwd(x, W, b=None, out_dtype=None, relu=False, dropout_p=0.0, seed=0, 
     out = torch.empty(M, Nn, device=x.device, dtype=out_dtype or x.dtype)
     e0 = _tick(tag) if tag else None
     gemm(x, W, out, M, Nn, K, K, True, K, True, Nn, bias=b, relu=relu, dropout_p=dropout_p,
-         seed=seed, residual=residual, ldr=Nn, col_scale_n=col_scale_n, col_scale=col_scale)
+         seed=seed, residual=residual, ldr=Nn, col_scale_n=col_scale_n, col_scale=col_scale, seed_base=seed_base)
     _tock(e0)
     return out
 
@@ -200,8 +202,9 @@ def linear_wgrad_grouped(items, accumulate=True):
 
 # ------------------------------------------------------------------------------------- LayerNorm
 def layernorm_fwd(x, gamma, beta, eps=1e-5, pe=None, pe_period=1, relu=False, dropout_p=0.0, seed=0,
-                  out_f32=True, lp_dtype=None, save_stats=True):
+                  out_f32=True, lp_dtype=None, save_stats=True, seed_base=None):
     _gpu(x, gamma, beta, pe)
+    _seed_word(seed_base)
     rows, D = x.shape
     of = torch.empty(rows, D, device=x.device, dtype=torch.float32) if out_f32 else None
     ol = torch.empty(rows, D, device=x.device, dtype=lp_dtype) if lp_dtype is not None else None
@@ -210,17 +213,19 @@ def layernorm_fwd(x, gamma, beta, eps=1e-5, pe=None, pe_period=1, relu=False, dr
     a = N.LnFwdArgs(_p(x).value, _dt(x), x.stride(0), _p(gamma).value, _p(beta).value, float(eps),
                     _p(pe).value, int(pe_period), int(relu), float(dropout_p), int(seed) & 0xFFFFFFFF,
                     _p(of).value, D, _p(ol).value, _dt(ol) if ol is not None else 0, D, _p(mean).value,
-                    _p(rstd).value)
+                    _p(rstd).value, _p(seed_base).value)
     N.call("rp_layernorm_fwd", rows, D, ctypes.byref(a), _stream(x))
     return of, ol, mean, rstd
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, y=None, dropout_p=0.0, seed=0, dres=None, want_f32=True,
-                  lp_dtype=None, lp_dropout_p=0.0, lp_seed=0, dgamma=None, dbeta=None, ws=None, defer=None):
+                  lp_dtype=None, lp_dropout_p=0.0, lp_seed=0, dgamma=None, dbeta=None, ws=None, defer=None,
+                  seed_base=None):
     """Returns (dx_f32, dx_lp); accumulates dgamma / dbeta (fp32 [D]) when given.  With ``defer`` (a
     list), the gamma / beta partial reductions are appended to it as (partials, out) pairs for one
     ``colsum_batched`` call later instead of being launched here."""
     _gpu(dy, x, mean, rstd, gamma, y, dres)
+    _seed_word(seed_base)
     rows, D = x.shape
     dev = x.device
     dx = torch.empty(rows, D, device=dev, dtype=torch.float32) if want_f32 else None
@@ -243,7 +248,7 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, y=None, dropout_p=0.0, seed=0, dres=
                     _dt(y) if y is not None else 0, y.stride(0) if y is not None else 0,
                     float(dropout_p), int(seed) & 0xFFFFFFFF, _p(dres).value, D, _p(dx).value, D,
                     _p(dxl).value, _dt(dxl) if dxl is not None else 0, D, float(lp_dropout_p),
-                    int(lp_seed) & 0xFFFFFFFF, _p(pg).value, _p(pb).value, ld_part)
+                    int(lp_seed) & 0xFFFFFFFF, _p(pg).value, _p(pb).value, ld_part, _p(seed_base).value)
     N.call("rp_layernorm_bwd", rows, D, ctypes.byref(a), _stream(x))
     jobs = [(part, dgamma.as_strided((2 * D,), (1,)))] if both else \
         [(p, o) for p, o in ((pg, dgamma), (pb, dbeta)) if o is not None]
@@ -310,13 +315,14 @@ def colsum(X, w=None, out=None, accumulate=False, ws=None):
 
 
 # ------------------------------------------------------------------------------------- attention
-def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, q_prescaled=False, out_lo=None):
+def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, q_prescaled=False, out_lo=None, seed_base=None):
     """-> (out [B*T, H*dk], lse [B, H, T], dropmask or None).  The dropout keep bits drawn by the
     forward are returned and must be handed to attn_bwd.  q_prescaled: the Q columns of qkv hold
     Q * scale * log2(e) (linear_fwd's col_scale); the same flag must go to attn_bwd.  out_lo (bf16,
     optional, out's shape): filled with the output's rounding residual; hand it to attn_bwd too."""
     _gpu(qkv, key_valid)
     _contig(qkv, key_valid)
+    _seed_word(seed_base)
     dk = qkv.shape[1] // (3 * H)
     out = torch.empty(B * T, H * dk, device=qkv.device, dtype=qkv.dtype)
     lse = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
@@ -329,7 +335,7 @@ def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, q_prescaled=
         if out_lo.shape != out.shape or out_lo.dtype != out.dtype or not out_lo.is_contiguous():
             raise ValueError("attn_fwd: out_lo must be a contiguous tensor like out")
     N.call("rp_attn_fwd", _adt(qkv, q_prescaled), _p(qkv), _p(key_valid), B, T, H, dk, float(scale), float(dropout_p),
-           int(seed) & 0xFFFFFFFF, _p(out), _p(out_lo), _p(lse), _p(mask), _stream(qkv))
+           int(seed) & 0xFFFFFFFF, _p(seed_base), _p(out), _p(out_lo), _p(lse), _p(mask), _stream(qkv))
     _tock(e0)
     return out, lse, mask
 
@@ -377,7 +383,7 @@ def _rows(t, H, dk):
 
 
 def mha_fwd(q, k, v, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, seed=0, q_prescaled=False,
-            empty_uniform=False):
+            empty_uniform=False, seed_base=None):
     """General (self / cross) attention core.  q [B*Tq, >=H*dk], k/v [B*Tk, >=H*dk] row views (any row
     stride), key_valid [B, Tk] uint8.  -> (out [B*Tq, H*dk], lse [B, H, Tq], dropmask or None)."""
     _gpu(q, k, v, key_valid)
@@ -401,6 +407,8 @@ def mha_fwd(q, k, v, key_valid, B, Tq, Tk, H, scale, dropout_p=0.0, seed=0, q_pr
     a.lse = lse.data_ptr()
     a.dropmask = mask.data_ptr() if mask is not None else None
     a.empty_rows_uniform = int(empty_uniform)
+    _seed_word(seed_base)
+    a.seed_base = _p(seed_base).value
     N.call("rp_mha_fwd", _adt(q, q_prescaled), ctypes.byref(a), _stream(q))
     return out, lse, mask
 
@@ -513,22 +521,13 @@ def adam_coefficients(lr, beta1, beta2, eps, weight_decay, step):
     return list(buf)
 
 
-_seed_base = {"t": None}
-
-
-def set_seed_base(t):
-    """Graph-replayable dropout (rp_set_seed_base): while ``t`` (a uint32/int32 device word) is set,
-    dropout launches draw with rp_hash(*t, seed) read when the kernel runs; None restores plain seeds."""
+def _seed_word(t):
+    """Validate an optional graph-replayable dropout base: an int32 device word (see include/rp_api.h,
+    "Graph-replayable dropout"); it is passed per launch, the library holds no dropout state."""
     if t is not None:
         _gpu(t)
-        if t.dtype not in (torch.int32, torch.uint32) or t.numel() < 1:
-            raise TypeError("set_seed_base: needs an int32 device word")
-    N.call("rp_set_seed_base", _p(t))
-    _seed_base["t"] = t
-
-
-def seed_base_active():
-    return _seed_base["t"] is not None
+        if t.dtype not in (torch.int32, torch.uint32) or t.numel() < 1 or t.data_ptr() % 4:
+            raise TypeError("seed_base: needs an aligned int32 device word")
 
 
 # ------------------------------------------------------------------------------------- inference

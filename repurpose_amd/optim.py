@@ -99,6 +99,17 @@ class FusedAdam(torch.optim.Optimizer):
             self.state[p] = {"step": self._step_t, "exp_avg": self._m[o:o + k].view_as(p),
                              "exp_avg_sq": self._v[o:o + k].view_as(p)}
 
+    def state_dict(self):
+        """torch Adam's layout, detached from the live flat buffers: every parameter gets its OWN
+        ``step`` tensor and its own copies of ``exp_avg`` / ``exp_avg_sq``.  (Inside the optimizer all
+        trained parameters share one step tensor and view the flat moment buffers; handing those out
+        would make a torch.optim.Adam that loads the dict — in process, or through torch.save /
+        torch.load, which keep the sharing — add 1 to the shared step once per parameter.)"""
+        sd = super().state_dict()
+        sd["state"] = {i: {k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+                       for i, st in sd["state"].items()}
+        return sd
+
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._ensure()

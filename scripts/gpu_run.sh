@@ -23,6 +23,12 @@ for s in $STEPS; do
     smoke)   step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 400 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     benchfull) step benchfull 500 python -u bench.py ;;
+    gloo2)   RP_DIST_BACKEND=gloo step gloo2 400 python -u bench.py --gpus 2 --steps 3 --warmup 1 ;;
+    dp1)     RP_BENCH_DP=1 step dp1 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+               --master-addr 127.0.0.1 --master-port 29533 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    dp1eager) RP_BENCH_DP=1 step dp1eager 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+               --master-addr 127.0.0.1 --master-port 29534 bench.py --steps 10 --warmup 3 --no-cpu-baseline --graph off ;;
+    b1)      step b1 400 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-parity-mode --no-fresh-batch ;;
   esac
 done
 echo ALLDONE

@@ -76,10 +76,11 @@ def test_softnms_batched_random_vs_oracle(dev):
         np.testing.assert_array_equal(final[b, :cnt[b]].cpu().numpy(), s.numpy())
 
 
-@pytest.mark.parametrize("n,ms", [(1500, 1500), (3000, 40), (7000, 7000)])
+@pytest.mark.parametrize("n,ms", [(1500, 1500), (3000, 40), (6000, 6000), (6144, 300), (7000, 7000)])
 def test_softnms_beyond_1024_candidates(dev, n, ms):
     """The reference function has no candidate cap (models/softnms.py:3-38): 1500 / 3000 candidates
-    run from LDS, 7000 from the global workspace path; indices and final scores match numpy."""
+    run from LDS (6000 / 6144: 117 / 120 KiB of dynamic LDS, above the 64 KiB default), 7000 from the
+    global workspace path; indices and final scores match numpy."""
     rs = np.random.RandomState(n)
     s = np.sort(rs.uniform(0.0, 1, n).astype(np.float32))[::-1].copy()
     c = rs.uniform(0, 20000, n).astype(np.float32)

@@ -637,3 +637,24 @@ def test_wgrad_grouped_repeat_bitwise(dev, T):
         else:
             for a, c in zip(first, got):
                 assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("Kr", [128, 192, 512])
+def test_gemm8_dgrad_gate_prefetch_repeat_bitwise(dev, Kr):
+    """Race guard for the 256-row kernel's gated dgrad (the linear2 dgrad of the encoder: bf16 ReLU /
+    dropout gate touched one K-tile before the epilogue, two loads left in flight by the counted
+    waits of the last two K-tiles): relaunched eight times at short reduction depths, every launch
+    matches fp64 and is bitwise the first."""
+    M, Nout = 16384, 2048
+    dy = rnd(M, Kr, dev=dev, seed=500 + Kr).to(torch.bfloat16)
+    w = rnd(Kr, Nout, dev=dev, seed=600 + Kr, scale=0.05).to(torch.bfloat16)
+    gate = rnd(M, Nout, dev=dev, seed=700 + Kr).to(torch.bfloat16)
+    ref = (dy.double() @ w.double()) * (gate.double() > 0) * (1 / 0.9)
+    first = None
+    for _ in range(8):
+        got = K.linear_dgrad(dy, w, out_dtype=torch.bfloat16, gate=gate, gate_scale=1 / 0.9)
+        close(got, ref, atol=2e-2 + 4e-3 * math.sqrt(Kr), rtol=1e-2, what=f"gated dgrad K={Kr}")
+        if first is None:
+            first = got.clone()
+        else:
+            assert torch.equal(first, got)

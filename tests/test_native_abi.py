@@ -33,7 +33,7 @@ def test_argument_errors_are_reported():
         N.call("rp_gemm", 0, 8, 8, 7, ctypes.c_void_p(16), 8, 1, ctypes.c_void_p(16), 8, 1, ctypes.c_void_p(16), 8, 0,
                1.0, None, None)
     with pytest.raises(RuntimeError, match="head dim"):
-        N.call("rp_attn_fwd", 0, None, None, 1, 1, 1, 32, 1.0, 0.0, 0, None, None, None, None, None)
+        N.call("rp_attn_fwd", 0, None, None, 1, 1, 1, 32, 1.0, 0.0, 0, None, None, None, None, None, None)
     fake = ctypes.c_void_p(16)
     assert N.load().rp_softnms_workspace(2, 1000) == 0 and N.load().rp_softnms_workspace(2, 7000) == 2 * 5 * 7000 * 4
     with pytest.raises(RuntimeError, match="needs rp_softnms_workspace"):

@@ -77,6 +77,38 @@ def test_loads_reference_adam_checkpoint_and_saves_the_same_layout():
         assert torch.equal(st2["exp_avg"], st["exp_avg"]) and torch.equal(st2["exp_avg_sq"], st["exp_avg_sq"])
 
 
+def test_state_dict_resumes_in_torch_adam_through_a_checkpoint_file(tmp_path):
+    """A FusedAdam checkpoint saved with torch.save and resumed by torch.optim.Adam (the reference
+    trainer, main.py:222) steps every parameter from step 3 to 4 — no step tensor is shared — and does
+    not alias FusedAdam's live moment buffers."""
+    torch.manual_seed(0)
+    ref = Oracle(**CFG)
+    sd = _torch_adam_after_steps(ref).state_dict()
+    m = MMCTransformer(**CFG)
+    m.load_state_dict(ref.state_dict())
+    opt = FusedAdam(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    opt.load_state_dict(sd)
+    out = opt.state_dict()
+    steps = [st["step"] for st in out["state"].values()]
+    assert len({id(t) for t in steps}) == len(steps)
+    f = tmp_path / "ckpt.pth"
+    torch.save({"optimizer": out}, f)
+    loaded = torch.load(f, weights_only=True)["optimizer"]
+    topt2 = torch.optim.Adam(ref.parameters(), lr=1e-3, weight_decay=1e-4)
+    topt2.load_state_dict(loaded)
+    for n, p in ref.named_parameters():
+        p.grad = None if n.startswith("reg_head.") else torch.ones_like(p)
+    before = opt._m.clone()
+    topt2.step()
+    for i, st in topt2.state_dict()["state"].items():
+        assert float(st["step"]) == 4.0, i
+    assert torch.equal(opt._m, before)  # the resumed torch Adam wrote its own copies
+    # and the dict FusedAdam hands out is a snapshot, not a view of its flat buffers
+    k = next(iter(out["state"]))
+    out["state"][k]["exp_avg"].add_(1.0)
+    assert torch.equal(opt._m, before)
+
+
 def test_fresh_state_dict_matches_torch_adam_layout():
     m = MMCTransformer(**CFG)
     ref = Oracle(**CFG)
