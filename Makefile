@@ -30,3 +30,25 @@ clean:
 	rm -rf build $(LIB)
 
 .PHONY: all clean
+
+# Host-side sanitizer build of the C ABI: the launchers' argument validation,
+# workspace queries and host arithmetic compiled with AddressSanitizer + UndefinedBehaviorSanitizer
+# (host code only: -Xarch_host; the device code is compiled as usual), driven through every error path by
+# tests/native/abi_errors.cpp.  Runs without a GPU; tests/test_asan_abi.py runs it.
+ASAN_DIR := build/asan
+ASAN_FLAGS := -O1 -g -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -fno-omit-frame-pointer \
+	-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all
+ASAN_OBJ := $(patsubst $(CSRC)/%.hip,$(ASAN_DIR)/%.o,$(SRC))
+
+$(ASAN_DIR)/%.o: $(CSRC)/%.hip $(CSRC)/rp_common.h include/rp_api.h Makefile
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) $(ASAN_FLAGS) -c $< -o $@
+
+$(ASAN_DIR)/abi_errors: tests/native/abi_errors.cpp $(ASAN_OBJ) include/rp_api.h
+	$(HIPCC) -x c++ -O1 -g -std=c++17 -Iinclude -fno-omit-frame-pointer -fsanitize=address,undefined \
+		-fno-sanitize-recover=all -c tests/native/abi_errors.cpp -o $(ASAN_DIR)/abi_errors.o
+	$(HIPCC) -fsanitize=address,undefined $(ASAN_DIR)/abi_errors.o $(ASAN_OBJ) -o $@
+
+asan: $(ASAN_DIR)/abi_errors
+
+.PHONY: asan

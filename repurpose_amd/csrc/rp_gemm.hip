@@ -1358,6 +1358,7 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
     e.col_scale_n = ep->col_scale_n;
     e.col_scale = ep->col_scale;
     e.prefetch_gate = rp_gemm_prefetch_enabled();
+    RP_REQUIRE(ep->dropout_p >= 0.f && ep->dropout_p < 1.f, "rp_gemm: dropout_p must be in [0, 1)");
     RP_REQUIRE(e.col_scale_n >= 0 && e.col_scale_n % 8 == 0, "rp_gemm: col_scale_n must be a multiple of 8");
     RP_REQUIRE(!e.accumulate || c_dtype == RP_F32, "rp_gemm: accumulate needs an fp32 C");
     RP_REQUIRE(!e.drop_thresh || M * N < (int64_t)UINT32_MAX, "rp_gemm: dropout index overflow");

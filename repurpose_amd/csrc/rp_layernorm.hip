@@ -266,6 +266,7 @@ extern "C" int rp_layernorm_fwd(int64_t rows, int64_t D, const rp_ln_fwd_args* p
   a.gamma = p->gamma; a.beta = p->beta; a.eps = p->eps;
   a.pe = p->pe; a.pe_period = p->pe_period;
   a.relu = p->relu;
+  RP_REQUIRE(p->dropout_p >= 0.f && p->dropout_p < 1.f, "rp_layernorm_fwd: dropout_p must be in [0, 1)");
   a.drop_thresh = rp_dropout_thresh(p->dropout_p);
   a.drop_scale = p->dropout_p > 0.f ? 1.f / (1.f - p->dropout_p) : 1.f;
   a.drop_seed = p->dropout_seed;
@@ -289,6 +290,8 @@ extern "C" int rp_layernorm_bwd(int64_t rows, int64_t D, const rp_ln_bwd_args* p
   a.x = p->x; a.x_dtype = p->x_dtype; a.ldx = p->ldx;
   a.mean = p->mean; a.rstd = p->rstd; a.gamma = p->gamma;
   a.y = p->y; a.y_dtype = p->y_dtype; a.ldy = p->ldy;
+  RP_REQUIRE(p->dropout_p >= 0.f && p->dropout_p < 1.f && p->dx_lp_dropout_p >= 0.f && p->dx_lp_dropout_p < 1.f,
+             "rp_layernorm_bwd: dropout_p must be in [0, 1)");
   a.drop_thresh = rp_dropout_thresh(p->dropout_p);
   a.drop_scale = p->dropout_p > 0.f ? 1.f / (1.f - p->dropout_p) : 1.f;
   a.drop_seed = p->dropout_seed;
