@@ -976,6 +976,73 @@ __device__ __forceinline__ void dma_rows64(const bf16* __restrict__ base, int64_
   }
 }
 
+// Buffer-descriptor form of the LDS-DMA pieces (the tile loops' steady state).  A lane's source
+// address inside a tile is fixed for the whole sweep (its row of the 8-row piece, its swizzled chunk),
+// so it is computed ONCE as a 32-bit voffset; a tile then costs one scalar offset (row0 * row bytes)
+// and one buffer_load ... lds per piece.  The global_load_lds form recomputed a clamped 64-bit address
+// per piece every tile (two v_mul_lo_u32 + v_mad_u64_u32 + 64-bit adds per piece: ~30 VALU + ~30 SALU
+// per tile and wave of the dK/dV kernel).  Partial tiles (row0 + 64 > nrows) keep the clamped path.
+typedef int rp_srd __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ rp_srd make_srd(const void* p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  rp_srd s;
+  s[0] = (int)__builtin_amdgcn_readfirstlane((uint32_t)a);
+  s[1] = (int)(__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xFFFFu);  // stride 0
+  s[2] = -1;          // num_records: no range check — callers only load inside the operand
+  s[3] = 0x00020000;  // raw buffer, 32-bit data format (cdna_hip_programming.md T8 recipe)
+  return s;
+}
+// lane l's 16 (4) bytes at srd.base + voff + soff land at LDS byte lds + 16 l (4 l); untracked by the
+// compiler like dma16 (the kernels' counted vmcnt orders it)
+__device__ __forceinline__ void dma16b(const rp_srd& srd, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_nop 0\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "v"(voff), "s"(srd), "s"(soff)
+      : "memory");
+}
+__device__ __forceinline__ void dma4b(const rp_srd& srd, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %2, %3, %4 offen lds\n\t"
+      "s_nop 0\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "v"(voff), "s"(srd), "s"(soff)
+      : "memory");
+}
+
+// rows [row0, row0 + 64) of a [rows][64] bf16 operand -> the swizzled 8 KB image (two 1 KB pieces per
+// wave, as dma_rows64), descriptor form for full tiles: piece j of wave w is
+// dma16b(srd, vo_j, row0 * rowbytes, image + (2w + j) * 1 KB)
+struct Rows64 {
+  const bf16* base;
+  int64_t ld;
+  rp_srd srd;
+  uint32_t vo0, vo1, rowbytes;
+  bool fast;  // every full tile's byte offsets fit 32 bits
+  __device__ __forceinline__ void init(const bf16* b, int64_t ld_, int nrows, int w, int lane) {
+    base = b;
+    ld = ld_;
+    srd = make_srd(b);
+    const int r0 = (w * 2) * 8 + (lane >> 3), r1 = r0 + 8;
+    const int c0 = (lane & 7) ^ (((r0 >> 1) & 3) << 1), c1 = (lane & 7) ^ (((r1 >> 1) & 3) << 1);
+    vo0 = (uint32_t)((r0 * ld_ + c0 * 8) * 2);
+    vo1 = (uint32_t)((r1 * ld_ + c1 * 8) * 2);
+    rowbytes = (uint32_t)(ld_ * 2);
+    fast = ((int64_t)nrows + 64) * ld_ * 2 < ((int64_t)1 << 31);
+  }
+};
+
 // raw workgroup barrier: no release / acquire fence, so the compiler adds no vmcnt(0) for the LDS-DMA
 // loads still in flight (the explicit counted vmcnt before it is what makes a tile's DMA visible);
 // the empty asm statements keep the compiler from moving memory operations across it
@@ -997,8 +1064,11 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
   constexpr int TILE = KV_QT * C::ROWB;
   // keep bits: KB/64 key tiles x 4 groups x 64 queries, u16 — one full 1 KB DMA piece (at KB = 64 the
   // second half holds a copy of the first)
-  constexpr int MASKB = 1024;
-  constexpr int BUF = 2 * TILE + 2 * KV_QT * 4 + MASKB;  // Q, dO, raw lse, raw delta, keep bits
+  // slot: Q, dO images, then four 1 KB regions — raw lse row, raw delta row, keep bits, scratch — one
+  // per wave's fifth DMA piece (wave 0, and wave 3 without dropout, load a dummy row into the scratch
+  // region, so every wave issues five DMA instructions per tile and one counted wait serves all)
+  constexpr int XR = 1024;
+  constexpr int BUF = 2 * TILE + 4 * XR;
   constexpr int NBUF = 3;
   // three separate arrays rather than one indexed ring: every LDS address of a step is then a per-lane
   // base plus an immediate offset
@@ -1061,31 +1131,60 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
   // LDS-DMA of query tile it into ring slot BI: Q and dO (two 1 KB pieces each per wave), the S start
   // (wave 1; -inf past Tq) and dP start (wave 2) rows and the keep-bit words (wave 3, with dropout):
   // D = 4 DMA instructions per wave, 5 for waves 1, 2 and (with dropout) 3
+  Rows64 rq, rdo;
+  rq.init(Qg, ldq, Tq, w, lane);
+  rdo.init(dOg, lddo, Tq, w, lane);
+  // the wave's fifth piece: wave 1 the lse row constants, wave 2 the delta ones (lanes 0..15 cover the
+  // tile's 64 floats, the other lanes repeat them), wave 3 the keep bits, the rest a dummy delta row
+  const bool xmask = DROP && w == 3;
+  const uint16_t* mslab = DROP ? dmask + (int64_t)bh * KT * 4 * ldm : dmask;
+  const rp_srd srd_x = make_srd(xmask ? (const void*)mslab : (const void*)(w == 1 ? nls_bh : ndl_bh));
+  uint32_t vo_x = (uint32_t)(lane & 15) * 16u;
+  const uint32_t bpr_x = xmask ? 2u : 4u;  // source bytes per query row
+  const uint32_t xo = (uint32_t)(2 * TILE + XR * (w == 1 ? 0 : (w == 2 ? 1 : (xmask ? 2 : 3))));
+  if (xmask) {
+    const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
+    int tile = kb * (KB / 64) + (r >> 2);
+    tile = tile < KT ? tile : KT - 1;  // keys past Tk: their dK / dV rows are written as zeros
+    // KB = 64: lanes 32..63 repeat lanes 0..31's words into the unused second half of the region
+    vo_x = (uint32_t)((((int64_t)tile * 4 + (r & 3)) * ldm + cch * 8) * 2);
+  }
+  const bool xfast = (int64_t)KT * 4 * ldm * 2 < ((int64_t)1 << 31) && rq.fast && rdo.fast;
+  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
   auto issue = [&](int it, auto bi) {
+    constexpr int BI = decltype(bi)::value;
     char* buf = ring(bi);
     const int qs0 = it * KV_QT;
-    dma_rows64(Qg, ldq, qs0, Tq, buf, w, lane);
-    dma_rows64(dOg, lddo, qs0, Tq, buf + TILE, w, lane);
-    const int q = qs0 + lane;
-    if (w == 1) dma4(q < Tq ? nls_bh + q : kPadStart, lds_addr(buf + 2 * TILE));
-    if (w == 2) dma4(ndl_bh + (q < Tq ? q : Tq - 1), lds_addr(buf + 2 * TILE + KV_QT * 4));
-    if (DROP && w == 3) {
-      const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
-      int tile = kb * (KB / 64) + (r >> 2);
-      tile = tile < KT ? tile : KT - 1;  // keys past Tk: their dK / dV rows are written as zeros
-      // KB = 64: lanes 32..63 repeat lanes 0..31's words into the unused second half of the slot
-      dma16(dmask + (((int64_t)bh * KT + tile) * 4 + (r & 3)) * ldm + qs0 + cch * 8,
-            lds_addr(buf + 2 * TILE + 2 * KV_QT * 4));
+    if (xfast && qs0 + KV_QT <= Tq) {
+      const uint32_t t = slot_lds[BI];
+      const uint32_t pq = t + (uint32_t)(w * 2) * 1024u;
+      dma16b(rq.srd, rq.vo0, (uint32_t)qs0 * rq.rowbytes, pq);
+      dma16b(rq.srd, rq.vo1, (uint32_t)qs0 * rq.rowbytes, pq + 1024u);
+      dma16b(rdo.srd, rdo.vo0, (uint32_t)qs0 * rdo.rowbytes, pq + TILE);
+      dma16b(rdo.srd, rdo.vo1, (uint32_t)qs0 * rdo.rowbytes, pq + TILE + 1024u);
+      dma16b(srd_x, vo_x, (uint32_t)qs0 * bpr_x, t + xo);
+    } else {  // partial tile: clamped rows, -inf S start past Tq
+      dma_rows64(Qg, ldq, qs0, Tq, buf, w, lane);
+      dma_rows64(dOg, lddo, qs0, Tq, buf + TILE, w, lane);
+      const int q = qs0 + lane;
+      if (xmask) {
+        const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
+        int tile = kb * (KB / 64) + (r >> 2);
+        tile = tile < KT ? tile : KT - 1;
+        dma16(dmask + (((int64_t)bh * KT + tile) * 4 + (r & 3)) * ldm + qs0 + cch * 8, lds_addr(buf + xo));
+      } else if (w == 1) {
+        dma4(q < Tq ? nls_bh + q : kPadStart, lds_addr(buf + xo));
+      } else {
+        dma4(ndl_bh + (q < Tq ? q : Tq - 1), lds_addr(buf + xo));
+      }
     }
   };
-  // step it waits for DMA(it); issued after it by then: DMA(it + 1) (D instructions, if it exists)
+  // step it waits for DMA(it); issued after it by then: DMA(it + 1) (5 instructions, if it exists)
   auto wait_tile = [&](bool next) {
     if (!next)
       wait_vm<0>();
-    else if (w == 1 || w == 2 || (DROP && w == 3))
-      wait_vm<5>();
     else
-      wait_vm<4>();
+      wait_vm<5>();
   };
 
   const int nqt = (Tq + KV_QT - 1) / KV_QT;
@@ -1100,8 +1199,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
     const char* Ql = cur;
     const char* dOl = cur + TILE;
     const float* lrow = reinterpret_cast<const float*>(cur + 2 * TILE);
-    const float* drow = lrow + KV_QT;
-    const uint16_t* mw = reinterpret_cast<const uint16_t*>(cur + 2 * TILE + 2 * KV_QT * 4);
+    const float* drow = reinterpret_cast<const float*>(cur + 2 * TILE + XR);
+    const uint16_t* mw = reinterpret_cast<const uint16_t*>(cur + 2 * TILE + 2 * XR);
 
     // one half = 32 queries: S / dP products (16 MFMAs), the probability / dS VALU, then the dV / dK
     // products (16 MFMAs) that consume both 16-query rows of the half
@@ -1665,15 +1764,32 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
   // LDS-DMA of key tile it into slot BI: K and V (two 1 KB pieces each per wave) and, with dropout,
   // wave 1 the 4 x 128 keep-bit words of this query block (columns past ldm clamped: their queries
   // are past Tq and never read)
+  Rows64 rk, rv;
+  rk.init(Kg, ldk, Tk, w, lane);
+  rv.init(Vg, ldv, Tk, w, lane);
+  // keep bits (wave 1): lane (g, c) reads words [tile][g][this block's 128 queries], column chunk c
+  const rp_srd srd_m = make_srd(mrow);
+  int64_t mcol = (int64_t)qb * QB + (lane & 15) * 8;
+  mcol = mcol < ldm - 8 ? mcol : ldm - 8;
+  const uint32_t vo_m = (uint32_t)((((int64_t)(lane >> 4)) * ldm + mcol) * 2);
+  const bool xfast = (int64_t)KT * 4 * ldm * 2 < ((int64_t)1 << 31) && rk.fast && rv.fast;
+  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
   auto issue = [&](int it, auto bi) {
+    constexpr int BI = decltype(bi)::value;
     char* buf = ring(bi);
     const int k0 = it * FW_KT;
-    dma_rows64(Kg, ldk, k0, Tk, buf, w, lane);
-    dma_rows64(Vg, ldv, k0, Tk, buf + TILE, w, lane);
-    if (DROP && w == 1) {
-      int64_t col = (int64_t)qb * QB + (lane & 15) * 8;
-      col = col < ldm - 8 ? col : ldm - 8;
-      dma16(mrow + ((int64_t)it * 4 + (lane >> 4)) * ldm + col, lds_addr(buf + 2 * TILE));
+    if (xfast && k0 + FW_KT <= Tk) {
+      const uint32_t t = slot_lds[BI];
+      const uint32_t pk = t + (uint32_t)(w * 2) * 1024u;
+      dma16b(rk.srd, rk.vo0, (uint32_t)k0 * rk.rowbytes, pk);
+      dma16b(rk.srd, rk.vo1, (uint32_t)k0 * rk.rowbytes, pk + 1024u);
+      dma16b(rv.srd, rv.vo0, (uint32_t)k0 * rv.rowbytes, pk + TILE);
+      dma16b(rv.srd, rv.vo1, (uint32_t)k0 * rv.rowbytes, pk + TILE + 1024u);
+      if (DROP && w == 1) dma16b(srd_m, vo_m, (uint32_t)it * 8u * (uint32_t)ldm, t + 2 * TILE);
+    } else {
+      dma_rows64(Kg, ldk, k0, Tk, buf, w, lane);
+      dma_rows64(Vg, ldv, k0, Tk, buf + TILE, w, lane);
+      if (DROP && w == 1) dma16(mrow + ((int64_t)it * 4 + (lane >> 4)) * ldm + mcol, lds_addr(buf + 2 * TILE));
     }
   };
   auto wait_tile = [&](bool next) {
@@ -1895,10 +2011,25 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
     constexpr int BI = decltype(bi)::value;
     return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
   };
+  Rows64 rk, rv;
+  rk.init(Kg, ldk, Tk, w, lane);
+  rv.init(Vg, ldv, Tk, w, lane);
+  const bool xfast = rk.fast && rv.fast;
+  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
   auto issue = [&](int it, auto bi) {  // K and V of key tile it: two 1 KB pieces each per wave
-    char* buf = ring(bi);
-    dma_rows64(Kg, ldk, it * FW_KT, Tk, buf, w, lane);
-    dma_rows64(Vg, ldv, it * FW_KT, Tk, buf + TILE, w, lane);
+    constexpr int BI = decltype(bi)::value;
+    const int k0 = it * FW_KT;
+    if (xfast && k0 + FW_KT <= Tk) {
+      const uint32_t pk = slot_lds[BI] + (uint32_t)(w * 2) * 1024u;
+      dma16b(rk.srd, rk.vo0, (uint32_t)k0 * rk.rowbytes, pk);
+      dma16b(rk.srd, rk.vo1, (uint32_t)k0 * rk.rowbytes, pk + 1024u);
+      dma16b(rv.srd, rv.vo0, (uint32_t)k0 * rv.rowbytes, pk + TILE);
+      dma16b(rv.srd, rv.vo1, (uint32_t)k0 * rv.rowbytes, pk + TILE + 1024u);
+    } else {
+      char* buf = ring(bi);
+      dma_rows64(Kg, ldk, k0, Tk, buf, w, lane);
+      dma_rows64(Vg, ldv, k0, Tk, buf + TILE, w, lane);
+    }
   };
   // step it waits for DMA(it).  Issued after it, in order: (it >= 2) the 2 keep-bit stores of step
   // it - 2, DMA(it + 1) (4), the 2 stores of step it - 1 (it >= 1).

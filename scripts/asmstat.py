@@ -57,7 +57,7 @@ def main():
     for name, ops in blocks:
         c = Counter(classify(o) for o in ops)
         tot += c
-        if len(ops) > 40:
+        if len(ops) > int(__import__("os").environ.get("MINOPS", "40")):
             print(f"{name:16s} n={len(ops):5d} " + " ".join(f"{k}={c[k]}" for k in
                   ("mfma", "valu", "trans", "ds", "vmem", "wait", "barrier", "salu")))
     print("total", dict(tot))
