@@ -12,6 +12,8 @@
  *   rp_gemm               nn.Linear fwd/dgrad/wgrad              models/MMCTransformer.py:32,121,63-93;
  *                         and MHA in_proj/out_proj, linear1/2 of the 16 nn.TransformerEncoderLayer
  *                         (constructed at models/MMCTransformer.py:41-55)
+ *   rp_gemm_ln_fwd/bwd    Linear + residual + LayerNorm seams of the pre-LN encoder layers
+ *                         models/MMCTransformer.py:41-55 (out_proj/linear2 -> norm2/norm1 and back)
  *   rp_layernorm_fwd/bwd  nn.LayerNorm (+ PE add, ReLU, dropout)  models/MMCTransformer.py:35,124,127,
  *                         58,141,65,72,84; encoder-layer norm1/norm2
  *   rp_attn_fwd/bwd       nn.MultiheadAttention -> SDPA (key padding mask, dropout 0.1)
@@ -120,6 +122,59 @@ typedef struct {
   int64_t M, N, ldy, ldx;
 } rp_wgrad_item;
 int rp_gemm_wgrad_grouped(int64_t K, const rp_wgrad_item* items, int n_items, int accumulate, void* stream);
+
+/* GEMM + LayerNorm over whole 512-wide rows (bf16 operands, fp32 accumulate), one launch per
+ * pre-LN encoder-layer seam (models/MMCTransformer.py:41-55, d_model = 512):
+ *   rp_gemm_ln_fwd:  x_out = dropout(A W^T + bias) + residual          (rp_gemm with that epilogue)
+ *                    h_out = LayerNorm(x_out; gamma, beta, eps), mean/rstd saved (rp_layernorm_fwd)
+ *     A [M, lda] bf16 (k-major), W [512, ldw >= K] bf16 (the nn.Linear weight); x_out fp32, h_out bf16.
+ *     Replaces x1 = x + drop1(out_proj(.)) followed by norm2(x1), and x2 = x1 + drop2(linear2(.))
+ *     followed by the next layer's norm1 (or encoder_norm).
+ *   rp_gemm_ln_bwd:  dh = A W (A = dY [M, lda] bf16, W [K, ldw >= 512] bf16: the dgrad of a Linear
+ *                    whose weight is [K][512]), then rp_layernorm_bwd's row computation on dh
+ *                    (x, mean, rstd, gamma, dres -> dx fp32, dx_lp bf16 with dropout(lp_dropout_p,
+ *                    lp_seed), gamma / beta partials per 32-row block as rp_layernorm_bwd writes them).
+ *     dh itself is never written.  Replaces linear1 / in_proj dgrad followed by norm2 / norm1 backward.
+ * Results are bitwise those of the unfused calls (same MFMA k order, same epilogue and LayerNorm
+ * arithmetic).  M % 64 == 0, K % 64 == 0; one workgroup per 64 rows. */
+typedef struct rp_gemm_ln_args {
+  const void* A;
+  int64_t lda;
+  const void* W;
+  int64_t ldw;
+  /* forward */
+  const float* bias;
+  float dropout_p;
+  uint32_t dropout_seed;
+  const uint32_t* seed_base; /* optional, as rp_gemm_epilogue.seed_base (dropout_seed and lp_seed) */
+  const float* residual;
+  int64_t ldr;
+  float* x_out;
+  int64_t ldx_out;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  void* h_out;
+  int64_t ldh;
+  float* mean; /* fwd: written; bwd: read */
+  float* rstd;
+  /* backward */
+  const float* x;
+  int64_t ldx;
+  const float* dres; /* optional */
+  int64_t lddres;
+  float* dx;
+  int64_t lddx;
+  void* dx_lp; /* optional */
+  int64_t lddx_lp;
+  float lp_dropout_p;
+  uint32_t lp_seed;
+  float* dgamma_part; /* optional: [M/32][ld_part] */
+  float* dbeta_part;
+  int64_t ld_part;
+} rp_gemm_ln_args;
+int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* a, void* stream);
+int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* a, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* LayerNorm over the last dim D (<= 4096, multiple of 4), one row per wavefront.
@@ -291,6 +346,40 @@ typedef struct rp_mha_args {
                               0 = torch key_padding_mask semantics (-inf: such rows are NaN) */
   const uint32_t* seed_base; /* optional, as rp_gemm_epilogue.seed_base (forward dropout stream seed) */
 } rp_mha_args;
+
+/* General attention core (fp32) for head dims the flash kernels do not serve (d_k > 64) and masks
+ * that differ between queries or heads — models/transformer.py:52-81 exactly: scores = scale * Q K^T,
+ * scores[mask == 0] = -1e9, P = softmax(scores), out = P V; backward with no gradient through masked
+ * scores.  q / k / v rows as rp_mha_args (fp32, head h at columns h*head_dim ..); mask (optional)
+ * uint8 addressed mask[b*mask_sb + h*mask_sh + q*mask_sq + k*mask_sk] (element strides, 0 on a
+ * broadcast dimension).  probs: [B, H, Tq, Tk] fp32 workspace the forward fills and the backward reads;
+ * dscores: [B, H, Tq, Tk] fp32 backward workspace; dq / dk / dv fully overwritten. */
+typedef struct rp_mha_general_args {
+  const float* q;
+  int64_t ldq;
+  const float* k;
+  int64_t ldk;
+  const float* v;
+  int64_t ldv;
+  int B, Tq, Tk, H, head_dim;
+  float scale;
+  const uint8_t* mask;
+  int64_t mask_sb, mask_sh, mask_sq, mask_sk;
+  float* probs;
+  float* out;
+  int64_t ldo;
+  const float* dout;
+  int64_t lddo;
+  float* dscores;
+  float* dq;
+  int64_t lddq;
+  float* dk;
+  int64_t lddk;
+  float* dv;
+  int64_t lddv;
+} rp_mha_general_args;
+int rp_mha_general_fwd(const rp_mha_general_args* args, void* stream);
+int rp_mha_general_bwd(const rp_mha_general_args* args, void* stream);
 
 int64_t rp_mha_dropmask_elems(int B, int Tq, int Tk, int H);
 int rp_mha_fwd(int dtype, const rp_mha_args* args, void* stream);

@@ -468,6 +468,12 @@ class _Schedule:
         # graph capture (graph.py): the model's device seed word, passed to every dropout launch
         self.sb = model._seed_base
         self.saved = None
+        # bf16 at d_model 512: GEMM + LayerNorm seams as single launches (rp_gemm_ln_*), opt-in with
+        # RP_GEMM_LN=1: bitwise the unfused pairs, but the 64 x 512 full-row tile streams the whole weight
+        # through every CU's LDS, and at one workgroup per CU that measured +0.17 ms per step at the bench
+        # shape (interleaved A/B) — the 128 x 128 GEMM + separate LayerNorm stays the default
+        self.fused_ln = (self.dt == torch.bfloat16 and self.M % 64 == 0 and model.d_model == 512
+                         and os.environ.get("RP_GEMM_LN", "0") == "1")
 
     # ---- parameter access ----
     def P(self, name):  # fp32 master tensor
@@ -514,10 +520,14 @@ class _Schedule:
         x, _, mu0, rs0 = K.layernorm_fwd(proj, self.P("input_norm.weight"), self.P("input_norm.bias"),
                                          pe=pe, pe_period=T, save_stats=save)
         layers = []
+        # bf16 at d_model 512: every "Linear + residual -> LayerNorm" seam is one rp_gemm_ln_fwd launch
+        # (out_proj -> norm2, linear2 -> the next norm1 / encoder_norm), bitwise the unfused pair
+        fused = self.fused_ln
+        _, h1, mu1, rs1 = K.layernorm_fwd(x, self.P("multimodal_encoder.layers.0.norm1.weight"),
+                                          self.P("multimodal_encoder.layers.0.norm1.bias"),
+                                          out_f32=False, lp_dtype=dt, save_stats=save)
         for l in range(L):
             pre = f"multimodal_encoder.layers.{l}."
-            _, h1, mu1, rs1 = K.layernorm_fwd(x, self.P(pre + "norm1.weight"), self.P(pre + "norm1.bias"),
-                                              out_f32=False, lp_dtype=dt, save_stats=save)
             # the Q columns leave the GEMM as Q * scale * log2(e) (rounded once, read by the attention
             # forward and both backward kernels: the backward recomputes the forward's exact scores)
             qkv = K.linear_fwd(h1, self.W(pre + "self_attn.in_proj_weight"), self.P(pre + "self_attn.in_proj_bias"),
@@ -527,19 +537,33 @@ class _Schedule:
             olo = torch.empty(M, d, device=qkv.device, dtype=dt) if (save and dt != _F32) else None
             o, lse, dmask = K.attn_fwd(qkv, kv, B, T, H, scale, p, self.seed(100 + 4 * l), seed_base=self.sb, q_prescaled=True,
                                        out_lo=olo)
-            x1 = K.linear_fwd(o, self.W(pre + "self_attn.out_proj.weight"), self.P(pre + "self_attn.out_proj.bias"),
-                              out_dtype=_F32, dropout_p=p, seed=self.seed(101 + 4 * l), seed_base=self.sb, residual=x)
-            _, h2, mu2, rs2 = K.layernorm_fwd(x1, self.P(pre + "norm2.weight"), self.P(pre + "norm2.bias"),
-                                              out_f32=False, lp_dtype=dt, save_stats=save)
+            nxt = f"multimodal_encoder.layers.{l + 1}.norm1." if l + 1 < L else "encoder_norm."
+            if fused:
+                x1, h2, mu2, rs2 = K.linear_ln_fwd(o, self.W(pre + "self_attn.out_proj.weight"),
+                                                   self.P(pre + "self_attn.out_proj.bias"), x,
+                                                   self.P(pre + "norm2.weight"), self.P(pre + "norm2.bias"),
+                                                   dropout_p=p, seed=self.seed(101 + 4 * l), seed_base=self.sb)
+            else:
+                x1 = K.linear_fwd(o, self.W(pre + "self_attn.out_proj.weight"), self.P(pre + "self_attn.out_proj.bias"),
+                                  out_dtype=_F32, dropout_p=p, seed=self.seed(101 + 4 * l), seed_base=self.sb, residual=x)
+                _, h2, mu2, rs2 = K.layernorm_fwd(x1, self.P(pre + "norm2.weight"), self.P(pre + "norm2.bias"),
+                                                  out_f32=False, lp_dtype=dt, save_stats=save)
             f = K.linear_fwd(h2, self.W(pre + "linear1.weight"), self.P(pre + "linear1.bias"), relu=True,
                              dropout_p=p, seed=self.seed(102 + 4 * l), seed_base=self.sb)
-            x2 = K.linear_fwd(f, self.W(pre + "linear2.weight"), self.P(pre + "linear2.bias"), out_dtype=_F32,
-                              dropout_p=p, seed=self.seed(103 + 4 * l), seed_base=self.sb, residual=x1)
+            if fused:
+                x2, hn, mun, rsn = K.linear_ln_fwd(f, self.W(pre + "linear2.weight"), self.P(pre + "linear2.bias"), x1,
+                                                   self.P(nxt + "weight"), self.P(nxt + "bias"), dropout_p=p,
+                                                   seed=self.seed(103 + 4 * l), seed_base=self.sb)
+            else:
+                x2 = K.linear_fwd(f, self.W(pre + "linear2.weight"), self.P(pre + "linear2.bias"), out_dtype=_F32,
+                                  dropout_p=p, seed=self.seed(103 + 4 * l), seed_base=self.sb, residual=x1)
+                _, hn, mun, rsn = K.layernorm_fwd(x2, self.P(nxt + "weight"), self.P(nxt + "bias"),
+                                                  out_f32=False, lp_dtype=dt, save_stats=save)
             if save:
                 layers.append((x, h1, mu1, rs1, qkv, o, olo, lse, dmask, x1, h2, mu2, rs2, f))
             x = x2
-        _, e, muE, rsE = K.layernorm_fwd(x, self.P("encoder_norm.weight"), self.P("encoder_norm.bias"),
-                                         out_f32=False, lp_dtype=dt, save_stats=save)
+            h1, mu1, rs1 = hn, mun, rsn
+        e, muE, rsE = h1, mu1, rs1  # the last seam normalised with encoder_norm
         z = K.linear_fwd(e, self.W("feature_map.0.weight"), self.P("feature_map.0.bias"), out_dtype=_F32)
         feats, _, muF, rsF = K.layernorm_fwd(z, self.P("feature_map.1.weight"), self.P("feature_map.1.bias"),
                                              relu=True, dropout_p=p, seed=self.seed(1), seed_base=self.sb, save_stats=save)
@@ -669,11 +693,17 @@ class _Schedule:
                                 dropout_p=p, seed=self.seed(1), seed_base=self.sb, want_f32=False, lp_dtype=dt,
                                 dgamma=G("feature_map.1.weight"), dbeta=G("feature_map.1.bias"), ws=ws, defer=cs)
         wgrad(dz, S["e"], "feature_map.0.weight", "feature_map.0.bias")
-        de = K.linear_dgrad(dz, self.W("feature_map.0.weight"), out_dtype=_F32)
         # encoder_norm; emit the masked lp gradient for the last layer's dropout2
-        dx, g2 = K.layernorm_bwd(de, S["xL"], S["muE"], S["rsE"], self.P("encoder_norm.weight"), lp_dtype=dt,
-                                 lp_dropout_p=p, lp_seed=self.seed(103 + 4 * (L - 1)), seed_base=self.sb,
-                                 dgamma=G("encoder_norm.weight"), dbeta=G("encoder_norm.bias"), ws=ws, defer=cs)
+        if self.fused_ln:
+            dx, g2 = K.linear_ln_bwd(dz, self.W("feature_map.0.weight"), S["xL"], S["muE"], S["rsE"],
+                                     self.P("encoder_norm.weight"), lp_dtype=dt, lp_dropout_p=p,
+                                     lp_seed=self.seed(103 + 4 * (L - 1)), seed_base=self.sb,
+                                     dgamma=G("encoder_norm.weight"), dbeta=G("encoder_norm.bias"), ws=ws, defer=cs)
+        else:
+            de = K.linear_dgrad(dz, self.W("feature_map.0.weight"), out_dtype=_F32)
+            dx, g2 = K.layernorm_bwd(de, S["xL"], S["muE"], S["rsE"], self.P("encoder_norm.weight"), lp_dtype=dt,
+                                     lp_dropout_p=p, lp_seed=self.seed(103 + 4 * (L - 1)), seed_base=self.sb,
+                                     dgamma=G("encoder_norm.weight"), dbeta=G("encoder_norm.bias"), ws=ws, defer=cs)
         ready(["encoder_norm.", "feature_map.", "cls_head."])
         for l in reversed(range(L)):
             pre = f"multimodal_encoder.layers.{l}."
@@ -683,11 +713,17 @@ class _Schedule:
             dzf = K.linear_dgrad(g2, self.W(pre + "linear2.weight"), out_dtype=dt, gate=f, gate_scale=sd)
             # linear1 (ReLU + dropout folded into the gate above)
             wgrad(dzf, h2, pre + "linear1.weight", pre + "linear1.bias")
-            dh2 = K.linear_dgrad(dzf, self.W(pre + "linear1.weight"), out_dtype=_F32)
-            # norm2 + residual; masked lp gradient for dropout1
-            dx1, g1 = K.layernorm_bwd(dh2, x1, mu2, rs2, self.P(pre + "norm2.weight"), dres=dx, lp_dtype=dt,
-                                      lp_dropout_p=p, lp_seed=self.seed(101 + 4 * l), seed_base=self.sb,
-                                      dgamma=G(pre + "norm2.weight"), dbeta=G(pre + "norm2.bias"), ws=ws, defer=cs)
+            # norm2 + residual; masked lp gradient for dropout1 (bf16: one rp_gemm_ln_bwd launch)
+            if self.fused_ln:
+                dx1, g1 = K.linear_ln_bwd(dzf, self.W(pre + "linear1.weight"), x1, mu2, rs2, self.P(pre + "norm2.weight"),
+                                          dres=dx, lp_dtype=dt, lp_dropout_p=p, lp_seed=self.seed(101 + 4 * l),
+                                          seed_base=self.sb, dgamma=G(pre + "norm2.weight"),
+                                          dbeta=G(pre + "norm2.bias"), ws=ws, defer=cs)
+            else:
+                dh2 = K.linear_dgrad(dzf, self.W(pre + "linear1.weight"), out_dtype=_F32)
+                dx1, g1 = K.layernorm_bwd(dh2, x1, mu2, rs2, self.P(pre + "norm2.weight"), dres=dx, lp_dtype=dt,
+                                          lp_dropout_p=p, lp_seed=self.seed(101 + 4 * l), seed_base=self.sb,
+                                          dgamma=G(pre + "norm2.weight"), dbeta=G(pre + "norm2.bias"), ws=ws, defer=cs)
             # out_proj
             wgrad(g1, o, pre + "self_attn.out_proj.weight", pre + "self_attn.out_proj.bias")
             do = K.linear_dgrad(g1, self.W(pre + "self_attn.out_proj.weight"), out_dtype=dt)
@@ -696,13 +732,20 @@ class _Schedule:
                               out_lo=olo)
             # in_proj
             wgrad(dqkv, h1, pre + "self_attn.in_proj_weight", pre + "self_attn.in_proj_bias")
-            dh1 = K.linear_dgrad(dqkv, self.W(pre + "self_attn.in_proj_weight"), out_dtype=_F32)
             # norm1 + residual; masked lp gradient for the previous layer's dropout2
             last = l == 0
-            dx, g2 = K.layernorm_bwd(dh1, x, mu1, rs1, self.P(pre + "norm1.weight"), dres=dx1,
-                                     lp_dtype=None if last else dt, lp_dropout_p=0.0 if last else p,
-                                     lp_seed=0 if last else self.seed(103 + 4 * (l - 1)), seed_base=self.sb,
-                                     dgamma=G(pre + "norm1.weight"), dbeta=G(pre + "norm1.bias"), ws=ws, defer=cs)
+            if self.fused_ln:
+                dx, g2 = K.linear_ln_bwd(dqkv, self.W(pre + "self_attn.in_proj_weight"), x, mu1, rs1,
+                                         self.P(pre + "norm1.weight"), dres=dx1, lp_dtype=None if last else dt,
+                                         lp_dropout_p=0.0 if last else p,
+                                         lp_seed=0 if last else self.seed(103 + 4 * (l - 1)), seed_base=self.sb,
+                                         dgamma=G(pre + "norm1.weight"), dbeta=G(pre + "norm1.bias"), ws=ws, defer=cs)
+            else:
+                dh1 = K.linear_dgrad(dqkv, self.W(pre + "self_attn.in_proj_weight"), out_dtype=_F32)
+                dx, g2 = K.layernorm_bwd(dh1, x, mu1, rs1, self.P(pre + "norm1.weight"), dres=dx1,
+                                         lp_dtype=None if last else dt, lp_dropout_p=0.0 if last else p,
+                                         lp_seed=0 if last else self.seed(103 + 4 * (l - 1)), seed_base=self.sb,
+                                         dgamma=G(pre + "norm1.weight"), dbeta=G(pre + "norm1.bias"), ws=ws, defer=cs)
             ready([pre])
         if deferred:
             flush_group()

@@ -44,6 +44,23 @@ class LnBwdArgs(ctypes.Structure):
                 ("ld_part", c_i64), ("seed_base", c_vp)]
 
 
+class MhaGeneralArgs(ctypes.Structure):
+    _fields_ = [("q", c_vp), ("ldq", c_i64), ("k", c_vp), ("ldk", c_i64), ("v", c_vp), ("ldv", c_i64), ("B", c_i),
+                ("Tq", c_i), ("Tk", c_i), ("H", c_i), ("head_dim", c_i), ("scale", c_f), ("mask", c_vp),
+                ("mask_sb", c_i64), ("mask_sh", c_i64), ("mask_sq", c_i64), ("mask_sk", c_i64), ("probs", c_vp),
+                ("out", c_vp), ("ldo", c_i64), ("dout", c_vp), ("lddo", c_i64), ("dscores", c_vp), ("dq", c_vp),
+                ("lddq", c_i64), ("dk", c_vp), ("lddk", c_i64), ("dv", c_vp), ("lddv", c_i64)]
+
+
+class GemmLnArgs(ctypes.Structure):
+    _fields_ = [("A", c_vp), ("lda", c_i64), ("W", c_vp), ("ldw", c_i64), ("bias", c_vp), ("dropout_p", c_f),
+                ("dropout_seed", c_u32), ("seed_base", c_vp), ("residual", c_vp), ("ldr", c_i64), ("x_out", c_vp),
+                ("ldx_out", c_i64), ("gamma", c_vp), ("beta", c_vp), ("eps", c_f), ("h_out", c_vp), ("ldh", c_i64),
+                ("mean", c_vp), ("rstd", c_vp), ("x", c_vp), ("ldx", c_i64), ("dres", c_vp), ("lddres", c_i64),
+                ("dx", c_vp), ("lddx", c_i64), ("dx_lp", c_vp), ("lddx_lp", c_i64), ("lp_dropout_p", c_f),
+                ("lp_seed", c_u32), ("dgamma_part", c_vp), ("dbeta_part", c_vp), ("ld_part", c_i64)]
+
+
 class WgradItem(ctypes.Structure):
     _fields_ = [("dY", c_vp), ("X", c_vp), ("dW", c_vp), ("db", c_vp), ("M", c_i64), ("N", c_i64), ("ldy", c_i64),
                 ("ldx", c_i64)]
@@ -77,6 +94,8 @@ _SIGNATURES = {
     "rp_gemm_wgrad_workspace": (c_i64, [c_i64, c_i64, c_i64]),
     "rp_gemm_wgrad": (c_i, [c_i, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i, c_vp, c_i64, c_vp]),
     "rp_gemm_wgrad_grouped": (c_i, [c_i64, c_vp, c_i, c_i, c_vp]),
+    "rp_gemm_ln_fwd": (c_i, [c_i64, c_i64, ctypes.POINTER(GemmLnArgs), c_vp]),
+    "rp_gemm_ln_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(GemmLnArgs), c_vp]),
     "rp_layernorm_fwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnFwdArgs), c_vp]),
     "rp_layernorm_bwd_blocks": (c_i64, [c_i64]),
     "rp_layernorm_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnBwdArgs), c_vp]),
@@ -95,6 +114,8 @@ _SIGNATURES = {
     "rp_attn_bwd_dq": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp, c_vp]),
     "rp_mha_dropmask_elems": (c_i64, [c_i, c_i, c_i, c_i]),
     "rp_mha_fwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_vp]),
+    "rp_mha_general_fwd": (c_i, [ctypes.POINTER(MhaGeneralArgs), c_vp]),
+    "rp_mha_general_bwd": (c_i, [ctypes.POINTER(MhaGeneralArgs), c_vp]),
     "rp_mha_bwd": (c_i, [c_i, ctypes.POINTER(MhaArgs), c_i, c_vp]),
     "rp_pad_rows": (c_i, [c_vp, c_i, c_vp, c_i, c_i, c_i, c_f, c_vp, c_vp]),
     "rp_tiou_hits": (c_i, [c_vp, c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_i, c_i, c_vp, c_vp]),

@@ -1007,19 +1007,6 @@ __device__ __forceinline__ void dma16b(const rp_srd& srd, uint32_t voff, uint32_
       : "s"(lds), "v"(voff), "s"(srd), "s"(soff)
       : "memory");
 }
-__device__ __forceinline__ void dma4b(const rp_srd& srd, uint32_t voff, uint32_t soff, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dword %2, %3, %4 offen lds\n\t"
-      "s_nop 0\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(lds), "v"(voff), "s"(srd), "s"(soff)
-      : "memory");
-}
 
 // rows [row0, row0 + 64) of a [rows][64] bf16 operand -> the swizzled 8 KB image (two 1 KB pieces per
 // wave, as dma_rows64), descriptor form for full tiles: piece j of wave w is

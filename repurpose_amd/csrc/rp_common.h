@@ -153,3 +153,26 @@ __device__ __forceinline__ int rp_xcd_remap(int bid, int nwg) {
   int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
   return base + i;
 }
+
+// One LDS-DMA wave instruction (global_load_lds_dwordx4): lane l's 16 bytes at g land at LDS byte
+// address lds + 16 l.  Inline asm on purpose: the compiler does not track it, so it inserts no
+// conservative vmcnt(0) before the LDS reads of a pipelined loop (its alias analysis cannot tell
+// that they read another ring slot) — the caller orders every DMA before its readers with a counted
+// s_waitcnt vmcnt + barrier.  m0 is saved and restored around it.
+__device__ __forceinline__ void rp_dma16(const void* g, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, off\n\t"
+      "s_nop 0\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "v"(g)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t rp_lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}

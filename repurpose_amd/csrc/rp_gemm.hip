@@ -1318,6 +1318,289 @@ int wgrad8_plan(int64_t M, int64_t N, int64_t K, int& splits, int64_t& kchunk) {
   return 256;
 }
 
+
+// ============== GEMM + LayerNorm with full-row tiles (d_model = 512 output columns) ==============
+// The four N = 512 GEMMs of an encoder layer feed a LayerNorm (reference: the pre-LN encoder layer
+// built at models/MMCTransformer.py:41-55 — x1 = x + drop(out_proj(.)), norm2(x1); x2 = x1 +
+// drop(linear2(.)), next layer's norm1(x2) / encoder_norm; and their backward).  With 128 x 128 tiles
+// the GEMM wrote the fp32 rows and a separate LayerNorm pass read them back (33.5 MB each way per
+// launch at M = 16384), and the LayerNorm backward read the fp32 dgrad output back the same way.
+// Here one workgroup owns 64 WHOLE rows (64 x 512 outputs, 8 waves, wave w the 64 columns
+// [64w, 64w + 64)), so the LayerNorm runs in the GEMM's epilogue on rows staged in LDS:
+//   fwd: x_out = dropout(A W^T + bias) + residual (fp32, the residual stream), h = LN(x_out) (bf16),
+//        mean / rstd saved — the arithmetic of gemm_epilogue followed by ln_fwd_kernel<8>, op for op;
+//   bwd: dh = dY W (kept in LDS, never written), then ln_bwd_kernel<8>'s row loop on it (dx fp32 with
+//        the residual gradient added, the dropout-masked bf16 copy for the next GEMM, gamma / beta
+//        partials per 32-row block in that kernel's order and layout).
+// The MFMA products are the 128 x 128 kernel's (16x16x32 bf16, K in 64-deep steps, k ascending), so
+// every output is bitwise the unfused pair's.  Main loop: two LDS stages of (A 64 x 64, B 512 x 64)
+// = 72 KiB each, one barrier per K step, one workgroup per CU (256 row blocks at M = 16384).
+constexpr int GL_BM = 64, GL_N = 512, GL_NT = 512, GL_BK = 64;
+constexpr int GL_AB = GL_BM * GL_BK * 2;  // A image of a stage (8 KiB)
+constexpr int GL_BB = GL_N * GL_BK * 2;   // B image(s) of a stage (64 KiB)
+constexpr int GL_STAGE = GL_AB + GL_BB;
+constexpr int GL_CST = GL_N + 4;          // fp32 row stride of the staged output rows
+constexpr int GL_LDS = 2 * GL_STAGE;
+static_assert(GL_BM * GL_CST * 4 <= GL_LDS, "staged rows fit the main-loop LDS");
+
+struct GlnDev {
+  const bf16* A; int64_t lda;
+  const bf16* W; int64_t ldw;  // fwd: W [512][K] (k-major, nn.Linear weight); bwd: W [K][512] (n-major)
+  const float* bias;
+  uint32_t drop_thresh; float drop_scale; uint32_t drop_seed; const uint32_t* seed_base;
+  const float* residual; int64_t ldr;
+  float* xo; int64_t ldxo;
+  const float* gamma; const float* beta; float eps;
+  bf16* h; int64_t ldh;
+  float* mean; float* rstd;
+  const float* x; int64_t ldx;
+  const float* dres; int64_t lddres;
+  float* dx; int64_t lddx;
+  bf16* dx_lp; int64_t lddx_lp; uint32_t lp_thresh; float lp_scale; uint32_t lp_seed;
+  float* dgamma_part; float* dbeta_part; int64_t ld_part;
+};
+
+// Main loop: a four-slot ring of 32-deep K steps (A 64 x 32 = 4 KiB, B 512 x 32 = 32 KiB per slot),
+// three steps in flight (the DMA of step t + 3 goes into the slot step t - 1 read, issued right after
+// the barrier that ends those reads), counted s_waitcnt vmcnt + raw barrier per step.  A two-stage
+// 64-deep version with a full drain per step measured slower than the unfused pair at K = 2048 (one
+// workgroup per CU cannot hide a 72 KiB fill per step): this one keeps ~108 KiB in flight per CU.
+// Pieces per slot: A 4 (waves 0-3), B 32 (four per wave) -> 5 DMA instructions for waves 0-3, 4 for 4-7.
+constexpr int GL_KS = 32;                    // K per ring slot
+constexpr int GL_SA = GL_BM * GL_KS * 2;     // A image of a slot (4 KiB)
+constexpr int GL_SLOT = GL_SA + GL_N * GL_KS * 2;
+constexpr int GL_RING = 4;
+static_assert(GL_RING * GL_SLOT <= GL_LDS, "ring fits");
+
+template <bool BKM>
+__device__ __forceinline__ void gln_issue(const GlnDev& a, int64_t m0, int64_t k0, uint32_t slot, int w, int lane) {
+  if (w < 4) {  // A: [64 rows][32 k], 64-B rows, kswz32
+    const int r = w * 16 + (lane >> 2);
+    rp_dma16(a.A + (m0 + r) * a.lda + k0 + kswz32(r, lane & 3) * 8, slot + w * 1024);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int I = w * 4 + j;
+    const bf16* src;
+    if constexpr (BKM) {  // [512 rows][32 k], 64-B rows, kswz32
+      const int r = I * 16 + (lane >> 2);
+      src = a.W + (int64_t)r * a.ldw + k0 + kswz32(r, lane & 3) * 8;
+    } else {  // four [32 k][128 cols] images (8 KiB), 256-B rows, mswz
+      const int k = (I & 7) * 4 + (lane >> 4);
+      src = a.W + (k0 + k) * a.ldw + (I >> 3) * 128 + mswz(k, lane & 15) * 8;
+    }
+    rp_dma16(src, slot + GL_SA + I * 1024);
+  }
+}
+
+// acc[i][j][r] = C[m0 + 16 i + 4 g + r][64 w + 16 j + c] over the whole K
+template <bool BKM>
+__device__ __forceinline__ void gln_mainloop(const GlnDev& a, int64_t m0, int64_t K, char* lds, f32x4 (&acc)[4][4],
+                                             int w, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (int)(K / GL_KS);
+  const uint32_t base = rp_lds_addr(lds);
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+    if (t < nk) gln_issue<BKM>(a, m0, (int64_t)t * GL_KS, base + t * GL_SLOT, w, lane);
+  for (int t = 0; t < nk; ++t) {
+    // DMA instructions issued after step t's: those of steps t+1, t+2 (if they exist)
+    const int after = (nk - 1 - t) < 2 ? (nk - 1 - t) : 2;
+    if (w < 4) {
+      if (after == 2) rp_waitcnt<10, 15>(); else if (after == 1) rp_waitcnt<5, 15>(); else rp_waitcnt<0, 15>();
+    } else {
+      if (after == 2) rp_waitcnt<8, 15>(); else if (after == 1) rp_waitcnt<4, 15>(); else rp_waitcnt<0, 15>();
+    }
+    rp_raw_barrier();
+    if (t + 3 < nk) gln_issue<BKM>(a, m0, (int64_t)(t + 3) * GL_KS, base + ((t + 3) & 3) * GL_SLOT, w, lane);
+    const char* cur = lds + (t & 3) * GL_SLOT;
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag_k_swz<32>(cur, i * 16, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bfr[j] = BKM ? frag_k_swz<32>(cur + GL_SA, 64 * w + 16 * j, 0, lane)
+                   : frag_m_swz(cur + GL_SA + (w >> 1) * 8192, (w & 1) * 64 + 16 * j, 0, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();  // every wave's reads of the ring are done before the epilogue reuses the LDS
+}
+
+__device__ __forceinline__ void gln_stage(const f32x4 (&acc)[4][4], float* cs, int w, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[(i * 16 + g * 4 + r) * GL_CST + 64 * w + j * 16 + c] = acc[i][j][r];
+}
+
+__device__ __forceinline__ void ld8(float (&v)[8], const float* p) {
+  const float4 q0 = *reinterpret_cast<const float4*>(p), q1 = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = q0.x; v[1] = q0.y; v[2] = q0.z; v[3] = q0.w; v[4] = q1.x; v[5] = q1.y; v[6] = q1.z; v[7] = q1.w;
+}
+__device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void st8bf(bf16* p, const float (&v)[8]) {
+  uint4 q;
+  bf16* e = reinterpret_cast<bf16*>(&q);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = (bf16)v[j];
+  *reinterpret_cast<uint4*>(p) = q;
+}
+
+__global__ __launch_bounds__(GL_NT, 1) void gemm_ln_fwd_kernel(int64_t M, int64_t K, const GlnDev a) {
+  __shared__ __attribute__((aligned(1024))) char lds[GL_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t m0 = (int64_t)blockIdx.x * GL_BM;
+  f32x4 acc[4][4];
+  gln_mainloop<true>(a, m0, K, lds, acc, w, lane);
+  // this wave's rows w*8 .. w*8+7, lane l holds columns 8l .. 8l+7 (ln_fwd_kernel<8>'s layout)
+  const int c0 = lane * 8;
+  float res[8][8];
+#pragma unroll
+  for (int rr = 0; rr < 8; ++rr) ld8(res[rr], a.residual + (m0 + w * 8 + rr) * a.ldr + c0);
+  float bi[8], gm[8], bt[8];
+  ld8(bi, a.bias + c0);
+  ld8(gm, a.gamma + c0);
+  ld8(bt, a.beta + c0);
+  float* cs = reinterpret_cast<float*>(lds);
+  gln_stage(acc, cs, w, lane);
+  __syncthreads();
+  const uint32_t dseed = a.drop_thresh ? rp_seed_eff(a.seed_base, a.drop_seed) : 0u;
+#pragma unroll 2
+  for (int rr = 0; rr < 8; ++rr) {
+    const int row = w * 8 + rr;
+    const int64_t m = m0 + row;
+    float v[8];
+    ld8(v, cs + row * GL_CST + c0);
+    // gemm_epilogue (MODE 0, fp32 C): alpha (1) * acc + bias, dropout, + residual
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += bi[e];
+    if (a.drop_thresh) {
+      const uint32_t kb = rp_keep_bits<8>(dseed, (uint32_t)(m * GL_N + c0), a.drop_thresh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * a.drop_scale : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += res[rr][e];
+    st8(a.xo + m * a.ldxo + c0, v);
+    // ln_fwd_kernel<8>
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i];
+    const float mean = rp_wave_sum(s) * (1.f / GL_N);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = v[i] - mean;
+      q += d * d;
+    }
+    const float var = rp_wave_sum(q) * (1.f / GL_N);
+    const float rstd = rsqrtf(var + a.eps);
+    float y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) y[i] = (v[i] - mean) * rstd * gm[i] + bt[i];
+    st8bf(a.h + m * a.ldh + c0, y);
+    if (lane == 0) {
+      a.mean[m] = mean;
+      a.rstd[m] = rstd;
+    }
+  }
+}
+
+__global__ __launch_bounds__(GL_NT, 1) void gemm_ln_bwd_kernel(int64_t M, int64_t K, const GlnDev a) {
+  __shared__ __attribute__((aligned(1024))) char lds[GL_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t m0 = (int64_t)blockIdx.x * GL_BM;
+  f32x4 acc[4][4];
+  gln_mainloop<false>(a, m0, K, lds, acc, w, lane);
+  const int c0 = lane * 8;
+  float gam[8];
+  ld8(gam, a.gamma + c0);
+  float* cs = reinterpret_cast<float*>(lds);
+  gln_stage(acc, cs, w, lane);
+  __syncthreads();
+  const uint32_t lseed = a.lp_thresh ? rp_seed_eff(a.seed_base, a.lp_seed) : 0u;
+  // ln_bwd_kernel<8>, one 32-row block at a time (its rows w, w+8, w+16, w+24 per wave, in that order)
+#pragma unroll 1
+  for (int blk = 0; blk < 2; ++blk) {
+    float pg[8], pb[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pg[i] = pb[i] = 0.f;
+#pragma unroll 1
+    for (int rr = w; rr < 32; rr += 8) {
+      const int row = blk * 32 + rr;
+      const int64_t m = m0 + row;
+      float g[8], x[8], r[8];
+      ld8(x, a.x + m * a.ldx + c0);
+      if (a.dres) ld8(r, a.dres + m * a.lddres + c0);
+      ld8(g, cs + row * GL_CST + c0);
+      const float mu = a.mean[m], rs = a.rstd[m];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        x[i] = (x[i] - mu) * rs;
+        const float gg = g[i] * gam[i];
+        s1 += gg;
+        s2 += gg * x[i];
+        pg[i] += g[i] * x[i];
+        pb[i] += g[i];
+      }
+      s1 = rp_wave_sum(s1) * (1.f / GL_N);
+      s2 = rp_wave_sum(s2) * (1.f / GL_N);
+      float dx[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dx[i] = rs * (g[i] * gam[i] - s1 - x[i] * s2);
+      if (a.dres) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dx[i] += r[i];
+      }
+      st8(a.dx + m * a.lddx + c0, dx);
+      if (a.dx_lp) {
+        if (a.lp_thresh) {
+          const uint32_t kb = rp_keep_bits<8>(lseed, (uint32_t)(m * GL_N + c0), a.lp_thresh);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dx[i] = ((kb >> i) & 1u) ? dx[i] * a.lp_scale : 0.f;
+        }
+        st8bf(a.dx_lp + m * a.lddx_lp + c0, dx);
+      }
+    }
+    // the block's gamma / beta partial row (rows 0..31 of the staging area are consumed by now)
+    __syncthreads();
+    float* red = cs;  // [2][8 waves][512]
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[(0 * 8 + w) * GL_N + c0 + i] = pg[i];
+      red[(1 * 8 + w) * GL_N + c0 + i] = pb[i];
+    }
+    __syncthreads();
+    {
+      const int c = tid;  // GL_NT == GL_N: one column per thread
+      float sg = 0.f, sb = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        sg += red[(0 * 8 + k) * GL_N + c];
+        sb += red[(1 * 8 + k) * GL_N + c];
+      }
+      const int64_t pr = m0 / 32 + blk;
+      if (a.dgamma_part) a.dgamma_part[pr * a.ld_part + c] = sg;
+      if (a.dbeta_part) a.dbeta_part[pr * a.ld_part + c] = sb;
+    }
+    __syncthreads();
+  }
+}
 }  // namespace
 
 extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int a_kmajor,
@@ -1464,4 +1747,70 @@ extern "C" int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const v
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(g + g2)), dim3(256), 0, s, slab, splits, n, dW, bslab, M, db,
                      (int)g, accumulate);
   return rp_check_launch("rp_gemm_wgrad");
+}
+
+// ---- GEMM + LayerNorm entry points (include/rp_api.h) ----
+static int gemm_ln_common(const char* fn, int64_t M, int64_t K, const rp_gemm_ln_args* p, GlnDev& d) {
+  RP_REQUIRE(p, "%s: null args", fn);
+  RP_REQUIRE(M >= 0 && K > 0 && M % GL_BM == 0 && K % GL_BK == 0, "%s: M must be a multiple of 64 and K of 64 (M=%lld K=%lld)",
+             fn, (long long)M, (long long)K);
+  RP_REQUIRE(p->A && p->W && p->gamma, "%s: null operand", fn);
+  RP_REQUIRE(rp_aligned16(p->A) && rp_aligned16(p->W) && rp_aligned16(p->gamma), "%s: 16-byte alignment required", fn);
+  RP_REQUIRE(p->lda >= K && p->lda % 8 == 0, "%s: bad lda", fn);
+  RP_REQUIRE(p->dropout_p >= 0.f && p->dropout_p < 1.f, "%s: dropout_p must be in [0, 1)", fn);
+  d = GlnDev{};
+  d.A = (const bf16*)p->A; d.lda = p->lda; d.W = (const bf16*)p->W; d.ldw = p->ldw;
+  d.gamma = p->gamma;
+  d.drop_thresh = rp_dropout_thresh(p->dropout_p);
+  d.drop_scale = p->dropout_p > 0.f ? 1.f / (1.f - p->dropout_p) : 1.f;
+  d.drop_seed = p->dropout_seed;
+  d.seed_base = p->seed_base;
+  d.mean = p->mean; d.rstd = p->rstd;
+  RP_REQUIRE(p->mean && p->rstd, "%s: null mean / rstd", fn);
+  return RP_OK;
+}
+
+extern "C" int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, void* stream) {
+  GlnDev d;
+  const int rc = gemm_ln_common("rp_gemm_ln_fwd", M, K, p, d);
+  if (rc) return rc;
+  RP_REQUIRE(p->ldw >= K && p->ldw % 8 == 0, "rp_gemm_ln_fwd: W must be [512][ldw >= K]");
+  RP_REQUIRE(p->bias && p->beta && p->residual && p->x_out && p->h_out, "rp_gemm_ln_fwd: null operand");
+  RP_REQUIRE(rp_aligned16(p->bias) && rp_aligned16(p->beta) && rp_aligned16(p->residual) && rp_aligned16(p->x_out) &&
+                 rp_aligned16(p->h_out) && p->ldr % 4 == 0 && p->ldx_out % 4 == 0 && p->ldh % 8 == 0 &&
+                 p->ldr >= 512 && p->ldx_out >= 512 && p->ldh >= 512,
+             "rp_gemm_ln_fwd: output / residual alignment or leading dims");
+  RP_REQUIRE(!d.drop_thresh || M * 512 < (int64_t)UINT32_MAX, "rp_gemm_ln_fwd: dropout index overflow");
+  d.bias = p->bias; d.beta = p->beta; d.eps = p->eps;
+  d.residual = p->residual; d.ldr = p->ldr;
+  d.xo = p->x_out; d.ldxo = p->ldx_out;
+  d.h = (bf16*)p->h_out; d.ldh = p->ldh;
+  if (M == 0) return RP_OK;
+  hipLaunchKernelGGL(gemm_ln_fwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
+  return rp_check_launch("rp_gemm_ln_fwd");
+}
+
+extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, void* stream) {
+  GlnDev d;
+  const int rc = gemm_ln_common("rp_gemm_ln_bwd", M, K, p, d);
+  if (rc) return rc;
+  RP_REQUIRE(p->ldw >= 512 && p->ldw % 8 == 0, "rp_gemm_ln_bwd: W must be [K][ldw >= 512]");
+  RP_REQUIRE(p->x && p->dx, "rp_gemm_ln_bwd: null x / dx");
+  RP_REQUIRE(rp_aligned16(p->x) && rp_aligned16(p->dx) && (!p->dres || rp_aligned16(p->dres)) &&
+                 (!p->dx_lp || rp_aligned16(p->dx_lp)) && p->ldx % 4 == 0 && p->lddx % 4 == 0 &&
+                 p->lddres % 4 == 0 && p->lddx_lp % 8 == 0 && p->ldx >= 512 && p->lddx >= 512 &&
+                 (!p->dres || p->lddres >= 512) && (!p->dx_lp || p->lddx_lp >= 512),
+             "rp_gemm_ln_bwd: alignment or leading dims");
+  RP_REQUIRE(p->lp_dropout_p >= 0.f && p->lp_dropout_p < 1.f, "rp_gemm_ln_bwd: lp_dropout_p must be in [0, 1)");
+  RP_REQUIRE(!p->dgamma_part || p->ld_part >= 512, "rp_gemm_ln_bwd: ld_part < 512");
+  d.x = p->x; d.ldx = p->ldx; d.dres = p->dres; d.lddres = p->lddres;
+  d.dx = p->dx; d.lddx = p->lddx;
+  d.dx_lp = (bf16*)p->dx_lp; d.lddx_lp = p->lddx_lp;
+  d.lp_thresh = rp_dropout_thresh(p->lp_dropout_p);
+  d.lp_scale = p->lp_dropout_p > 0.f ? 1.f / (1.f - p->lp_dropout_p) : 1.f;
+  d.lp_seed = p->lp_seed;
+  d.dgamma_part = p->dgamma_part; d.dbeta_part = p->dbeta_part; d.ld_part = p->ld_part;
+  if (M == 0) return RP_OK;
+  hipLaunchKernelGGL(gemm_ln_bwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
+  return rp_check_launch("rp_gemm_ln_bwd");
 }

@@ -200,6 +200,74 @@ def linear_wgrad_grouped(items, accumulate=True):
         _tock(e0, fl)
 
 
+# ----------------------------------------------------------------------- GEMM + LayerNorm seams
+def linear_ln_fwd(x, W, b, residual, gamma, beta, eps=1e-5, dropout_p=0.0, seed=0, seed_base=None):
+    """One launch (rp_gemm_ln_fwd) for ``y = dropout(x W^T + b) + residual`` (fp32, returned) and
+    ``h = LayerNorm(y)`` (bf16) with its mean / rstd — bitwise linear_fwd(..., residual=...) followed by
+    layernorm_fwd(y, out_f32=False, lp_dtype=bf16).  x [M, K] bf16, W [512, K] bf16, M % 64 == 0.
+    Returns (y, h, mean, rstd)."""
+    _gpu(x, W, b, residual, gamma, beta)
+    _seed_word(seed_base)
+    M, K = x.shape
+    dev = x.device
+    y = torch.empty(M, 512, device=dev, dtype=torch.float32)
+    h = torch.empty(M, 512, device=dev, dtype=torch.bfloat16)
+    mean = torch.empty(M, device=dev, dtype=torch.float32)
+    rstd = torch.empty(M, device=dev, dtype=torch.float32)
+    a = N.GemmLnArgs(A=_p(x).value, lda=x.stride(0), W=_p(W).value, ldw=W.stride(0), bias=_p(b).value,
+                     dropout_p=float(dropout_p), dropout_seed=int(seed) & 0xFFFFFFFF, seed_base=_p(seed_base).value,
+                     residual=_p(residual).value, ldr=residual.stride(0), x_out=_p(y).value, ldx_out=512,
+                     gamma=_p(gamma).value, beta=_p(beta).value, eps=float(eps), h_out=_p(h).value, ldh=512,
+                     mean=_p(mean).value, rstd=_p(rstd).value)
+    e0 = _tick("gemm_ln_fwd")
+    N.call("rp_gemm_ln_fwd", M, K, ctypes.byref(a), _stream(x))
+    _tock(e0, 2.0 * M * 512 * K)
+    return y, h, mean, rstd
+
+
+def linear_ln_bwd(dy, W, x, mean, rstd, gamma, dres=None, lp_dtype=None, lp_dropout_p=0.0, lp_seed=0, dgamma=None,
+                  dbeta=None, defer=None, ws=None, seed_base=None):
+    """One launch (rp_gemm_ln_bwd) for ``dh = dy W`` (dy [M, K] bf16, W [K, 512] bf16) followed by the
+    LayerNorm backward of the LayerNorm whose input was x — bitwise linear_dgrad(dy, W, fp32) then
+    layernorm_bwd(dh, x, mean, rstd, gamma, dres=..., lp_dtype=..., ...); dh is never written.
+    Returns (dx fp32, dx_lp or None); gamma / beta partials as layernorm_bwd (``defer`` / ``ws``)."""
+    _gpu(dy, W, x, mean, rstd, gamma, dres)
+    _seed_word(seed_base)
+    M, K = dy.shape
+    dev = dy.device
+    D = 512
+    dx = torch.empty(M, D, device=dev, dtype=torch.float32)
+    dxl = torch.empty(M, D, device=dev, dtype=lp_dtype) if lp_dtype is not None else None
+    nb = M // 32
+    both = (dgamma is not None and dbeta is not None and dgamma.is_contiguous() and dbeta.is_contiguous()
+            and dbeta.data_ptr() == dgamma.data_ptr() + 4 * D and dgamma.dtype == dbeta.dtype == torch.float32
+            and dgamma.untyped_storage().data_ptr() == dbeta.untyped_storage().data_ptr())
+    ld_part = 2 * D if both else D
+    if both:
+        part = torch.empty(nb, 2 * D, device=dev, dtype=torch.float32)
+        pg, pb = part[:, :D], part[:, D:]
+    else:
+        pg = torch.empty(nb, D, device=dev, dtype=torch.float32) if dgamma is not None else None
+        pb = torch.empty(nb, D, device=dev, dtype=torch.float32) if dbeta is not None else None
+    a = N.GemmLnArgs(A=_p(dy).value, lda=dy.stride(0), W=_p(W).value, ldw=W.stride(0), gamma=_p(gamma).value,
+                     seed_base=_p(seed_base).value, mean=_p(mean).value, rstd=_p(rstd).value, x=_p(x).value,
+                     ldx=x.stride(0), dres=_p(dres).value, lddres=dres.stride(0) if dres is not None else 0,
+                     dx=_p(dx).value, lddx=D, dx_lp=_p(dxl).value, lddx_lp=D, lp_dropout_p=float(lp_dropout_p),
+                     lp_seed=int(lp_seed) & 0xFFFFFFFF, dgamma_part=_p(pg).value, dbeta_part=_p(pb).value,
+                     ld_part=ld_part)
+    e0 = _tick("gemm_ln_bwd")
+    N.call("rp_gemm_ln_bwd", M, K, ctypes.byref(a), _stream(dy))
+    _tock(e0, 2.0 * M * 512 * K)
+    jobs = [(part, dgamma.as_strided((2 * D,), (1,)))] if both else \
+        [(p, o) for p, o in ((pg, dgamma), (pb, dbeta)) if o is not None]
+    if defer is not None:
+        defer.extend(jobs)
+    else:
+        for p, o in jobs:
+            colsum(p, out=o, accumulate=True, ws=ws)
+    return dx, dxl
+
+
 # ------------------------------------------------------------------------------------- LayerNorm
 def layernorm_fwd(x, gamma, beta, eps=1e-5, pe=None, pe_period=1, relu=False, dropout_p=0.0, seed=0,
                   out_f32=True, lp_dtype=None, save_stats=True, seed_base=None):
@@ -446,6 +514,49 @@ def mha_bwd(q, k, v, out, dout, lse, key_valid, B, Tq, Tk, H, scale, dropout_p=0
 
 
 # ------------------------------------------------------------------------------------- focal loss
+def mha_general_fwd(q, k, v, mask4, B, Tq, Tk, H, dk, scale):
+    """General attention core (rp_mha_general_fwd, fp32): q [B*Tq, >= H*dk], k / v [B*Tk, >= H*dk] row
+    views, mask4 None or a uint8 view broadcast to [B, H, Tq, Tk] (any strides).  Returns (out
+    [B*Tq, H*dk], probs [B, H, Tq, Tk]) — probs is the backward's input."""
+    _gpu(q, k, v, mask4)
+    for t in (q, k, v):
+        if t.dtype != torch.float32 or t.stride(1) != 1:
+            raise TypeError("mha_general: fp32 row views with unit column stride")
+    out = torch.empty(B * Tq, H * dk, device=q.device, dtype=torch.float32)
+    probs = torch.empty(B, H, Tq, Tk, device=q.device, dtype=torch.float32)
+    a = _general_args(q, k, v, mask4, B, Tq, Tk, H, dk, scale, probs)
+    a.out, a.ldo = _p(out).value, out.stride(0)
+    N.call("rp_mha_general_fwd", ctypes.byref(a), _stream(q))
+    return out, probs
+
+
+def mha_general_bwd(q, k, v, dout, probs, mask4, B, Tq, Tk, H, dk, scale):
+    """Backward of mha_general_fwd -> (dq, dk, dv) [rows, H*dk] fp32."""
+    _gpu(q, k, v, dout, probs, mask4)
+    dev = q.device
+    dq = torch.empty(B * Tq, H * dk, device=dev, dtype=torch.float32)
+    dkk = torch.empty(B * Tk, H * dk, device=dev, dtype=torch.float32)
+    dv = torch.empty(B * Tk, H * dk, device=dev, dtype=torch.float32)
+    ds = torch.empty_like(probs)
+    a = _general_args(q, k, v, mask4, B, Tq, Tk, H, dk, scale, probs)
+    a.dout, a.lddo, a.dscores = _p(dout).value, dout.stride(0), _p(ds).value
+    a.dq, a.lddq, a.dk, a.lddk, a.dv, a.lddv = _p(dq).value, dq.stride(0), _p(dkk).value, dkk.stride(0), \
+        _p(dv).value, dv.stride(0)
+    N.call("rp_mha_general_bwd", ctypes.byref(a), _stream(q))
+    return dq, dkk, dv
+
+
+def _general_args(q, k, v, mask4, B, Tq, Tk, H, dk, scale, probs):
+    a = N.MhaGeneralArgs(q=_p(q).value, ldq=q.stride(0), k=_p(k).value, ldk=k.stride(0), v=_p(v).value,
+                         ldv=v.stride(0), B=B, Tq=Tq, Tk=Tk, H=H, head_dim=dk, scale=float(scale), probs=_p(probs).value)
+    if mask4 is not None:
+        if mask4.dtype != torch.uint8 or tuple(mask4.shape) != (B, H, Tq, Tk):
+            raise ValueError("mha_general: mask4 must be a uint8 view of shape [B, H, Tq, Tk]")
+        a.mask = _p(mask4).value
+        a.mask_sb, a.mask_sh, a.mask_sq, a.mask_sk = mask4.stride()
+    return a
+
+
 def focal_fwd_sum(x, t, mask=None, alpha=0.7, gamma=2.0):
     _gpu(x, t, mask)
     x, t = x.contiguous().float(), t.contiguous().float()

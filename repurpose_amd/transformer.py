@@ -18,14 +18,16 @@ fused in the epilogue), every LayerNorm rp_layernorm_fwd/bwd, the attention core
 (independent q/k/v row strides, Tq != Tk for cross attention; q/k/v of one input come from ONE
 GEMM into a [rows, 3d] buffer).  Arithmetic is fp32 (exact-f32 MFMA), like the reference.
 
-Masks: ``mask`` is [B, 1, Tk] (per-key padding, the form the reference passes), [B, Tk] (the same),
-or [B, Tq, Tk] whose rows are equal for every query (checked); a key is excluded iff mask == 0, like
-the reference's ``masked_fill(mask == 0, -1e9)`` (:69-71).  A sequence with no valid key at all gets
-the reference's result too: every score is the same constant, so each query averages ALL values
-(including the padded ones) and no gradient reaches q or k (rp_mha empty_rows_uniform).  Masks that
-differ between queries raise NotImplementedError.  Head dims d_k = d_model / num_heads up to 64 run
-on the d_k = 64 kernels with each head zero-padded to 64 (zero columns add nothing to QK^T; the
-scale stays 1/sqrt(d_k)); larger head dims raise NotImplementedError.
+Masks follow the reference exactly: ``mask.unsqueeze(1)`` broadcast against the scores [B, H, Tq, Tk]
+(:69-71; a mask that does not broadcast raises, as masked_fill does), a score is replaced by -1e9 iff
+mask == 0.  Two HIP paths:
+  * per-key masks (the [B, 1, Tk] padding mask the reference passes, a [B, Tq, Tk] mask whose rows are
+    equal, no mask) with head dims d_k <= 64: the flash kernels rp_mha_fwd/bwd (heads below 64 are
+    zero-padded to 64 — zero columns add nothing to QK^T, the scale stays 1/sqrt(d_k)); a sequence with
+    no valid key averages all values, the -1e9 result (rp_mha empty_rows_uniform);
+  * everything else — d_k > 64, masks that differ between queries (causal) or heads (a [B, Tk] mask,
+    which the reference's unsqueeze(1) broadcasts as [1, B, 1, Tk], i.e. per HEAD when B == H):
+    rp_mha_general_fwd/bwd, the same formula with the probabilities materialised.
 Residual-branch dropout (p > 0, training) is torch's nn.Dropout on the branch, as in the reference.
 """
 import math
@@ -116,21 +118,48 @@ def _layernorm(ln, x):
     return _LayerNormFn.apply(x, ln.weight, ln.bias, float(ln.eps))
 
 
-def _key_valid(mask, B, Tq, Tk, device):
+def _mask4(mask, B, H, Tq, Tk):
+    """The reference's ``mask.unsqueeze(1)`` broadcast to the scores [B, H, Tq, Tk] (models/transformer.py
+    :69-71) as a uint8 keep view (strides 0 on broadcast dimensions), or None."""
     if mask is None:
+        return None
+    m = mask.unsqueeze(1)
+    shape = torch.broadcast_shapes(m.shape, (B, H, Tq, Tk))  # raises where masked_fill would
+    if tuple(shape) != (B, H, Tq, Tk):
+        raise RuntimeError(f"MultiHeadAttention: mask {tuple(mask.shape)} broadcasts the scores ({B}, {H}, {Tq}, "
+                           f"{Tk}) to {tuple(shape)}")
+    return (m != 0).to(torch.uint8).expand(B, H, Tq, Tk)
+
+
+def _key_valid(m4, B, Tk, device):
+    """[B, Tk] uint8 key mask if the broadcast mask depends only on (batch, key), else None."""
+    if m4 is None:
         return torch.ones(B, Tk, device=device, dtype=torch.uint8)
-    m = mask
-    if m.dim() == 3:
-        if m.shape[1] != 1:
-            if tuple(m.shape) != (B, Tq, Tk):
-                raise ValueError(f"MultiHeadAttention: mask shape {tuple(mask.shape)} does not match ({B}, {Tq}, {Tk})")
-            if not bool(((m != 0) == (m[:, :1] != 0)).all()):
-                raise NotImplementedError("MultiHeadAttention: masks that differ between queries are not supported "
-                                          "(key-padding masks [B, 1, Tk], or [B, Tq, Tk] with equal rows)")
-        m = m[:, 0]
-    if tuple(m.shape) != (B, Tk):
-        raise ValueError(f"MultiHeadAttention: mask shape {tuple(mask.shape)} does not match keys ({B}, {Tk})")
-    return (m != 0).to(torch.uint8).contiguous()
+    if m4.stride(1) == 0 and m4.stride(2) == 0:
+        return m4[:, 0, 0, :].contiguous()
+    if bool((m4 == m4[:, :1, :1, :]).all()):
+        return m4[:, 0, 0, :].contiguous()
+    return None
+
+
+class _GeneralAttnFn(torch.autograd.Function):
+    """softmax(scale * Q K^T, masked with -1e9) V for any head dim and any broadcast mask
+    (rp_mha_general_fwd/bwd)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, m4, B, Tq, Tk, H, dk, scale):
+        out, probs = K.mha_general_fwd(q, k, v, m4, B, Tq, Tk, H, dk, scale)
+        ctx.save_for_backward(q, k, v, probs)
+        ctx.m4 = m4
+        ctx.dims = (B, Tq, Tk, H, dk, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, probs = ctx.saved_tensors
+        B, Tq, Tk, H, dk, scale = ctx.dims
+        dq, dkk, dv = K.mha_general_bwd(q, k, v, dout.contiguous(), probs, ctx.m4, B, Tq, Tk, H, dk, scale)
+        return dq, dkk, dv, None, None, None, None, None, None, None
 
 
 # --------------------------------------------------------------------------------- modules
@@ -194,9 +223,9 @@ class MultiHeadAttention(nn.Module):
         self.num_heads = num_heads
         self.d_model = d_model
         self.d_k = d_model // num_heads
-        if self.d_k > 64 or self.d_k * num_heads != d_model:
-            raise NotImplementedError(f"MultiHeadAttention: d_model {d_model} / {num_heads} heads (head dims up to 64 "
-                                      "dividing d_model; the HIP kernels implement 64, smaller heads are zero-padded)")
+        if self.d_k * num_heads != d_model:
+            raise ValueError(f"MultiHeadAttention: d_model {d_model} is not divisible by {num_heads} heads "
+                             "(the reference's view(bs, -1, num_heads, d_k) needs it)")
         self.q_linear = nn.Linear(d_model, d_model)
         self.k_linear = nn.Linear(d_model, d_model)
         self.v_linear = nn.Linear(d_model, d_model)
@@ -224,8 +253,12 @@ class MultiHeadAttention(nn.Module):
             (qp,) = self._project(q, [self.q_linear])
             (kp,) = self._project(k, [self.k_linear])
             (vp,) = self._project(v, [self.v_linear])
-        kv = _key_valid(mask, B, Tq, Tk, q.device)
         H, dk = self.num_heads, self.d_k
+        m4 = _mask4(mask, B, H, Tq, Tk)
+        kv = _key_valid(m4, B, Tk, q.device) if dk <= 64 else None
+        if kv is None:  # head dims above 64 or masks varying per query / head: the general core
+            att = _GeneralAttnFn.apply(qp, kp, vp, m4, B, Tq, Tk, H, dk, self._inv_scale)
+            return _linear(self.out, att.reshape(B, Tq, self.d_model), residual=residual)
         if dk < 64:  # zero-pad every head to the kernels' 64 columns
             qp, kp, vp = (F.pad(t.reshape(t.shape[0], H, dk), (0, 64 - dk)).reshape(t.shape[0], H * 64)
                           for t in (qp, kp, vp))

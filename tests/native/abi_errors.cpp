@@ -140,6 +140,30 @@ int main() {
   BAD(rp_mha_bwd(RP_BF16, &ma, 8, nullptr), "phases");
   BAD(rp_mha_fwd(RP_BF16, &ma, nullptr), "null pointer");
 
+  // GEMM + LayerNorm seams, general attention core
+  rp_gemm_ln_args gl;
+  memset(&gl, 0, sizeof gl);
+  BAD(rp_gemm_ln_fwd(100, 512, &gl, nullptr), "multiple of 64");
+  BAD(rp_gemm_ln_fwd(128, 512, nullptr, nullptr), "null");
+  BAD(rp_gemm_ln_fwd(128, 512, &gl, nullptr), "null operand");
+  gl.A = P; gl.lda = 512; gl.W = P; gl.ldw = 512; gl.gamma = F; gl.mean = F; gl.rstd = F; gl.dropout_p = 2.f;
+  BAD(rp_gemm_ln_fwd(128, 512, &gl, nullptr), "dropout_p");
+  gl.dropout_p = 0.f;
+  BAD(rp_gemm_ln_fwd(128, 512, &gl, nullptr), "null operand");
+  BAD(rp_gemm_ln_bwd(128, 512, &gl, nullptr), "null x");
+  gl.x = F; gl.ldx = 512; gl.dx = F; gl.lddx = 512; gl.lp_dropout_p = -1.f;
+  BAD(rp_gemm_ln_bwd(128, 512, &gl, nullptr), "lp_dropout_p");
+  rp_mha_general_args mg;
+  memset(&mg, 0, sizeof mg);
+  BAD(rp_mha_general_fwd(nullptr, nullptr), "null");
+  BAD(rp_mha_general_fwd(&mg, nullptr), "bad shape");
+  mg.B = 1; mg.Tq = 4; mg.Tk = 4; mg.H = 2; mg.head_dim = 96; mg.q = mg.k = mg.v = F; mg.probs = F;
+  mg.ldq = mg.ldk = mg.ldv = 100;
+  BAD(rp_mha_general_fwd(&mg, nullptr), "leading dims");
+  mg.ldq = mg.ldk = mg.ldv = 192;
+  BAD(rp_mha_general_fwd(&mg, nullptr), "bad out");
+  BAD(rp_mha_general_bwd(&mg, nullptr), "dout");
+
   // losses / heads
   BAD(rp_focal_fwd_sum(F, F, nullptr, -1, 0.7f, 2.f, F, nullptr), nullptr);
   BAD(rp_focal_fwd_sum(nullptr, nullptr, nullptr, 4, 0.7f, 2.f, F, nullptr), "null");

@@ -143,14 +143,67 @@ def test_head_dims_below_64(dev, d_model, heads):
 
 @pytest.mark.gpu
 def test_per_query_masks(dev):
-    """[B, Tq, Tk] masks whose rows agree for every query run (the reference broadcasts any mask,
-    :69-71); masks that differ between queries are refused loudly."""
+    """[B, Tq, Tk] masks whose rows agree for every query (flash path), and masks that differ between
+    queries — random, with fully masked rows among them (the general core, -1e9 semantics)."""
     _mha_case(dev, D, H, [33, 20], mask_fn=lambda m, T: m.expand(m.shape[0], T, m.shape[2]).contiguous())
-    m = R.MultiHeadAttention(D, H).to(dev)
-    x = torch.randn(2, 8, D, device=dev)
-    bad = torch.ones(2, 8, 8, device=dev)
-    bad[0, 3, 5] = 0
-    with pytest.raises(NotImplementedError):
-        m(x, x, x, bad)
-    with pytest.raises(NotImplementedError):
-        R.MultiHeadAttention(256, 2)  # head dim 128
+    g = torch.Generator().manual_seed(17)
+
+    def varying(m, T):
+        r = (torch.rand(m.shape[0], T, m.shape[2], generator=g) > 0.4) & m
+        r[0, 5] = False  # a query with no valid key: uniform over all keys
+        return r
+
+    _mha_case(dev, D, H, [33, 20], mask_fn=varying)
+
+
+@pytest.mark.gpu
+def test_causal_self_attention(dev):
+    """A causal (lower-triangular) mask on self attention, as a user of the reference module would pass."""
+    torch.manual_seed(0)
+    ref = O.MultiHeadAttention(D, H)
+    torch.manual_seed(0)
+    ours = R.MultiHeadAttention(D, H).to(dev)
+    x = torch.randn(2, 37, D, generator=torch.Generator().manual_seed(1))
+    causal = torch.tril(torch.ones(37, 37, dtype=torch.bool)).expand(2, 37, 37)
+    xr, xo = x.clone().requires_grad_(True), x.to(dev).requires_grad_(True)
+    yr, yo = ref(xr, xr, xr, causal), ours(xo, xo, xo, causal.to(dev))
+    assert (yo.detach().cpu() - yr.detach()).abs().max().item() < 1e-3 * max(1.0, yr.abs().max().item())
+    w = torch.randn(yr.shape, generator=torch.Generator().manual_seed(2))
+    (yr * w).sum().backward()
+    (yo * w.to(dev)).sum().backward()
+    rel = (xo.grad.cpu() - xr.grad).abs().max().item() / xr.grad.abs().max().item()
+    assert rel < 2e-3, rel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d_model,heads", [(256, 2), (192, 2), (320, 4)])
+def test_head_dims_above_64(dev, d_model, heads):
+    """d_k = 128, 96 and 80 (the reference takes any, :42): the general core."""
+    _mha_case(dev, d_model, heads, [33, 20])
+
+
+@pytest.mark.gpu
+def test_batch_key_mask_broadcasts_like_the_reference(dev):
+    """A [B, Tk] mask: the reference's unsqueeze(1) makes it [B, 1, Tk], which broadcasts against the
+    scores [B, H, Tq, Tk] as [1, B, 1, Tk] — per HEAD when B == H, an error otherwise."""
+    torch.manual_seed(0)
+    ref = O.MultiHeadAttention(D, H)
+    torch.manual_seed(0)
+    ours = R.MultiHeadAttention(D, H).to(dev)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(H, 12, D, generator=g)  # B == H
+    m = torch.rand(H, 12, generator=g) > 0.3
+    yr = ref(x, x, x, m)
+    yo = ours(x.to(dev), x.to(dev), x.to(dev), m.to(dev))
+    assert (yo.detach().cpu() - yr.detach()).abs().max().item() < 1e-3 * max(1.0, yr.abs().max().item())
+    x3 = torch.randn(3, 12, D, generator=g)  # B = 3 is neither 1 nor H: the reference raises
+    m3 = torch.ones(3, 12, dtype=torch.bool)
+    with pytest.raises(RuntimeError):
+        ref(x3, x3, x3, m3)
+    with pytest.raises(RuntimeError):
+        ours(x3.to(dev), x3.to(dev), x3.to(dev), m3.to(dev))
+
+
+def test_indivisible_model_width_is_refused():
+    with pytest.raises(ValueError):
+        R.MultiHeadAttention(250, 4)
