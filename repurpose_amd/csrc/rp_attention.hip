@@ -1008,6 +1008,34 @@ __device__ __forceinline__ void dma16b(const rp_srd& srd, uint32_t voff, uint32_
       : "memory");
 }
 
+// A tile's four row pieces (two operands x two 1 KB pieces, each operand one descriptor and one scalar
+// offset) in one asm block: m0 saved / restored once around the group instead of per piece (the
+// per-piece form spent 5 scalar instructions per piece: ~30 % of the loop's SALU)
+__device__ __forceinline__ void dma16b_x4(const rp_srd& s0, uint32_t v00, uint32_t v01, uint32_t o0, const rp_srd& s1,
+                                          uint32_t v10, uint32_t v11, uint32_t o1, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %5, %9, %11 offen lds\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %6, %9, %11 offen lds\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %7, %10, %12 offen lds\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %8, %10, %12 offen lds\n\t"
+      "s_nop 0\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "s"(lds + 1024u), "s"(lds + 8192u), "s"(lds + 9216u), "v"(v00), "v"(v01), "v"(v10), "v"(v11),
+        "s"(s0), "s"(s1), "s"(o0), "s"(o1)
+      : "memory");
+}
+
 // rows [row0, row0 + 64) of a [rows][64] bf16 operand -> the swizzled 8 KB image (two 1 KB pieces per
 // wave, as dma_rows64), descriptor form for full tiles: piece j of wave w is
 // dma16b(srd, vo_j, row0 * rowbytes, image + (2w + j) * 1 KB)
@@ -1145,10 +1173,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
     if (xfast && qs0 + KV_QT <= Tq) {
       const uint32_t t = slot_lds[BI];
       const uint32_t pq = t + (uint32_t)(w * 2) * 1024u;
-      dma16b(rq.srd, rq.vo0, (uint32_t)qs0 * rq.rowbytes, pq);
-      dma16b(rq.srd, rq.vo1, (uint32_t)qs0 * rq.rowbytes, pq + 1024u);
-      dma16b(rdo.srd, rdo.vo0, (uint32_t)qs0 * rdo.rowbytes, pq + TILE);
-      dma16b(rdo.srd, rdo.vo1, (uint32_t)qs0 * rdo.rowbytes, pq + TILE + 1024u);
+      static_assert(TILE == 8192, "dma16b_x4 places the second operand 8 KB on");
+      dma16b_x4(rq.srd, rq.vo0, rq.vo1, (uint32_t)qs0 * rq.rowbytes, rdo.srd, rdo.vo0, rdo.vo1,
+                (uint32_t)qs0 * rdo.rowbytes, pq);
       dma16b(srd_x, vo_x, (uint32_t)qs0 * bpr_x, t + xo);
     } else {  // partial tile: clamped rows, -inf S start past Tq
       dma_rows64(Qg, ldq, qs0, Tq, buf, w, lane);
@@ -1768,10 +1795,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
     if (xfast && k0 + FW_KT <= Tk) {
       const uint32_t t = slot_lds[BI];
       const uint32_t pk = t + (uint32_t)(w * 2) * 1024u;
-      dma16b(rk.srd, rk.vo0, (uint32_t)k0 * rk.rowbytes, pk);
-      dma16b(rk.srd, rk.vo1, (uint32_t)k0 * rk.rowbytes, pk + 1024u);
-      dma16b(rv.srd, rv.vo0, (uint32_t)k0 * rv.rowbytes, pk + TILE);
-      dma16b(rv.srd, rv.vo1, (uint32_t)k0 * rv.rowbytes, pk + TILE + 1024u);
+      static_assert(TILE == 8192, "dma16b_x4 places the second operand 8 KB on");
+      dma16b_x4(rk.srd, rk.vo0, rk.vo1, (uint32_t)k0 * rk.rowbytes, rv.srd, rv.vo0, rv.vo1,
+                (uint32_t)k0 * rv.rowbytes, pk);
       if (DROP && w == 1) dma16b(srd_m, vo_m, (uint32_t)it * 8u * (uint32_t)ldm, t + 2 * TILE);
     } else {
       dma_rows64(Kg, ldk, k0, Tk, buf, w, lane);
@@ -2008,10 +2034,9 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
     const int k0 = it * FW_KT;
     if (xfast && k0 + FW_KT <= Tk) {
       const uint32_t pk = slot_lds[BI] + (uint32_t)(w * 2) * 1024u;
-      dma16b(rk.srd, rk.vo0, (uint32_t)k0 * rk.rowbytes, pk);
-      dma16b(rk.srd, rk.vo1, (uint32_t)k0 * rk.rowbytes, pk + 1024u);
-      dma16b(rv.srd, rv.vo0, (uint32_t)k0 * rv.rowbytes, pk + TILE);
-      dma16b(rv.srd, rv.vo1, (uint32_t)k0 * rv.rowbytes, pk + TILE + 1024u);
+      static_assert(TILE == 8192, "dma16b_x4 places the second operand 8 KB on");
+      dma16b_x4(rk.srd, rk.vo0, rk.vo1, (uint32_t)k0 * rk.rowbytes, rv.srd, rv.vo0, rv.vo1,
+                (uint32_t)k0 * rv.rowbytes, pk);
     } else {
       char* buf = ring(bi);
       dma_rows64(Kg, ldk, k0, Tk, buf, w, lane);
@@ -2222,6 +2247,16 @@ static bool attn_pipe_enabled() {
   return v != 0;
 }
 
+static size_t attn_fwd_pad() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_ATTN_FWD_LDS_PAD");
+    v = e ? atol(e) : 0;
+    if (v < 0 || v > 65536) v = 0;
+  }
+  return (size_t)v;
+}
+
 // RP_ATTN_DMA_F=0 selects the register-staged forward kernel (A/B tuning)
 static bool attn_dma_f_enabled() {
   static int v = -1;
@@ -2246,10 +2281,13 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
     else
       hipLaunchKernelGGL((attn_fwd_kernel<T, false, 1>), grid, dim3(NT), 0, s, a);
   } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX && attn_dma_f_enabled()) {
+    // RP_ATTN_FWD_LDS_PAD (bytes of unused dynamic LDS): tuning knob for the workgroups per CU
+    // (53.8 KB static -> three per CU, a fourth of the metric grid then runs as a one-per-CU tail)
+    const size_t pad = attn_fwd_pad();
     if (a.drop_thresh)
-      hipLaunchKernelGGL((attn_fwd_dma_kernel<true>), grid, dim3(NT), 0, s, a);
+      hipLaunchKernelGGL((attn_fwd_dma_kernel<true>), grid, dim3(NT), pad, s, a);
     else
-      hipLaunchKernelGGL((attn_fwd_dma_kernel<false>), grid, dim3(NT), 0, s, a);
+      hipLaunchKernelGGL((attn_fwd_dma_kernel<false>), grid, dim3(NT), pad, s, a);
   } else {
     if (a.drop_thresh)
       hipLaunchKernelGGL((attn_fwd_kernel<T, true, 2>), grid, dim3(NT), 0, s, a);
