@@ -596,8 +596,17 @@ __global__ void attn_delta_kernel(MhaDev a) {
   const T* d = (const T*)a.dout + row * a.lddo;
   for (int e = lane * 8; e < D; e += 512) {
     float s = 0.f;
+    if constexpr (std::is_same<T, bf16>::value) {  // one 16-byte load per operand (ld % 8 == 0)
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(o + e);
+      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(d + e);
+      bf16x8 lv;
+      if (ol) lv = *reinterpret_cast<const bf16x8*>(ol + e);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += (rp_ld(o + e + j) + (ol ? rp_ld(ol + e + j) : 0.f)) * rp_ld(d + e + j);
+      for (int j = 0; j < 8; ++j) s += ((float)ov[j] + (ol ? (float)lv[j] : 0.f)) * (float)dv[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += (rp_ld(o + e + j) + (ol ? rp_ld(ol + e + j) : 0.f)) * rp_ld(d + e + j);
+    }
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);

@@ -37,9 +37,10 @@ def test_backward_fp32_parity_L16(dev):
     in float32 included) lands up to 1.5e-2 (max-abs) / 1.5e-3 (norm) from it on single tensors (ReLU
     gates of linear1 flip on pre-activations within fp32 rounding of zero), so a fixed per-tensor
     max-abs gate against the fp32 oracle measures rounding, not the kernels.  Gates: the GPU fp32
-    gradient of the whole model within 4x the fp32 reference's own norm distance to fp64 (floor 2e-4);
-    per tensor a coarse bound (norm 5e-3, max-abs 2.5e-2) that single flips stay inside and a broken
-    kernel or layer (O(1) off) does not."""
+    gradient of the whole model within 1e-3 (or 4x the fp32 reference's own distance) in norm, the
+    median tensor within 2e-4 (a systematic error moves every tensor; a flip moves one or two), and per
+    tensor a coarse bound (norm 5e-3, max-abs 2.5e-2) that single flips stay inside and a broken kernel
+    or layer (O(1) off) does not."""
     torch.manual_seed(3)
     ref = Oracle(**L16).eval()  # dropout off; autograd runs the training path of the encoder layers
     torch.manual_seed(3)
@@ -84,9 +85,14 @@ def test_backward_fp32_parity_L16(dev):
     gr = torch.cat([g32[n].flatten() for n, q in ref64.named_parameters() if q.grad is not None])
     e_flat = ((gm - gx).norm() / gx.norm()).item()
     r_flat = ((gr - gx).norm() / gx.norm()).item()
-    print(f"L=16 fp32 vs fp64: flat norm error {e_flat:.2e} (fp32 reference {r_flat:.2e}); worst tensor "
-          f"{max(rows, key=lambda r: r[3])[0]} norm {max(r[3] for r in rows):.2e}")
-    assert e_flat <= max(2e-4, 4 * r_flat), (e_flat, r_flat)
+    med = sorted(r[3] for r in rows)[len(rows) // 2]
+    r_med = sorted(r[4] for r in rows)[len(rows) // 2]
+    print(f"L=16 fp32 vs fp64: flat norm error {e_flat:.2e} (fp32 reference {r_flat:.2e}); median tensor "
+          f"{med:.2e} (reference {r_med:.2e}); worst tensor {max(rows, key=lambda r: r[3])[0]} norm "
+          f"{max(r[3] for r in rows):.2e}")
+    # one flipped gate moved the flat norm to 3.2e-4 on one box (layer 8 linear1.weight 1.5e-3)
+    assert e_flat <= max(1e-3, 4 * r_flat), (e_flat, r_flat)
+    assert med <= 2e-4, (med, r_med)
     assert n_checked == 16 * 12 + 18  # every encoder tensor + input projection/norm, encoder norm, feature map, cls head
 
 
