@@ -3,9 +3,9 @@
 
 * fp32 (parity mode): every trainable gradient of the L = 16 tri-modal model against torch autograd
   through the CPU oracle in float64 (stock nn.TransformerEncoderLayer modules, the reference's
-  construction order), ragged lengths, dropout off: the whole gradient no farther from the fp64
-  gradient (norm) than 4x the reference's own fp32 arithmetic (the oracle in float32), and every tensor
-  within a coarse bound that single ReLU-gate flips stay inside;
+  construction order), ragged lengths, dropout off.  With every ReLU's on/off pattern pinned to the GPU
+  forward's, each tensor within 5x the oracle-in-fp32's own distance to fp64; unpinned, a coarse bound
+  per tensor that single ReLU switches (pre-activations within rounding of zero) stay inside;
 * bf16 (bench mode) with the deferred grouped weight gradients active — the single 16-layer
   rp_gemm_wgrad_grouped launch the bench runs — against the fp32 GPU gradients of the same model on
   the same batch: per tensor ||g_bf16 - g_fp32||_2 <= 0.10 ||g_fp32||_2 (bf16 operands carry 2^-9
@@ -13,6 +13,8 @@
 * the L = 16 bf16-vs-fp32 training trajectory (the round-2 40-step script, shortened): 10 FusedAdam
   steps at T = 512, dropout off, losses within 2 % per step and 0.6 % on average.
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -32,68 +34,88 @@ def _grads(m):
     return {n: p.grad.detach().double().cpu() for n, p in m.named_parameters() if p.grad is not None}
 
 
+class _Gate(torch.nn.Module):
+    """A ReLU whose on/off pattern is given (the GPU forward's): z * gate, gradient gate."""
+
+    def __init__(self, gate):
+        super().__init__()
+        self.gate = gate
+
+    def forward(self, z):
+        return z * self.gate.to(z.dtype)
+
+
+def _pin_relus(oracle, gates, B, T):
+    """Every ReLU of the oracle's trained path follows the GPU forward's decisions."""
+    for l, layer in enumerate(oracle.multimodal_encoder.layers):
+        layer.activation = _Gate(gates["layers"][l].view(B, T, -1))
+    oracle.feature_map[2] = _Gate(gates["feats"].view(B, T, -1))
+    oracle.cls_head[2] = _Gate(gates["c1"].view(B, T, -1))
+    oracle.cls_head[5] = _Gate(gates["c2"].view(B, T, -1))
+
+
+def _grads_of(oracle, b, dtype):
+    o = copy.deepcopy(oracle).to(dtype)
+    o.zero_grad()
+    bb = {k: (v.to(dtype) if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in b.items()}
+    o.losses(*o(bb))["cls_loss"].backward()
+    return {n: q.grad.detach().double().clone() for n, q in o.named_parameters() if q.grad is not None}
+
+
 def test_backward_fp32_parity_L16(dev):
-    """The exact gradient is the oracle in float64.  At 16 layers fp32 arithmetic itself (the CPU oracle
-    in float32 included) lands up to 1.5e-2 (max-abs) / 1.5e-3 (norm) from it on single tensors (ReLU
-    gates of linear1 flip on pre-activations within fp32 rounding of zero), so a fixed per-tensor
-    max-abs gate against the fp32 oracle measures rounding, not the kernels.  Gates: the GPU fp32
-    gradient of the whole model within 1e-3 (or 4x the fp32 reference's own distance) in norm, the
-    median tensor within 2e-4 (a systematic error moves every tensor; a flip moves one or two), and per
-    tensor a coarse bound (norm 5e-3, max-abs 2.5e-2) that single flips stay inside and a broken kernel
-    or layer (O(1) off) does not."""
+    """fp32 gradients at the shipped depth against the exact (fp64) gradient.
+
+    A ReLU whose pre-activation lies within rounding of zero switches between fp32 implementations, and
+    one switched unit of a linear1 moves that layer's weight gradient by ~1e-3 and every layer below it
+    by ~1e-4 (measured: the GPU fp32 path and this container's CPU fp32 oracle each carry one or two such
+    switches at L = 16, on different layers).  So the tight gate runs with the gates pinned: the fp64
+    oracle (and the CPU fp32 oracle, for the rounding scale) take every ReLU's on/off pattern from the
+    GPU forward, and the GPU gradient must then be as close to fp64 as fp32 arithmetic is — per tensor
+    within 5x the CPU fp32 oracle's distance (floor 2e-6), flat within 4x (measured: flat 5.0e-7 vs the
+    CPU's 2.4e-7, worst tensor 2.7x).  Unpinned, every tensor stays
+    within a coarse bound (norm 5e-3, max-abs 2.5e-2) that switches stay inside and a broken kernel or
+    layer (O(1) off) does not."""
     torch.manual_seed(3)
     ref = Oracle(**L16).eval()  # dropout off; autograd runs the training path of the encoder layers
     torch.manual_seed(3)
     m = MMCTransformer(**L16, compute_dtype="fp32").to(dev).train()
     m.DROPOUT = 0.0
-    b = make_batch(L16, 2, 256, [256, 173], seed=8)
-    lr = ref.losses(*ref(b))["cls_loss"]
-    lr.backward()
-    g32 = {n: q.grad.detach().double().clone() for n, q in ref.named_parameters() if q.grad is not None}
-    ref64 = ref.double()
-    ref64.zero_grad()
-    b64 = {k: (v.double() if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in b.items()}
-    l64 = ref64.losses(*ref64(b64))["cls_loss"]
-    l64.backward()
-    lm = m.losses(*m(to_dev(b, dev)))["cls_loss"]
+    B, T = 2, 256
+    b = make_batch(L16, B, T, [256, 173], seed=8)
+    out = m(to_dev(b, dev))
+    S = out[1].grad_fn.run.saved  # the engine's saved forward activations (post-ReLU outputs)
+    gates = {"layers": [(lay[13] > 0).cpu() for lay in S["layers"]], "feats": (S["feats"] > 0).cpu(),
+             "c1": (S["c1"] > 0).cpu(), "c2": (S["c2"] > 0).cpu()}
+    lm = m.losses(*out)["cls_loss"]
     lm.backward()
     torch.cuda.synchronize()
-    assert abs(lm.item() - l64.item()) < 1e-3 * max(1.0, abs(l64.item()))
+    g64 = _grads_of(ref, b, torch.float64)
+    _pin_relus(ref, gates, B, T)
+    p64 = _grads_of(ref, b, torch.float64)
+    p32 = _grads_of(ref, b, torch.float32)
     rows = []
-    for (n, p), (n2, q) in zip(m.named_parameters(), ref64.named_parameters()):
-        assert n == n2
+    for n, p in m.named_parameters():
         if n.startswith("reg_head."):
-            assert p.grad is None and q.grad is None
+            assert p.grad is None and n not in g64
             continue
-        g, gx, gr = p.grad.cpu().double(), q.grad.double(), g32[n]
-        rows.append((n, (g - gx).abs().max().item() / (gx.abs().max().item() + 1e-30),
-                     (gr - gx).abs().max().item() / (gx.abs().max().item() + 1e-30),
-                     (g - gx).norm().item() / (gx.norm().item() + 1e-30),
-                     (gr - gx).norm().item() / (gx.norm().item() + 1e-30)))
-    # A ReLU gate of linear1 whose pre-activation lies within rounding of zero flips between fp32
-    # implementations and moves single gradient elements: measured on layer 8's linear1.weight, max-abs
-    # 1.5e-2 / norm 1.5e-3 from fp64 for this container's CPU fp32 AND for the GPU fp32 path, 2.8e-5 for
-    # the GPU box's CPU fp32 (another BLAS build).  So per tensor only a coarse bound (a broken kernel or
-    # layer is off by O(1)), and the tight gate on the whole gradient, where a flip is diluted.
-    n_checked = 0
-    for n, e_max, r_max, e_nrm, r_nrm in rows:
-        n_checked += 1
-        assert e_max <= 2.5e-2, f"{n}: max-abs rel {e_max:.2e} (fp32 reference {r_max:.2e})"
-        assert e_nrm <= 5e-3, f"{n}: norm rel {e_nrm:.2e} (fp32 reference {r_nrm:.2e})"
-    gm = torch.cat([p.grad.cpu().double().flatten() for n, p in m.named_parameters() if p.grad is not None])
-    gx = torch.cat([q.grad.double().flatten() for n, q in ref64.named_parameters() if q.grad is not None])
-    gr = torch.cat([g32[n].flatten() for n, q in ref64.named_parameters() if q.grad is not None])
-    e_flat = ((gm - gx).norm() / gx.norm()).item()
-    r_flat = ((gr - gx).norm() / gx.norm()).item()
-    med = sorted(r[3] for r in rows)[len(rows) // 2]
-    r_med = sorted(r[4] for r in rows)[len(rows) // 2]
-    print(f"L=16 fp32 vs fp64: flat norm error {e_flat:.2e} (fp32 reference {r_flat:.2e}); median tensor "
-          f"{med:.2e} (reference {r_med:.2e}); worst tensor {max(rows, key=lambda r: r[3])[0]} norm "
-          f"{max(r[3] for r in rows):.2e}")
-    # one flipped gate moved the flat norm to 3.2e-4 on one box (layer 8 linear1.weight 1.5e-3)
-    assert e_flat <= max(1e-3, 4 * r_flat), (e_flat, r_flat)
-    assert med <= 2e-4, (med, r_med)
-    assert n_checked == 16 * 12 + 18  # every encoder tensor + input projection/norm, encoder norm, feature map, cls head
+        g = p.grad.cpu().double()
+        nrm = lambda a, x: ((a - x).norm() / (x.norm() + 1e-30)).item()  # noqa: E731
+        rows.append((n, (g - g64[n]).abs().max().item() / (g64[n].abs().max().item() + 1e-30), nrm(g, g64[n]),
+                     nrm(g, p64[n]), nrm(p32[n], p64[n])))
+    assert len(rows) == 16 * 12 + 18  # every encoder tensor + input projection/norm, encoder norm, feature map, cls head
+    for n, e_max, e_nrm, pe, pr in rows:  # unpinned: coarse
+        assert e_max <= 2.5e-2, f"{n}: max-abs rel {e_max:.2e} (unpinned)"
+        assert e_nrm <= 5e-3, f"{n}: norm rel {e_nrm:.2e} (unpinned)"
+    flat = lambda gd: torch.cat([gd[n].flatten() for n, *_ in rows])  # noqa: E731
+    gm = torch.cat([dict(m.named_parameters())[n].grad.cpu().double().flatten() for n, *_ in rows])
+    e_flat = ((gm - flat(p64)).norm() / flat(p64).norm()).item()
+    r_flat = ((flat(p32) - flat(p64)).norm() / flat(p64).norm()).item()
+    worst = max(rows, key=lambda r: r[3] / max(2e-6, 5 * r[4]))
+    print(f"L=16 fp32, gates pinned: flat {e_flat:.2e} (CPU fp32 {r_flat:.2e}); worst tensor {worst[0]} "
+          f"{worst[3]:.2e} (CPU fp32 {worst[4]:.2e}); unpinned worst {max(r[2] for r in rows):.2e}")
+    for n, e_max, e_nrm, pe, pr in rows:
+        assert pe <= max(2e-6, 5 * pr), f"{n}: pinned norm rel {pe:.2e} (CPU fp32 {pr:.2e})"
+    assert e_flat <= 4 * r_flat, (e_flat, r_flat)
 
 
 def test_bf16_grouped_gradients_track_fp32_L16(dev, monkeypatch):
