@@ -2215,6 +2215,9 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
   }
 }
 
+// 128-row blocks (the LDS-DMA kernels) from this many workgroups up; 64-row blocks below
+constexpr int64_t ATTN_SMALL_GRID = 256;
+
 // RP_ATTN_BLOCK=64 | 128 forces the workgroup block (queries for fwd / dQ, keys for dK/dV), for tuning
 static int attn_block_override() {
   static int v = -1;
@@ -2278,9 +2281,11 @@ static bool attn_dma_f_enabled() {
 
 template <typename T>
 int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
-  // 128-query blocks unless that leaves fewer than two workgroups per CU (256 CUs): then 64
+  // 128-query blocks unless that leaves fewer than one workgroup per CU (256 CUs): then 64.  At one
+  // per CU the 128-row LDS-DMA kernel still beats the 64-row register-staged one at twice the
+  // workgroups (config 4, B = 1, T = 4096: 85 vs 96 us; dQ 78 vs 101; step 9.59 -> 9.06 ms)
   const int64_t big = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H;
-  const bool small = attn_block_override() ? attn_block_override() == 64 : big < 512;
+  const bool small = attn_block_override() ? attn_block_override() == 64 : big < ATTN_SMALL_GRID;
   const int qb = small ? NW * 16 : FW_QB;
   const int nqb = (a.Tq + qb - 1) / qb;
   const dim3 grid((unsigned)(nqb * a.B * a.H));
@@ -2328,9 +2333,9 @@ template <typename T>
 int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   const int64_t rows = (int64_t)a.B * a.Tq;
   const int nkb = (a.Tk + KV_KB - 1) / KV_KB;
-  // dQ: 128-query blocks unless that leaves fewer than two workgroups per CU (then 64, as the forward)
+  // dQ: 128-query blocks unless that leaves fewer than one workgroup per CU (then 64, as the forward)
   const bool small = attn_block_override() ? attn_block_override() == 64
-                                           : (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H < 512;
+                                           : (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H < ATTN_SMALL_GRID;
   const bool fused = (phases & 5) == 5;
   if (fused) {
     if (small) {
@@ -2349,8 +2354,9 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
   }
   if (phases & 2) {
-    // 128-key blocks unless that leaves fewer than two workgroups per CU: then 64
-    const bool small_kv = attn_block_override() ? attn_block_override() == 64 : (int64_t)nkb * a.B * a.H < 512;
+    // 128-key blocks unless that leaves fewer than one workgroup per CU: then 64
+    const bool small_kv =
+        attn_block_override() ? attn_block_override() == 64 : (int64_t)nkb * a.B * a.H < ATTN_SMALL_GRID;
     const dim3 grid(small_kv ? (unsigned)((a.Tk + NW * 16 - 1) / (NW * 16) * a.B * a.H) : (unsigned)(nkb * a.B * a.H));
     // bf16 with the producer's Q prescale: the LDS-DMA staged kernel (RP_ATTN_DMA=0: register staged)
     if (std::is_same<T, bf16>::value && a.qpre && !a.empty_uniform && attn_dma_enabled()) {

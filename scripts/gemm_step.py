@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--warm", action="store_true", help="no cache flush between launches")
     ap.add_argument("--only", default="")
+    ap.add_argument("--ablate", action="store_true", help="epilogue ablation of the main shapes")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     M, d, dff = 16384, 512, 2048
@@ -77,6 +78,23 @@ def main():
             dqkv, Wqkv, x, mu, rs, gm, dres=x1, lp_dtype=bf, lp_dropout_p=p, lp_seed=5, dgamma=flat[:d],
             dbeta=flat[d:]), M * d * 3 * d, M * 3 * d * E + 3 * d * d * E + 3 * M * d * F + M * d * E),
     ]
+    if a.ablate:  # the epilogue's share: the same shapes with fewer epilogue stages
+        cases = [
+            ("linear1 fwd plain", lambda: K.linear_fwd(h2, W1, b1), M * dff * d, M * d * E + dff * d * E + M * dff * E),
+            ("linear1 fwd relu", lambda: K.linear_fwd(h2, W1, b1, relu=True), M * dff * d,
+             M * d * E + dff * d * E + M * dff * E),
+            ("linear1 fwd relu+drop", lambda: K.linear_fwd(h2, W1, b1, relu=True, dropout_p=p, seed=2), M * dff * d,
+             M * d * E + dff * d * E + M * dff * E),
+            ("qkv fwd plain", lambda: K.linear_fwd(h1, Wqkv, bqkv), M * 3 * d * d, M * d * E + 3 * d * d * E + M * 3 * d * E),
+            ("linear2 fwd f32 plain", lambda: K.linear_fwd(f, W2, b2, out_dtype=f32), M * d * dff,
+             M * dff * E + d * dff * E + M * d * 4),
+            ("linear2 fwd f32 +res", lambda: K.linear_fwd(f, W2, b2, out_dtype=f32, residual=x1), M * d * dff,
+             M * dff * E + d * dff * E + 2 * M * d * 4),
+            ("linear2 fwd f32 +res+drop", lambda: K.linear_fwd(f, W2, b2, out_dtype=f32, dropout_p=p, seed=3,
+                                                               residual=x1), M * d * dff,
+             M * dff * E + d * dff * E + 2 * M * d * 4),
+            ("linear2 fwd bf16 plain", lambda: K.linear_fwd(f, W2, b2), M * d * dff, M * dff * E + d * dff * E + M * d * E),
+        ]
     flush = torch.empty(640 << 20, dtype=torch.uint8, device=dev)
     tot = 0.0
     for name, fn, fl, by in cases:
