@@ -48,15 +48,18 @@ struct AttnCfg {
   static constexpr int CPR = HD * (int)sizeof(T) / 16;  // 16-byte chunks per row
 };
 
-// Byte offset of (row, byte-in-row) in an LDS tile.  bf16: the 32-byte pair of 16-byte chunks is
-// XORed with (row >> 1) & 3, which makes both access patterns conflict-free: ds_read_b128 row
-// fragments (16 lanes = 16 rows x 2 adjacent chunks cover all 16 bank quads) and
-// ds_read_b64_tr_b16 column fragments (8 consecutive rows x one 32-byte pair cover all 8 bank
-// octets).  The pair index (bits 5-6) changes, the chunk parity (bit 4) and byte (bits 0-3) stay.
+// Byte offset of (row, byte-in-row) in an LDS tile.  bf16: the 16-byte chunk index is XORed with
+// lds_swz(row) = ((row >> 1) & 3) << 1 | ((row >> 3) & 1).  The pair bits ((row >> 1) & 3 on the
+// 32-byte pair index) make the 16x16x32 reads conflict-free: ds_read_b128 row fragments (16 lanes =
+// 16 rows x 2 adjacent chunks cover all 16 bank quads) and ds_read_b64_tr_b16 column fragments (4
+// consecutive rows x one 32-byte pair per 16-lane group); the chunk-parity bit (row >> 3) & 1 adds
+// the 32x32x16 row fragment (32 rows at one chunk: without it only 8 of the 16 bank quads, 4-way)
+// and leaves a 4-row block's parity constant, so the transposed reads stay conflict-free.
+__device__ __forceinline__ int lds_swz(int row) { return (((row >> 1) & 3) << 1) | ((row >> 3) & 1); }
 template <typename T>
 __device__ __forceinline__ int lds_off(int row, int byte) {
   if constexpr (std::is_same<T, bf16>::value)
-    return row * 128 + (byte ^ (((row >> 1) & 3) << 5));
+    return row * 128 + (byte ^ (lds_swz(row) << 4));
   else
     return row * AttnCfg<T>::ROWB + byte;
 }
@@ -970,7 +973,7 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
 
 // rows [row0, row0 + 64) of a [rows][64] bf16 operand (row stride ld) -> the swizzled 8 KB image of
 // lds_off<bf16>: eight 1 KB pieces (8 rows each), two per wave; lane l of a piece lands at physical
-// 16-byte chunk l & 7 of row l >> 3, which holds logical chunk (l & 7) ^ (((row >> 1) & 3) << 1)
+// 16-byte chunk l & 7 of row l >> 3, which holds logical chunk (l & 7) ^ lds_swz(row)
 __device__ __forceinline__ void dma_rows64(const bf16* __restrict__ base, int64_t ld, int row0, int nrows, char* tile,
                                            int w, int lane) {
   const uint32_t t = lds_addr(tile);
@@ -978,7 +981,7 @@ __device__ __forceinline__ void dma_rows64(const bf16* __restrict__ base, int64_
   for (int j = 0; j < 2; ++j) {
     const int I = w * 2 + j;
     const int r = I * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (((r >> 1) & 3) << 1);
+    const int c = (lane & 7) ^ lds_swz(r);
     int rr = row0 + r;
     rr = rr < nrows ? rr : nrows - 1;
     dma16(base + (int64_t)rr * ld + c * 8, t + I * 1024);
@@ -1059,7 +1062,7 @@ struct Rows64 {
     ld = ld_;
     srd = make_srd(b);
     const int r0 = (w * 2) * 8 + (lane >> 3), r1 = r0 + 8;
-    const int c0 = (lane & 7) ^ (((r0 >> 1) & 3) << 1), c1 = (lane & 7) ^ (((r1 >> 1) & 3) << 1);
+    const int c0 = (lane & 7) ^ lds_swz(r0), c1 = (lane & 7) ^ lds_swz(r1);
     vo0 = (uint32_t)((r0 * ld_ + c0 * 8) * 2);
     vo1 = (uint32_t)((r1 * ld_ + c1 * 8) * 2);
     rowbytes = (uint32_t)(ld_ * 2);
@@ -1342,6 +1345,290 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
         rp_st(dV + (int64_t)key * a.lddv + dt * 16 + i, ok ? dv[kt][dt][r] : 0.f);
       }
     }
+}
+
+// =================================================================================================
+// backward: dK, dV on 32x32x16 MFMAs (bf16, LDS-DMA) — same data flow, ring and DMA pieces as
+// attn_bwd_kv_dma_kernel<DROP, 2, true>, with each wave's 32 keys as ONE 32-wide MFMA column block:
+// a v_mfma_f32_32x32x16_bf16 holds the SIMD's vector issue for 8 of its 32 cycles where two
+// 16x16x32 ones (the same FLOPs) hold it for 16 of 32 — the kernel is issue-bound (SQ counters,
+// profiles/r03_attn_sq_counters.txt), so that is 256 issue cycles per wave and 64-query tile back.
+//   S  [32 q][32 keys] = Q' K^T   : A = Q rows (32x32x16 row fragments from the LDS image),
+//                                   B = K rows in registers (lane = key), 4 k-steps over dk = 64
+//   lane l (key kw0 + (l & 31), h = l >> 5) holds S rows (reg & 3) + 8 (reg >> 2) + 4h, reg 0..15:
+//   the row constants (-lse, -delta/ds) start the accumulators as four f32x4 LDS reads, and P / dS
+//   packed pairwise to bf16 (registers 8s .. 8s+7 -> k-step s) are the A operands of
+//   dV[key][d] += P^T dO, dK[key][d] += dS^T Q' with dO / Q' as transposed (tr16) column fragments
+//   whose k order matches: element j of lane half h = query 16s + 8 (j >> 2) + 4h + (j & 3).
+// =================================================================================================
+// 32x32x16 operand fragments: lane l (r = l & 31, h = l >> 5) holds X[r0 + r][k0 + 8h .. + 7]
+__device__ __forceinline__ bf16x8 row_frag32_lds(const char* lds, int r0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(lds + lds_off<bf16>(r0 + (lane & 31), (k0 + 8 * (lane >> 5)) * 2));
+}
+__device__ __forceinline__ bf16x8 row_frag32_gmem(const bf16* base, int64_t ld, int r0, int nrows, int k0, int lane) {
+  const int r = r0 + (lane & 31);
+  if (r >= nrows) {
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
+    return z;
+  }
+  return *reinterpret_cast<const bf16x8*>(base + (int64_t)r * ld + k0 + 8 * (lane >> 5));
+}
+// column fragment (B operand over a row index): lane l (c = l & 31, h = l >> 5) receives
+// X[R + 4h + {0..3}][c0 + c] and X[R + 8 + 4h + {0..3}][c0 + c] through two ds_read_b64_tr_b16:
+// 16-lane group G reads the 4-row block R + 4 (G >> 1) (+ 8), columns c0 + 16 (G & 1) .. + 15
+__device__ __forceinline__ bf16x8 col_frag32_lds(const char* lds, int R, int c0, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = R + 4 * (G >> 1) + q, col = c0 + 16 * (G & 1) + 4 * p;
+  const char* p0 = lds + lds_off<bf16>(row, col * 2);
+  const char* p1 = lds + lds_off<bf16>(row + 8, col * 2);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_kv32_kernel(MhaDev a) {
+  constexpr int KB = NW * 32;  // keys per workgroup (one 32-key MFMA block per wave)
+  using C = AttnCfg<bf16>;
+  constexpr int TILE = KV_QT * C::ROWB;
+  constexpr int XR = 1024;
+  constexpr int BUF = 2 * TILE + 4 * XR;  // Q, dO images, lse row, delta row, keep bits, scratch
+  constexpr int NBUF = 3;
+  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const uint8_t* __restrict__ kvalid = a.kvalid;
+  const uint16_t* __restrict__ dmask = a.dmask;
+  const int nkb = (Tk + KB - 1) / KB;
+  const int L = rp_xcd_remap(blockIdx.x, nkb * B * H);
+  const int bh = L / nkb, kb = L % nkb;
+  const int b = bh / H, hh = bh % H;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
+  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + hh * HD;
+  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + hh * HD;
+  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + hh * HD;
+  const bf16* dOg = (const bf16*)a.dout + (int64_t)b * Tq * lddo + hh * HD;
+  const int64_t plane = (int64_t)B * H * Tq;
+  const float* nls_bh = a.delta + 2 * plane + (int64_t)bh * Tq;
+  const float* ndl_bh = a.delta + plane + (int64_t)bh * Tq;
+  const int kw0 = kb * KB + w * 32;
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
+
+  // K, V as B operands of S and dP: lane holds X[kw0 + (l & 31)][16 ks + 8h .. + 7]
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    kf[ks] = row_frag32_gmem(Kg, ldk, kw0, Tk, ks * 16, lane);
+    vf[ks] = row_frag32_gmem(Vg, ldv, kw0, Tk, ks * 16, lane);
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(kf[ks]), "v"(vf[ks]));
+
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[dt][r] = dv[dt][r] = 0.f;
+
+  auto ring = [&](auto bi) -> char* {
+    constexpr int BI = decltype(bi)::value;
+    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
+  };
+  // LDS-DMA of query tile it: exactly attn_bwd_kv_dma_kernel's five pieces per wave
+  Rows64 rq, rdo;
+  rq.init(Qg, ldq, Tq, w, lane);
+  rdo.init(dOg, lddo, Tq, w, lane);
+  const bool xmask = DROP && w == 3;
+  const uint16_t* mslab = DROP ? dmask + (int64_t)bh * KT * 4 * ldm : dmask;
+  const rp_srd srd_x = make_srd(xmask ? (const void*)mslab : (const void*)(w == 1 ? nls_bh : ndl_bh));
+  uint32_t vo_x = (uint32_t)(lane & 15) * 16u;
+  const uint32_t bpr_x = xmask ? 2u : 4u;
+  const uint32_t xo = (uint32_t)(2 * TILE + XR * (w == 1 ? 0 : (w == 2 ? 1 : (xmask ? 2 : 3))));
+  if (xmask) {
+    const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
+    int tile = kb * (KB / 64) + (r >> 2);
+    tile = tile < KT ? tile : KT - 1;
+    vo_x = (uint32_t)((((int64_t)tile * 4 + (r & 3)) * ldm + cch * 8) * 2);
+  }
+  const bool xfast = (int64_t)KT * 4 * ldm * 2 < ((int64_t)1 << 31) && rq.fast && rdo.fast;
+  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
+  auto issue = [&](int it, auto bi) {
+    constexpr int BI = decltype(bi)::value;
+    char* buf = ring(bi);
+    const int qs0 = it * KV_QT;
+    if (xfast && qs0 + KV_QT <= Tq) {
+      const uint32_t t = slot_lds[BI];
+      const uint32_t pq = t + (uint32_t)(w * 2) * 1024u;
+      static_assert(TILE == 8192, "dma16b_x4 places the second operand 8 KB on");
+      dma16b_x4(rq.srd, rq.vo0, rq.vo1, (uint32_t)qs0 * rq.rowbytes, rdo.srd, rdo.vo0, rdo.vo1,
+                (uint32_t)qs0 * rdo.rowbytes, pq);
+      dma16b(srd_x, vo_x, (uint32_t)qs0 * bpr_x, t + xo);
+    } else {
+      dma_rows64(Qg, ldq, qs0, Tq, buf, w, lane);
+      dma_rows64(dOg, lddo, qs0, Tq, buf + TILE, w, lane);
+      const int q = qs0 + lane;
+      if (xmask) {
+        const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
+        int tile = kb * (KB / 64) + (r >> 2);
+        tile = tile < KT ? tile : KT - 1;
+        dma16(dmask + (((int64_t)bh * KT + tile) * 4 + (r & 3)) * ldm + qs0 + cch * 8, lds_addr(buf + xo));
+      } else if (w == 1) {
+        dma4(q < Tq ? nls_bh + q : kPadStart, lds_addr(buf + xo));
+      } else {
+        dma4(ndl_bh + (q < Tq ? q : Tq - 1), lds_addr(buf + xo));
+      }
+    }
+  };
+  auto wait_tile = [&](bool next) {
+    if (!next)
+      wait_vm<0>();
+    else
+      wait_vm<5>();
+  };
+  // this lane's key: keep-bit word row and bit (layout of include/rp_api.h / mask_ld)
+  const int kwl = w * 32 + (lane & 31);
+  const int ko = kwl & 63;
+  const int mrow_l = (kwl >> 6) * 4 + ((ko & 15) >> 2);
+  const int kbit = (ko >> 4) * 4 + (ko & 3);
+
+  const int nqt = (Tq + KV_QT - 1) / KV_QT;
+  issue(0, std::integral_constant<int, 0>());
+  if (nqt > 1) issue(1, std::integral_constant<int, 1>());
+  auto step = [&](auto bi, int it) {
+    constexpr int BI = decltype(bi)::value;
+    wait_tile(it + 1 < nqt);
+    raw_barrier();
+    if (it + 2 < nqt) issue(it + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    const char* cur = ring(bi);
+    const char* Ql = cur;
+    const char* dOl = cur + TILE;
+    const float* lrow = reinterpret_cast<const float*>(cur + 2 * TILE);
+    const float* drow = reinterpret_cast<const float*>(cur + 2 * TILE + XR);
+    const uint16_t* mw = reinterpret_cast<const uint16_t*>(cur + 2 * TILE + 2 * XR);
+
+    // one query block qb = 32 queries: S / dP (8 MFMAs), the probability / dS VALU, then the dV / dK
+    // products (8 MFMAs) over its two 16-query k-steps
+    // a query block's 16 row constants of this lane: four f32x4 reads, concatenated in register order
+    // (reg 4m + r <-> row r + 8m + 4h)
+    auto rows16 = [&](const float* src, int qb) -> f32x16 {
+      const int r0 = qb * 32 + 4 * h;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(src + r0);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + r0 + 8);
+      const f32x4 x2 = *reinterpret_cast<const f32x4*>(src + r0 + 16);
+      const f32x4 x3 = *reinterpret_cast<const f32x4*>(src + r0 + 24);
+      const f32x8 lo = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+      const f32x8 hi = __builtin_shufflevector(x2, x3, 0, 1, 2, 3, 4, 5, 6, 7);
+      return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+    };
+    auto sdp = [&](int qb, f32x16& s, f32x16& dp) {
+      // the row constants enter as the first products' C operands (the dropout re-reads -delta/ds:
+      // a 32x32 MFMA's D overwrites its C, so keeping them live would cost 16 register copies)
+      const f32x16 nl = rows16(lrow, qb);
+      const f32x16 nd = rows16(drow, qb);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 qa = row_frag32_lds(Ql, qb * 32, ks * 16, lane);
+        const bf16x8 da = row_frag32_lds(dOl, qb * 32, ks * 16, lane);
+        s = mfma32(qa, kf[ks], ks == 0 ? nl : s);
+        dp = mfma32(da, vf[ks], ks == 0 ? nd : dp);
+      }
+    };
+    auto prob = [&](int qb, f32x16& s, f32x16& dp, bf16x8 (&pa)[2], bf16x8 (&sa)[2]) {
+      f32x16 nd;
+      if constexpr (DROP) {  // re-read, not kept live: the opaque zero keeps the compiler from reusing sdp's load
+        int z = 0;
+        asm volatile("" : "+v"(z));
+        nd = rows16(drow + z, qb);
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        uint2 bits = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        if constexpr (DROP) bits = *reinterpret_cast<const uint2*>(mw + mrow_l * KV_QT + qb * 32 + 8 * m + 4 * h);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 4 * m + r;
+          const float pr = rp_exp2(s[j]);  // with dropout: p * ds
+          if constexpr (DROP) {
+            const uint32_t km = keep_mask(r < 2 ? bits.x : bits.y, kbit + 16 * (r & 1));
+            s[j] = bfi_select(km, pr, 0.f);
+            dp[j] = pr * bfi_select(km, dp[j], nd[j]);
+          } else {
+            s[j] = pr;
+            dp[j] = pr * dp[j];
+          }
+        }
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        f32x4 a0, a1, b0, b1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a0[r] = s[8 * ss + r];
+          a1[r] = s[8 * ss + 4 + r];
+          b0[r] = dp[8 * ss + r];
+          b1[r] = dp[8 * ss + 4 + r];
+        }
+        pa[ss] = pack8(a0, a1);
+        sa[ss] = pack8(b0, b1);
+      }
+    };
+    auto dvdk = [&](int qb, const bf16x8 (&pa)[2], const bf16x8 (&sa)[2]) {
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const bf16x8 dob = col_frag32_lds(dOl, qb * 32 + ss * 16, dt * 32, lane);
+          const bf16x8 qcb = col_frag32_lds(Ql, qb * 32 + ss * 16, dt * 32, lane);
+          dv[dt] = mfma32(pa[ss], dob, dv[dt]);
+          dk[dt] = mfma32(sa[ss], qcb, dk[dt]);
+        }
+    };
+    // both blocks' S / dP products first, so block 0's VALU runs beside block 1's MFMAs and block 1's
+    // VALU beside block 0's dV / dK products (attn_bwd_kv_dma_kernel's PIPE order)
+    f32x16 s0, dp0, s1, dp1;
+    bf16x8 pa0[2], sa0[2], pa1[2], sa1[2];
+    sdp(0, s0, dp0);
+    sdp(1, s1, dp1);
+    prob(0, s0, dp0, pa0, sa0);
+    dvdk(0, pa0, sa0);
+    prob(1, s1, dp1, pa1, sa1);
+    dvdk(1, pa1, sa1);
+  };
+  for (int it = 0; it < nqt; it += NBUF) {
+    step(std::integral_constant<int, 0>(), it);
+    if (it + 1 < nqt) step(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < nqt) step(std::integral_constant<int, 2>(), it + 2);
+  }
+  // store: dk[dt][reg] = dK[key = kw0 + (reg & 3) + 8 (reg >> 2) + 4h][dk = 32 dt + (l & 31)];
+  // masked keys -> 0; dK = dS^T Q' / log2(e)
+  bf16* dK = (bf16*)a.dk + (int64_t)b * Tk * a.lddk + hh * HD;
+  bf16* dV = (bf16*)a.dv + (int64_t)b * Tk * a.lddv + hh * HD;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int key = kw0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    if (key >= Tk) continue;
+    const bool ok = kvalid[(int64_t)b * Tk + key] != 0;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      rp_st(dK + (int64_t)key * a.lddk + dt * 32 + (lane & 31), ok ? dk[dt][reg] * (1.f / LOG2E) : 0.f);
+      rp_st(dV + (int64_t)key * a.lddv + dt * 32 + (lane & 31), ok ? dv[dt][reg] : 0.f);
+    }
+  }
 }
 
 // =================================================================================================
@@ -2248,6 +2535,13 @@ static bool attn_dma_q_enabled() {
   return v != 0 && attn_dma_enabled();
 }
 
+// RP_ATTN_KV32=1: the 32x32x16 dK/dV kernel instead of the 16x16x32 one — measured slower at the
+// metric shape, kept as a tested option.  Read at every launch (tests flip it).
+static bool attn_kv32_enabled() {
+  const char* e = getenv("RP_ATTN_KV32");
+  return e && e[0] == '1';
+}
+
 // RP_ATTN_PIPE=0: the dK/dV kernel processes its two 32-query halves one after the other instead of
 // issuing both halves' S / dP products ahead of the VALU (A/B tuning)
 static bool attn_pipe_enabled() {
@@ -2370,6 +2664,11 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   } while (0)
       if (small_kv) {
         if (a.drop_thresh) RP_KVD(true, 1); else RP_KVD(false, 1);
+      } else if (attn_kv32_enabled()) {
+        if (a.drop_thresh)
+          hipLaunchKernelGGL((attn_bwd_kv32_kernel<true>), grid, dim3(NT), 0, s, a);
+        else
+          hipLaunchKernelGGL((attn_bwd_kv32_kernel<false>), grid, dim3(NT), 0, s, a);
       } else {
         if (a.drop_thresh) RP_KVD(true, 2); else RP_KVD(false, 2);
       }

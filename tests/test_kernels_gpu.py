@@ -341,6 +341,33 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
 
 
 @pytest.mark.gpu
+def test_attention_kv32_option(dev, monkeypatch):
+    """RP_ATTN_KV32=1 (the 32x32x16 dK/dV kernel): ragged lengths down to one valid key, dropout, the
+    128-key-block path; dQ bitwise the default path's (same dQ kernel), dK / dV within bf16 rounding of
+    it and against fp64 at the tolerances above."""
+    B, H, T, p = 8, 8, 1030, 0.1
+    qkv0 = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(torch.bfloat16)
+    qkv, eff = prescale_q(qkv0, H, 0.125)
+    lens = torch.tensor([T, T - 1, 1000, 777, 640, 129, 2, 1], device=dev)
+    kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
+    olo = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 99, q_prescaled=True, out_lo=olo)
+    do = rnd(B * T, H * 64, dev=dev, seed=T + 1).to(torch.bfloat16)
+    outs = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("RP_ATTN_KV32", v)
+        outs[v] = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True, out_lo=olo)
+    torch.cuda.synchronize()
+    D = H * 64
+    assert torch.equal(outs["0"][:, :D], outs["1"][:, :D])
+    close_per_seq(outs["1"][:, D:], outs["0"][:, D:], B, atol=1e-2, rtol=1e-2, what="kv32 vs kv16 dk/dv")
+    ref_in = eff.requires_grad_(True)
+    ref = attn_ref(ref_in, kv, B, T, H, p, 99)
+    gref = torch.autograd.grad(ref, ref_in, do.double())[0]
+    close_per_seq(outs["1"][:, D:], gref[:, D:], B, atol=6e-2, rtol=6e-2, what="kv32 dk/dv vs fp64")
+
+
+@pytest.mark.gpu
 def test_mha_cross_128_blocks(dev):
     """Cross attention (Tq != Tk, both ragged) on the 128-row block path of all three kernels."""
     B, H, Tq, Tk, dk = 8, 8, 1100, 1000, 64
