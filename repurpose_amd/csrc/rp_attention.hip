@@ -49,13 +49,13 @@ struct AttnCfg {
 };
 
 // Byte offset of (row, byte-in-row) in an LDS tile.  bf16: the 16-byte chunk index is XORed with
-// lds_swz(row) = ((row >> 1) & 3) << 1 | ((row >> 3) & 1).  The pair bits ((row >> 1) & 3 on the
-// 32-byte pair index) make the 16x16x32 reads conflict-free: ds_read_b128 row fragments (16 lanes =
-// 16 rows x 2 adjacent chunks cover all 16 bank quads) and ds_read_b64_tr_b16 column fragments (4
-// consecutive rows x one 32-byte pair per 16-lane group); the chunk-parity bit (row >> 3) & 1 adds
-// the 32x32x16 row fragment (32 rows at one chunk: without it only 8 of the 16 bank quads, 4-way)
-// and leaves a 4-row block's parity constant, so the transposed reads stay conflict-free.
-__device__ __forceinline__ int lds_swz(int row) { return (((row >> 1) & 3) << 1) | ((row >> 3) & 1); }
+// lds_swz(row) = ((row >> 1) & 3) << 1, i.e. the 32-byte pair index with (row >> 1) & 3, which makes
+// both 16x16x32 access patterns conflict-free: ds_read_b128 row fragments (16 lanes = 16 rows x 2
+// adjacent chunks cover all 16 bank quads) and ds_read_b64_tr_b16 column fragments (8 consecutive
+// rows x one 32-byte pair cover all 8 bank octets).  (Adding the chunk-parity bit (row >> 3) & 1,
+// which spreads the 32x32x16 row fragment of the optional kv32 kernel over all 16 quads, made the
+// shipping 16x16 kernels 6-9 % slower, +0.27 ms per step: measured and reverted, round 3.)
+__device__ __forceinline__ int lds_swz(int row) { return ((row >> 1) & 3) << 1; }
 template <typename T>
 __device__ __forceinline__ int lds_off(int row, int byte) {
   if constexpr (std::is_same<T, bf16>::value)

@@ -20,18 +20,31 @@ __global__ void concat_kernel(const float* __restrict__ v, int dv, const float* 
   const int D = dv + da + dt;
   const int64_t r = blockIdx.x;
   TO* orow = out + r * D;
-  for (int c = threadIdx.x * 4; c < D; c += blockDim.x * 4) {
-    float4 q;
-    if (c < dv)
-      q = *reinterpret_cast<const float4*>(v + r * dv + c);
-    else if (c < dv + da)
-      q = *reinterpret_cast<const float4*>(a + r * da + (c - dv));
-    else
-      q = *reinterpret_cast<const float4*>(t + r * dt + (c - dv - da));
-    if constexpr (std::is_same<TO, float>::value) {
-      *reinterpret_cast<float4*>(orow + c) = q;
-    } else {
-      *reinterpret_cast<bf16x4*>(orow + c) = bf16x4{(bf16)q.x, (bf16)q.y, (bf16)q.z, (bf16)q.w};
+  // CU loads per thread issued together before any store (a load-convert-store loop keeps one load in
+  // flight per wave: latency-bound at ~3.6 TB/s for the step's 16384 x 2944 rows)
+  constexpr int CU = 4;
+  for (int c0 = threadIdx.x * 4; c0 < D; c0 += CU * blockDim.x * 4) {
+    float4 q[CU];
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      const int c = c0 + u * blockDim.x * 4;
+      if (c >= D) break;
+      if (c < dv)
+        q[u] = *reinterpret_cast<const float4*>(v + r * dv + c);
+      else if (c < dv + da)
+        q[u] = *reinterpret_cast<const float4*>(a + r * da + (c - dv));
+      else
+        q[u] = *reinterpret_cast<const float4*>(t + r * dt + (c - dv - da));
+    }
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      const int c = c0 + u * blockDim.x * 4;
+      if (c >= D) break;
+      if constexpr (std::is_same<TO, float>::value) {
+        *reinterpret_cast<float4*>(orow + c) = q[u];
+      } else {
+        *reinterpret_cast<bf16x4*>(orow + c) = bf16x4{(bf16)q[u].x, (bf16)q[u].y, (bf16)q[u].z, (bf16)q[u].w};
+      }
     }
   }
 }
