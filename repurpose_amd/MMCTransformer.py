@@ -615,14 +615,22 @@ class _Schedule:
         # bf16 training: the encoder layers' weight gradients are deferred and computed by grouped
         # whole-K launches (all 16 layers x 4 GEMMs = 768 256x256 tiles, three per CU: no split-K
         # slabs and no reduce pass).  Under DP a layer's gradient range is announced to the all-reduce
-        # hooks once its group has been launched, so the first group's exchange overlaps the backward
-        # of the remaining eight layers.
+        # hooks once all its GEMMs have been launched, so the first launch's exchange overlaps the
+        # backward of the remaining layers.
         deferred = [] if (dt == torch.bfloat16 and side is None and M % 64 == 0
                           and os.environ.get("RP_WGRAD_GROUPED", "1") != "0") else None
         held = []  # layer prefixes whose gradients wait for their group launch
-        # one launch for the whole encoder on one GPU; groups of 8 layers when gradient hooks (DP
-        # all-reduce) wait for them, so the first group's exchange overlaps the rest of the backward
-        per_launch = 4 * int(os.environ.get("RP_WGRAD_GROUP_LAYERS", "8" if m._grad_ready_hooks else "16"))
+        # one launch for the whole encoder on one GPU.  With gradient hooks (DP all-reduce) the first
+        # launch is cut so its exchange overlaps the rest of the backward: by default where its 256x256
+        # tiles first fill a whole number of rounds of the CUs (768 tiles at the metric shape: layers
+        # 15..11 plus layer 10's linear2 = 256 tiles = one round, the rest 512 = two; eight-layer
+        # groups were 384 + 384, a half-idle round each: 0.25 ms per step more); RP_WGRAD_GROUP_LAYERS=n
+        # cuts it every n whole layers instead
+        env_layers = os.environ.get("RP_WGRAD_GROUP_LAYERS")
+        per_launch = 4 * int(env_layers or "16")
+        tile_cut = deferred is not None and bool(m._grad_ready_hooks) and env_layers is None
+        ncu = torch.cuda.get_device_properties(dlogits.device).multi_processor_count if tile_cut else 0
+        cut = {"tiles": 0, "done": False}
 
         # LayerNorm gamma / beta partials: reduced together by one rp_colsum_batched launch per flush
         # (before the gradients they finish are announced, and at the end) instead of one per LayerNorm
@@ -644,6 +652,11 @@ class _Schedule:
         def wgrad(dy, x, wname, bname):
             if deferred is not None and wname.startswith("multimodal_encoder."):
                 deferred.append((dy, x, G(wname), G(bname)))
+                if tile_cut and not cut["done"]:
+                    cut["tiles"] += -(-dy.shape[1] // 256) * -(-x.shape[1] // 256)
+                    if cut["tiles"] >= ncu and (cut["tiles"] % ncu == 0 or cut["tiles"] >= 2 * ncu):
+                        cut["done"] = True
+                        flush_group()  # announces the layers already complete (held), not this one
                 return
             if side is None:
                 K.linear_wgrad(dy, x, G(wname), db=G(bname), ws=wws)
@@ -657,7 +670,7 @@ class _Schedule:
         def ready(prefixes, flush=False):
             if deferred is not None and prefixes[0].startswith("multimodal_encoder."):
                 held.append(prefixes)
-                if len(deferred) >= per_launch:
+                if not tile_cut and len(deferred) >= per_launch:
                     flush_group()
                 return
             if m._grad_ready_hooks:
