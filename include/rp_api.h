@@ -68,7 +68,8 @@ int rp_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream);
  *   B(n, k) = B[n*ldb + k] if b_kmajor else B[k*ldb + n]
  * A and B share `dtype` (RP_F32: exact-f32 MFMA parity mode; RP_BF16: bf16 MFMA, fp32 acc).
  * Requirements: the contiguous dimension of A, B and C is a multiple of 8 elements, leading
- * dimensions multiples of 8, base pointers 16-byte aligned.
+ * dimensions multiples of 8, base pointers 16-byte aligned (bias, residual and gate too; ldg a
+ * multiple of 8, ldr of 4).
  * Epilogue order: v = alpha*acc (+ bias[n]); v *= col_scale if n < col_scale_n; relu;
  *   dropout(p, seed, index m*N+n);
  *   gate: v *= gate_scale * (gate[m, n] > 0);  residual: v += residual[m, n];

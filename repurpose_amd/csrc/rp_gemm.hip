@@ -213,7 +213,13 @@ constexpr int gemm_lds_bytes() {
 // ---- shared epilogue: stage the 128x128 fp32 tile in LDS, then 16-byte row chunks per thread ----
 // MODE 0 applies the fused epilogue (bias, relu, dropout, gate, residual, accumulate) and converts;
 // MODE 1 stores the raw fp32 partial tile into split blockIdx.y's slab.
-template <typename TC, int MODE, bool HALVES = false>
+// RESB (fp32 C with a residual, MODE 0): every LDS read and residual load of a pass is issued before
+// the pass's first store.  In the interleaved loop each chunk's residual load waited behind the
+// previous chunk's store (the compiler cannot prove the output and residual rows apart): one HBM
+// round trip per chunk — s_memtime stamps put that epilogue at 1.5x the K = 512 main loop
+// (out_proj forward).  Only the residual shapes take it: the batched registers cost the others
+// their occupancy.
+template <typename TC, int MODE, bool HALVES = false, bool RESB = false>
 __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* lds, int tid, int lane, int wm, int wn,
                                               int64_t m0, int64_t n0, int64_t M, int64_t N, TC* __restrict__ Cout,
                                               int64_t ldc, float alpha, const EpiDev& ep, int split) {
@@ -238,6 +244,65 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* ld
           cs[((HALVES ? 0 : wm * 64) + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
   }
   __syncthreads();
+  if constexpr (RESB) {
+    static_assert(std::is_same<TC, float>::value && MODE == 0, "RESB: fp32 C, MODE 0");
+    constexpr int ITER = HR * CPRO / NT;
+    static_assert(HR * CPRO % NT == 0, "whole chunks per thread");
+    float4 v[ITER], r[ITER];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int id = tid + it * NT;
+      const int row = id / CPRO, cc = (id % CPRO) * OV;
+      const int64_t m = m0 + row + half * HR, n = n0 + cc;
+      v[it] = *reinterpret_cast<const float4*>(cs + row * CST + cc);
+      r[it] = (m < M && n < N) ? *reinterpret_cast<const float4*>(ep.residual + m * ep.ldr + n)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int id = tid + it * NT;
+      const int row = id / CPRO + half * HR, cc = (id % CPRO) * OV;
+      const int64_t m = m0 + row, n = n0 + cc;
+      if (m >= M || n >= N) continue;
+      float e4[4] = {v[it].x * alpha, v[it].y * alpha, v[it].z * alpha, v[it].w * alpha};
+      if (ep.bias) {
+        const float4 q = *reinterpret_cast<const float4*>(ep.bias + n);
+        e4[0] += q.x; e4[1] += q.y; e4[2] += q.z; e4[3] += q.w;
+      }
+      if (n < ep.col_scale_n) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) e4[e] *= ep.col_scale;
+      }
+      if (ep.relu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) e4[e] = fmaxf(e4[e], 0.f);
+      }
+      if (ep.drop_thresh) {
+        const uint32_t kb = rp_keep_bits<4>(dseed, (uint32_t)(m * N + n), ep.drop_thresh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) e4[e] = ((kb >> e) & 1u) ? e4[e] * ep.drop_scale : 0.f;
+      }
+      if (ep.gate) {
+        if (ep.gate_bf16) {
+          const bf16* gp = (const bf16*)ep.gate + m * ep.ldg + n;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) e4[e] = (float)gp[e] > 0.f ? e4[e] * ep.gate_scale : 0.f;
+        } else {
+          const float* gp = (const float*)ep.gate + m * ep.ldg + n;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) e4[e] = gp[e] > 0.f ? e4[e] * ep.gate_scale : 0.f;
+        }
+      }
+      e4[0] += r[it].x; e4[1] += r[it].y; e4[2] += r[it].z; e4[3] += r[it].w;
+      float* dst = (float*)Cbase + m * ldc + n;
+      if (ep.accumulate) {
+        const float4 q = *reinterpret_cast<const float4*>(dst);
+        e4[0] += q.x; e4[1] += q.y; e4[2] += q.z; e4[3] += q.w;
+      }
+      *reinterpret_cast<float4*>(dst) = make_float4(e4[0], e4[1], e4[2], e4[3]);
+    }
+    continue;
+  }
   for (int id = tid; id < HR * CPRO; id += NT) {
     const int row = id / CPRO + half * HR, cc = (id % CPRO) * OV;
     const int64_t m = m0 + row, n = n0 + cc;
@@ -552,7 +617,7 @@ __device__ __forceinline__ void dma_mainloop(const bf16* __restrict__ A, int64_t
   if (D::STAGES == 1) __syncthreads();
 }
 
-template <bool AK, bool BKM, typename TC, int MODE, int CFG>
+template <bool AK, bool BKM, typename TC, int MODE, int CFG, bool RESB = false>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t N, int64_t K,
                                                               const bf16* __restrict__ A, int64_t lda,
                                                               const bf16* __restrict__ B, int64_t ldb,
@@ -585,7 +650,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
   for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
   dma_mainloop<AK, BKM, CFG>(A, lda, M, B, ldb, N, m0, n0, kbeg, kend, want_bias, acc, bacc, lds, tid, lane, wid, wm,
                              wn);
-  gemm_epilogue<TC, MODE, D::HALVES>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
+  gemm_epilogue<TC, MODE, D::HALVES, RESB>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
   if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab, split);
 }
 
@@ -1234,6 +1299,20 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
       default: RP_DMA_LAUNCH1(AKV, BKV, MODEV, 2, GRID); break;               \
     }                                                                         \
   } while (0)
+      if constexpr (std::is_same<TC, float>::value) {
+        if (splits == 0 && ak && bk && ep.residual) {  // the residual (fp32) forward shapes: see RESB
+          dim3 grid((unsigned)tiles);
+          switch (cfg) {
+            case 0: hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, true, TC, 0, 0, true>), grid, dim3(NT), 0, s, M, N, K, ab,
+                                       lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab); break;
+            case 1: hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, true, TC, 0, 1, true>), grid, dim3(NT), 0, s, M, N, K, ab,
+                                       lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab); break;
+            default: hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, true, TC, 0, 2, true>), grid, dim3(NT), 0, s, M, N, K,
+                                        ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab); break;
+          }
+          return rp_check_launch("rp_gemm");
+        }
+      }
       if (splits == 0) {
         dim3 grid((unsigned)tiles);
         if (ak && bk) RP_DMA_LAUNCH(true, true, 0, grid);
