@@ -789,8 +789,11 @@ struct G8 {
   static constexpr int LDS = S * SLOT > EPI ? S * SLOT : EPI;
 };
 
-// epilogue: four passes of 64 rows staged as fp32 in LDS, then 16-byte row chunks per thread
-template <typename TC, int MODE, int BNT>
+// epilogue: four passes of 64 rows staged as fp32 in LDS, then 16-byte row chunks per thread.
+// GATEB (bf16 C, bf16 gate: the linear2 dgrad): a pass's gate chunks are loaded before its stores
+// (16 bytes per chunk; inline, each waited behind the previous chunk's store, as the residual did in
+// the 128 x 128 epilogue)
+template <typename TC, int MODE, int BNT, bool GATEB = false>
 __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], char* lds, int tid, int lane, int wm,
                                                int wn, int64_t m0, int64_t n0, int64_t M, int64_t N,
                                                TC* __restrict__ Cout, int64_t ldc, float alpha, const EpiDev& ep,
@@ -815,7 +818,20 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
             cs[(i * 16 + g * 4 + r) * G::CST + wn * G::WN + j * 16 + cl] = acc[(pass & 1) * 4 + i][j][r];
     }
     __syncthreads();
-    for (int id = tid; id < 64 * CPRO; id += NT8) {
+    constexpr int ITER = 64 * CPRO / NT8;
+    bf16x8 gv[GATEB ? ITER : 1];
+    if constexpr (GATEB) {
+      static_assert(OV == 8 && MODE == 0, "GATEB: bf16 C");
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int id = tid + it * NT8;
+        const int64_t m = m0 + pass * 64 + id / CPRO, n = n0 + (id % CPRO) * OV;
+        if (m < M && n < N) gv[it] = *reinterpret_cast<const bf16x8*>((const bf16*)ep.gate + m * ep.ldg + n);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int id = tid + it * NT8;
       const int row = id / CPRO, cc = (id % CPRO) * OV;
       const int64_t m = m0 + pass * 64 + row, n = n0 + cc;
       if (m >= M || n >= N) continue;
@@ -846,7 +862,10 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
 #pragma unroll
           for (int e = 0; e < OV; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * ep.drop_scale : 0.f;
         }
-        if (ep.gate) {
+        if constexpr (GATEB) {
+#pragma unroll
+          for (int e = 0; e < OV; ++e) v[e] = (float)gv[it][e] > 0.f ? v[e] * ep.gate_scale : 0.f;
+        } else if (ep.gate) {
           if (ep.gate_bf16) {
             const bf16* gp = (const bf16*)ep.gate + m * ep.ldg + n;
 #pragma unroll
@@ -907,7 +926,7 @@ __device__ __forceinline__ void rp_lgkm0() {
 
 // One 256 x BNT output tile over the K range [kbeg, kend): the phased main loop, the epilogue and
 // (bias_dst != null, m-major A) the tile rows' column sums of the staged A: bias_dst[m0 + r] (+)=.
-template <bool AK, bool BKM, typename TC, int MODE, int BNT>
+template <bool AK, bool BKM, typename TC, int MODE, int BNT, bool GATEB = false>
 __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __restrict__ A, int64_t lda,
                                            const bf16* __restrict__ B, int64_t ldb, TC* __restrict__ Cout,
                                            int64_t ldc, float alpha, const EpiDev& ep, int64_t kbeg, int64_t kend,
@@ -1085,7 +1104,7 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
   }
   if (wm == 0) rp_raw_barrier();  // match the lagging half's barrier count
   __syncthreads();
-  gemm8_epilogue<TC, MODE, BNT>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
+  gemm8_epilogue<TC, MODE, BNT, GATEB>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
   if (pf) asm volatile("" ::"v"(pfd[0]), "v"(pfd[1]));
   if (want_bias) {
     __syncthreads();
@@ -1102,7 +1121,7 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
   }
 }
 
-template <bool AK, bool BKM, typename TC, int MODE, int BNT>
+template <bool AK, bool BKM, typename TC, int MODE, int BNT, bool GATEB = false>
 __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int64_t K, const bf16* __restrict__ A,
                                                        int64_t lda, const bf16* __restrict__ B, int64_t ldb,
                                                        TC* __restrict__ Cout, int64_t ldc, float alpha, EpiDev ep,
@@ -1120,8 +1139,8 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
     kend = kbeg + kchunk < K ? kbeg + kchunk : K;
   }
   float* bias_dst = (MODE == 1 && bslab != nullptr && n0 == 0) ? bslab + (int64_t)split * M : nullptr;
-  gemm8_tile<AK, BKM, TC, MODE, BNT>(M, N, A, lda, B, ldb, Cout, ldc, alpha, ep, kbeg, kend, m0, n0, split, bias_dst, 0,
-                                     lds);
+  gemm8_tile<AK, BKM, TC, MODE, BNT, GATEB>(M, N, A, lda, B, ldb, Cout, ldc, alpha, ep, kbeg, kend, m0, n0, split,
+                                            bias_dst, 0, lds);
 }
 
 // grouped weight gradients on 256 x 256 tiles (the WgGroup of wgrad_grouped_kernel, whole K): twice
@@ -1255,6 +1274,13 @@ int launch_gemm8(int bn, int64_t M, int64_t N, int64_t K, const bf16* a, int64_t
   hipLaunchKernelGGL((gemm8_kernel<AKV, BKV, TC, MODEV, 256>), GRID, dim3(NT8), 0, s, M, N, K, a, lda, b, ldb, c, \
                      ldc, alpha, ep, kchunk, bslab)
 #define RP_G8_LAUNCH(AKV, BKV, MODEV, GRID) RP_G8_LAUNCH1(AKV, BKV, MODEV, 256, GRID)
+  if constexpr (!std::is_same<TC, float>::value) {
+    if (splits == 0 && ak && !bk && ep.gate && ep.gate_bf16) {  // the linear2 dgrad: see GATEB
+      hipLaunchKernelGGL((gemm8_kernel<true, false, TC, 0, 256, true>), dim3((unsigned)tiles), dim3(NT8), 0, s, M, N, K,
+                         a, lda, b, ldb, c, ldc, alpha, ep, kchunk, bslab);
+      return rp_check_launch("rp_gemm");
+    }
+  }
   if (splits == 0) {
     dim3 grid((unsigned)tiles);
     if (ak && bk) RP_G8_LAUNCH(true, true, 0, grid);
