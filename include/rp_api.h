@@ -293,9 +293,10 @@ enum { RP_ATTN_Q_PRESCALED = 0x100 };
  * sums the bf16-rounded probabilities the P.V product uses, on the matrix core).
  * out_lo (bf16, optional): bf16(O - bf16(O)), the rounding residual of out, for the backward's
  * delta = rowsum(dout * O) (pass the same pointer to the backward; NULL: delta from out alone).
- * Dropout on the attention probabilities with probability p: for query q and group g one stream
- * st = rp_hash(rp_hash(seed, b*H+h), q*4 + g) is advanced by xorshift32 (x ^= x<<13; x ^= x>>17;
- * x ^= x<<5) eight times per 64-key tile, tiles in order; in tile t word j (1..8th of the tile)
+ * Dropout on the attention probabilities with probability p: for query q and group g one
+ * multiply-with-carry stream (MWC64X) x = rp_hash(rp_hash(seed, b*H+h), q*4 + g),
+ * c = rp_hash(x, 0x6A09E667) >> 1 is stepped (t = 4294883355*x + c; x = lo32(t); c = hi32(t)) eight
+ * times per 64-key tile, tiles in order, each step giving the word x ^ c; in tile t word j (1..8th of the tile)
  * holds the keys 64t + 16*(j>>1) + 4g + 2*(j&1) + {0: low 16 bits, 1: high 16 bits}; a key is kept iff its 16 bits
  * read as int16 are >= round(p*65536) - 32768 (rp_hash: repurpose_amd/csrc/rp_common.h).
  * The forward writes the keep bits to `dropmask` (uint16 [B*H][ceil(T/64)][4][roundup(T,128)],

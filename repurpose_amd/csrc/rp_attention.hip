@@ -223,24 +223,28 @@ __device__ __forceinline__ float quad_sum(float v) {
 }
 
 // Attention dropout stream (include/rp_api.h, rp_attn_fwd): for query q and lane group g one
-// xorshift32 stream runs over the whole key range: st = rp_hash(seed_bh, q*4 + g), then eight
-// xorshift32 steps per 64-key tile, in tile order; in tile `tile` word j covers keys
-// 64*tile + 16*(j>>1) + 4*g + r with r = 2*(j&1) + {0: low half, 1: high half}; a key is kept iff its
-// half, read as a signed 16-bit integer, is >= round(p*65536) - 32768 (probability 1 - p, exact to
-// 2^-16).  One seeding hash per (query, lane group) per launch, carried across tiles in a register.
-// Outputs dm[j] (0xFFFF in each dropped half: the AND-NOT mask of the packed bf16 P pair) and
-// returns the 16 keep bits, bit (kt*4 + r).  Full-rate VALU only: a saturating packed 16-bit
-// subtract + arithmetic shift per pair, no 32-bit multiplies in the tile loop.
-__device__ __forceinline__ uint32_t drop_masks(uint32_t& st, uint32_t thr, uint32_t dm[8]) {
+// multiply-with-carry stream (MWC64X: x' = lo(A x + c), c' = hi(A x + c), A = 4294883355, output
+// word x' ^ c') runs over the whole key range, seeded x = rp_hash(seed_bh, q*4 + g), c =
+// rp_hash(x, 0x6A09E667) >> 1; eight steps per 64-key tile, in tile order; in tile `tile` word j
+// covers keys 64*tile + 16*(j>>1) + 4*g + r with r = 2*(j&1) + {0: low half, 1: high half}; a key is
+// kept iff its half, read as a signed 16-bit integer, is >= round(p*65536) - 32768 (probability
+// 1 - p, exact to 2^-16).  One step is one v_mad_u64_u32 (+ the carry move and the output xor):
+// ~11 issue cycles per word against ~26 for the xorshift32 stream of rounds 1-3, in a tile loop
+// that is VALU-issue bound (scripts/rng_cost_probe.hip).  Outputs dm[j] (0xFFFF in each dropped
+// half: the AND-NOT mask of the packed bf16 P pair) and returns the 16 keep bits, bit (kt*4 + r).
+constexpr uint32_t MWC_A = 4294883355u;
+__device__ __forceinline__ uint64_t mwc_seed(uint32_t x) {
+  return (uint64_t)x | ((uint64_t)(rp_hash(x, 0x6A09E667u) >> 1) << 32);
+}
+__device__ __forceinline__ uint32_t drop_masks(uint64_t& st, uint32_t thr, uint32_t dm[8]) {
   const short ts = (short)((int)thr - 32768);
   const i16x2 t2 = {ts, ts};
   uint32_t acc = 0u;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    st ^= st << 13;
-    st ^= st >> 17;
-    st ^= st << 5;
-    const i16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, st), t2);  // < 0 <=> dropped
+    st = (uint64_t)MWC_A * (uint32_t)st + (st >> 32);
+    const uint32_t wd = (uint32_t)st ^ (uint32_t)(st >> 32);
+    const i16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, wd), t2);  // < 0 <=> dropped
     const uint32_t m = __builtin_bit_cast(uint32_t, (i16x2)(d >> (short)15));
     dm[j] = m;
     // keep bit of the low half -> bit 4*(j>>1) + 2*(j&1); high half -> 16 + that + 1 (folded below)
@@ -355,18 +359,20 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
   // m: reference max (log2 units) once set (mset); 0 before, when O and l are still zero
   float m[QT], lp[QT];
   bool mset[QT];
+  float gthr[QT];  // grow bound of the lane-local test: -inf until the reference is set, then RESCALE_LOG2
   // dropout stream state of this lane's queries (carried across the key tiles)
-  uint32_t dst[QT];
+  uint64_t dst[QT];
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
     m[qt] = 0.f;
     lp[qt] = 0.f;
     mset[qt] = false;
+    gthr[qt] = -INFINITY;
     dst[qt] = 0u;
   }
   if constexpr (DROP) {
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) dst[qt] = rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g);
+    for (int qt = 0; qt < QT; ++qt) dst[qt] = mwc_seed(rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g));
   }
 
   Stage<T, FW_KT> sk, sv;
@@ -440,7 +446,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
     // RESCALE_LOG2 (P <= 2^8 meanwhile, exact in fp32/bf16 range), or on the first finite max;
     // l and O share the reference, so out = O / l is unchanged and the lse uses the same m.
     float rel[QT];
-    bool grow = false;
+    uint64_t grow = 0;
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
       if (!full) {
@@ -454,12 +460,16 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][qt][r]);
-      rel[qt] = quad_max(mx);
-      grow |= mset[qt] ? rel[qt] > RESCALE_LOG2 : rel[qt] > -INFINITY;  // no NaN anywhere
+      // the lane-local test decides the wave-uniform branch exactly as the quad maximum would (the
+      // quad maximum exceeds a bound iff one of its lanes does); the cross-lane reduction runs
+      // only inside the branch, on the tiles that move the reference
+      rel[qt] = mx;
+      grow |= __ballot(mx > gthr[qt]);  // no NaN anywhere
     }
-    if (__any(grow)) {  // wave-uniform branch: move the reference of the growing lanes
+    if (grow != 0) {  // wave-uniform branch: move the reference of the growing lanes
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) {
+        rel[qt] = quad_max(rel[qt]);
         const bool gq = mset[qt] ? rel[qt] > RESCALE_LOG2 : rel[qt] > -INFINITY;
         const float alpha = gq ? (mset[qt] ? rp_exp2(-rel[qt]) : 0.f) : 1.f;
         const float sub = gq ? rel[qt] : 0.f;
@@ -468,6 +478,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
         for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
         m[qt] += sub;
         mset[qt] = mset[qt] || gq;
+        gthr[qt] = mset[qt] ? RESCALE_LOG2 : -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) s[kt][qt] -= sub;
       }
@@ -484,7 +495,7 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
       }
       lp[qt] += (t4[0] + t4[1]) + (t4[2] + t4[3]);
     }
-    // ---- dropout: 8 drop masks per (query, tile) from one xorshift stream; keep bits stored ----
+    // ---- dropout: 8 drop masks per (query, tile) from one MWC stream; keep bits stored ----
     uint32_t dm[QT][8];
     if constexpr (DROP) {
 #pragma unroll
@@ -2304,7 +2315,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
   float m[QT];
   bool mset[QT];
-  uint32_t dst[QT];
+  float gthr[QT];  // the grow bound of the lane-local test: -inf until the reference is set, then RESCALE_LOG2
+  uint64_t dst[QT];
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
 #pragma unroll
@@ -2313,7 +2325,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
     ls[qt] = zero4();
     lp[qt] = 0.f;
     mset[qt] = false;
-    dst[qt] = DROP ? rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g) : 0u;
+    gthr[qt] = -INFINITY;
+    dst[qt] = DROP ? mwc_seed(rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g)) : 0u;
   }
 
   auto ring = [&](auto bi) -> char* {
@@ -2391,7 +2404,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
     }
     // ---- column max relative to the reference; deferred rescale (see attn_fwd_kernel) ----
     float rel[QT];
-    bool grow = false;
+    uint64_t grow = 0;
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
       float mx = s[0][qt][0];
@@ -2399,12 +2412,13 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][qt][r]);
-      rel[qt] = quad_max(mx);
-      grow |= mset[qt] ? rel[qt] > RESCALE_LOG2 : rel[qt] > -INFINITY;
+      rel[qt] = mx;  // lane-local test, quad maximum inside the branch (see attn_fwd_kernel)
+      grow |= __ballot(mx > gthr[qt]);  // one compare into a lane mask per query tile
     }
-    if (__any(grow)) {
+    if (grow != 0) {
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) {
+        rel[qt] = quad_max(rel[qt]);
         const bool gq = mset[qt] ? rel[qt] > RESCALE_LOG2 : rel[qt] > -INFINITY;
         const float alpha = gq ? (mset[qt] ? rp_exp2(-rel[qt]) : 0.f) : 1.f;
         const float sub = gq ? rel[qt] : 0.f;
@@ -2416,6 +2430,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
         for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
         m[qt] += sub;
         mset[qt] = mset[qt] || gq;
+        gthr[qt] = mset[qt] ? RESCALE_LOG2 : -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) s[kt][qt] -= sub;
       }

@@ -6,7 +6,8 @@ V=$1; N=${2:-3}; ARGS=${3:-"--steps 20 --warmup 3 --no-cpu-baseline --no-parity-
 mkdir -p gpurun_out
 for i in $(seq 1 $N); do
   for v in $VA $VB; do
-    env $V=$v timeout -k 10 300 python -u bench.py $ARGS > gpurun_out/abenv_$v.log 2>&1 || { echo "FAILED $V=$v"; tail -5 gpurun_out/abenv_$v.log; exit 1; }
-    echo "$V=$v $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/abenv_$v.log | head -1)"
+    lg=gpurun_out/abenv_$(echo "$v" | tr -c 'A-Za-z0-9_\n' _).log
+    env $V=$v timeout -k 10 300 python -u bench.py $ARGS > $lg 2>&1 || { echo "FAILED $V=$v"; tail -5 $lg; exit 1; }
+    echo "$V=$v $(grep -o '"ms_per_step": [0-9.]*' $lg | head -1)"
   done
 done

@@ -177,24 +177,35 @@ def test_layernorm_relu_dropout(dev):
 
 
 # ----------------------------------------------------------------------------------- attention
+MWC_A_COMPL = (1 << 32) - 4294883355  # csrc/rp_attention.hip MWC_A = 2^32 - 83941
+
+
+def mwc_step(x, c):
+    """One MWC64X step, t = A x + c = x 2^32 + (c - 83941 x), in exact int64 arithmetic: returns
+    (lo(t), hi(t))."""
+    d = c - MWC_A_COMPL * x
+    lo = torch.remainder(d, 1 << 32)
+    return lo, x + torch.div(d - lo, 1 << 32, rounding_mode="floor")
+
+
 def attn_keep(B, H, T, p, seed, dev):
     """torch restatement of the attention dropout bits (include/rp_api.h, rp_attn_fwd): per (query,
-    lane group g) one xorshift32 stream seeded by rp_hash, eight words per 64-key tile in tile order;
-    16-bit halves read as int16."""
+    lane group g) one MWC64X stream seeded x = rp_hash(seed_bh, q*4 + g), c = rp_hash(x, 0x6A09E667)
+    >> 1; eight output words (x ^ c after each step) per 64-key tile in tile order; 16-bit halves
+    read as int16."""
     KT = (T + 63) // 64
     bh = torch.arange(B * H, device=dev, dtype=torch.int64)
     sbh = rp_hash(seed, bh).view(B * H, 1, 1)
     q = torch.arange(T, device=dev, dtype=torch.int64).view(1, T, 1)
     g = torch.arange(4, device=dev, dtype=torch.int64).view(1, 1, 4)
-    st = rp_hash(sbh, q * 4 + g)                                # [BH, T, 4]
+    x = rp_hash(sbh, q * 4 + g)                                 # [BH, T, 4]
+    c = rp_hash(x, 0x6A09E667) >> 1
     tiles = []
     for _ in range(KT):
         words = []
         for _ in range(8):
-            st = (st ^ (st << 13)) & M32
-            st = st ^ (st >> 17)
-            st = (st ^ (st << 5)) & M32
-            words.append(st)
+            x, c = mwc_step(x, c)
+            words.append(x ^ c)
         tiles.append(torch.stack(words, -1))                    # [BH, T, g, j]
     w = torch.stack(tiles, 2)                                   # [BH, T, KT, g, j]
     half = torch.stack([w & 0xFFFF, w >> 16], -1)               # [BH, T, KT, g, j, lo/hi]
@@ -203,6 +214,20 @@ def attn_keep(B, H, T, p, seed, dev):
     keep = keep.view(B * H, T, KT, 4, 4, 2, 2)                  # [.., g, kt, r>>1, r&1]
     keep = keep.permute(0, 1, 2, 4, 3, 5, 6).reshape(B * H, T, KT * 64)[:, :, :T]
     return keep.reshape(B, H, T, T)
+
+
+def test_mwc_restatement_matches_the_full_product():
+    """the int64 MWC step equals the 64-bit product A x + c computed with Python integers"""
+    import random
+    rng = random.Random(5)
+    xs = [rng.randrange(1 << 32) for _ in range(256)] + [0, 1, M32]
+    cs = [rng.randrange(1 << 31) for _ in range(256)] + [0, (1 << 31) - 1, 4294883354]
+    x = torch.tensor(xs, dtype=torch.int64)
+    c = torch.tensor(cs, dtype=torch.int64)
+    lo, hi = mwc_step(x, c)
+    for xi, ci, l, h in zip(xs, cs, lo.tolist(), hi.tolist()):
+        t = 4294883355 * xi + ci
+        assert (l, h) == (t & M32, t >> 32)
 
 
 def attn_ref(qkv, kv, B, T, H, p=0.0, seed=0):
