@@ -135,6 +135,9 @@ class MMCTransformer(nn.Module):
         self._layout = None
         self._grad_ready_hooks = []   # called with (lo, hi) flat ranges whose gradients are final
         self._grad_done_hooks = []    # called once at the end of backward
+        # set by CapturedTrainStep in place of zero_grad(): the next backward WRITES every trained
+        # gradient (each has exactly one producer) instead of accumulating into a zeroed buffer
+        self._grad_fresh = False
         self._seed_base = None        # int32 device word while a step is captured (graph.py), else None
         self._build_flat()
         for p in self.parameters():
@@ -595,6 +598,8 @@ class _Schedule:
         sd = self.scale_drop
         S = self.saved
         self._g = m._bind_grads()
+        acc = not m._grad_fresh  # False: write the gradients (the captured step's zero_grad)
+        m._grad_fresh = False
         lib = _native.load()
         ws = torch.empty(max(lib.rp_colsum_workspace(M, 256), 1), device=dlogits.device, dtype=_F32)
         d, dff = m.d_model, m.d_ff
@@ -638,11 +643,11 @@ class _Schedule:
 
         def flush_cs():
             if cs:
-                K.colsum_batched(cs)
+                K.colsum_batched(cs, accumulate=acc)
                 cs.clear()
 
         def flush_group():
-            K.linear_wgrad_grouped(deferred)
+            K.linear_wgrad_grouped(deferred, accumulate=acc)
             deferred.clear()
             flush_cs()
             for pf in held:
@@ -659,11 +664,11 @@ class _Schedule:
                         flush_group()  # announces the layers already complete (held), not this one
                 return
             if side is None:
-                K.linear_wgrad(dy, x, G(wname), db=G(bname), ws=wws)
+                K.linear_wgrad(dy, x, G(wname), db=G(bname), accumulate=acc, ws=wws)
                 return
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                K.linear_wgrad(dy, x, G(wname), db=G(bname), ws=wws)
+                K.linear_wgrad(dy, x, G(wname), db=G(bname), accumulate=acc, ws=wws)
             dy.record_stream(side)
             x.record_stream(side)
 
@@ -688,8 +693,8 @@ class _Schedule:
 
         dl = dlogits.reshape(M, 1).contiguous().float()
         # cls_head[7]  (N = 1)
-        K.colsum(S["c2"], w=dl.view(M), out=G("cls_head.7.weight").view(-1), accumulate=True, ws=ws)
-        K.colsum(dl, out=G("cls_head.7.bias"), accumulate=True, ws=ws)
+        K.colsum(S["c2"], w=dl.view(M), out=G("cls_head.7.weight").view(-1), accumulate=acc, ws=ws)
+        K.colsum(dl, out=G("cls_head.7.bias"), accumulate=acc, ws=ws)
         dz2 = K.rowdot_bwd_dx(dl, self.P("cls_head.7.weight"), gate=S["c2"], gate_scale=sd, out_dtype=dt)
         # cls_head[4]
         wgrad(dz2, S["c1"], "cls_head.4.weight", "cls_head.4.bias")

@@ -2233,7 +2233,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
 constexpr int FD_TKMAX = 4096;
 
 template <bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_fwd_dma_kernel(MhaDev a) {
+__global__ __launch_bounds__(NT, 3) void attn_fwd_dma_kernel(MhaDev a) {
   constexpr int QT = 2, QB = NW * 16 * QT;  // 128 queries per workgroup
   using C = AttnCfg<bf16>;
   constexpr int TILE = FW_KT * C::ROWB;  // 8 KB

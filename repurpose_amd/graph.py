@@ -31,6 +31,8 @@ an N-rank step is one ``hipGraphLaunch`` per rank, the same execution mode as on
 warm-up steps run the collectives eagerly first (communicator set-up is not capturable).  A gloo
 reducer (CPU collectives) cannot be captured: it raises.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -81,8 +83,13 @@ class CapturedTrainStep:
                     raise ValueError(f"CapturedTrainStep.load: {k} shape {tuple(v.shape)} != captured {tuple(dst.shape)}")
                 dst.copy_(v, non_blocking=True)
 
-    def _eager(self):
-        self.opt.zero_grad()
+    def _eager(self, fresh=False):
+        if fresh:
+            # the captured step: the backward writes every gradient, so the 210 MB zero fill of the
+            # flat gradient buffer and the accumulate reads of the weight-gradient epilogues drop out
+            self.model._grad_fresh = True
+        else:
+            self.opt.zero_grad()
         out = self.model(self.batch)
         loss = self.loss_fn(self.model, out)
         loss.backward()
@@ -120,9 +127,10 @@ class CapturedTrainStep:
             # keep querying its own (uncaptured) events while this thread captures
             mode = "thread_local" if self.model._grad_ready_hooks else "global"
             with torch.cuda.graph(g, capture_error_mode=mode):
-                self._loss = self._eager()
+                self._loss = self._eager(fresh=os.environ.get("RP_GRAD_FRESH", "1") != "0")
         finally:
             self.model._seed_base = None
+            self.model._grad_fresh = False
             self.opt._coef_dev = None
         self.opt._step = step0  # capture executed nothing; replay() counts the step
         self._graph = g

@@ -125,3 +125,32 @@ def test_capture_requires_a_warmup_step(dev):
     m, o = _model(dev, "bf16", 0.0)
     with pytest.raises(ValueError, match="warmup"):
         CapturedTrainStep(m, o, _batches(dev, 1)[0], warmup=0)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_captured_backward_writes_every_gradient(dev, dtype):
+    """the captured step replaces zero_grad() by a backward that WRITES the gradients: poison every
+    trained gradient view with NaN before the capture; the replays must still match eager steps
+    bitwise (any gradient left to accumulate would carry the NaN into its parameters)"""
+    batches = _batches(dev, 3)
+    me, oe = _model(dev, dtype, 0.0)
+    for b in batches:
+        oe.zero_grad()
+        out = me(b)
+        (me.losses(*out)["cls_loss"] / 2).backward()
+        oe.step()
+    mg, og = _model(dev, dtype, 0.0)
+    run = CapturedTrainStep(mg, og, {k: v.clone() for k, v in batches[0].items()}, warmup=1)
+    run.load(batches[0])
+    run.step()
+    for p in mg.parameters():
+        if p.grad is not None:
+            p.grad.fill_(float("nan"))
+    for b in batches[1:]:
+        run.load(b)
+        run.step()
+    torch.cuda.synchronize()
+    n = me.trainable_numel()
+    assert torch.equal(mg.flat_params()[:n], me.flat_params()[:n])
+    assert torch.equal(og._m, oe._m) and torch.equal(og._v, oe._v)
+    assert not mg._grad_fresh
