@@ -43,8 +43,9 @@ extern "C" {
 #endif
 
 /* Element dropout used by the GEMM and LayerNorm epilogues, dropout(v, p, seed, idx):
- *   keep(seed, idx): w0 = rp_hash(seed, idx >> 3), w(j+1) = xorshift32(w(j)) (x ^= x<<13;
- *   x ^= x>>17; x ^= x<<5); element idx reads the 16 bits ((idx & 1) ? high : low) of
+ *   keep(seed, idx): w0 = rp_hash(seed, idx >> 3); w1..w3 = x ^ c after successive MWC64X steps
+ *   (t = 4294883355*x + c; x = lo32(t); c = hi32(t)) from x = w0, c = w0 >> 1; element idx reads
+ *   the 16 bits ((idx & 1) ? high : low) of
  *   w((idx & 7) >> 1) as int16 and is kept iff they are >= round(p*65536) - 32768;
  *   kept values are scaled by 1/(1-p).  rp_hash: repurpose_amd/csrc/rp_common.h. */
 enum { RP_OK = 0, RP_ERR_ARG = 1, RP_ERR_LAUNCH = 2 };

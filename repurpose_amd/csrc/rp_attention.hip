@@ -232,7 +232,6 @@ __device__ __forceinline__ float quad_sum(float v) {
 // ~11 issue cycles per word against ~26 for the xorshift32 stream of rounds 1-3, in a tile loop
 // that is VALU-issue bound (scripts/rng_cost_probe.hip).  Outputs dm[j] (0xFFFF in each dropped
 // half: the AND-NOT mask of the packed bf16 P pair) and returns the 16 keep bits, bit (kt*4 + r).
-constexpr uint32_t MWC_A = 4294883355u;
 __device__ __forceinline__ uint64_t mwc_seed(uint32_t x) {
   return (uint64_t)x | ((uint64_t)(rp_hash(x, 0x6A09E667u) >> 1) << 32);
 }
@@ -242,8 +241,7 @@ __device__ __forceinline__ uint32_t drop_masks(uint64_t& st, uint32_t thr, uint3
   uint32_t acc = 0u;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    st = (uint64_t)MWC_A * (uint32_t)st + (st >> 32);
-    const uint32_t wd = (uint32_t)st ^ (uint32_t)(st >> 32);
+    const uint32_t wd = rp_mwc_next(st);
     const i16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, wd), t2);  // < 0 <=> dropped
     const uint32_t m = __builtin_bit_cast(uint32_t, (i16x2)(d >> (short)15));
     dm[j] = m;

@@ -54,24 +54,29 @@ __device__ __forceinline__ uint32_t rp_hash(uint32_t seed, uint32_t idx) {
 
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 
+// multiply-with-carry step (MWC64X): state x | c << 32 -> lo / hi of A x + c; output word x ^ c
+constexpr uint32_t RP_MWC_A = 4294883355u;
+__device__ __forceinline__ uint32_t rp_mwc_next(uint64_t& st) {
+  st = (uint64_t)RP_MWC_A * (uint32_t)st + (st >> 32);
+  return (uint32_t)st ^ (uint32_t)(st >> 32);
+}
+
 // Element dropout (GEMM / LayerNorm epilogues), per aligned group of 8 elements (index idx ->
-// group idx >> 3, slot e = idx & 7): w0 = rp_hash(seed, group), w(j+1) = xorshift32(w(j));
-// slot e reads the 16-bit half (e & 1) of w(e >> 1) as int16 and is kept iff it is
-// >= thresh16 - 32768 (probability 1 - p to 2^-16).  Returns the 8 keep bits (bit e).
-// One hash + 3 shift-xor steps per 8 elements; the keep test is a saturating packed 16-bit
-// subtract + arithmetic shift per pair (no 32-bit multiply per element).
+// group idx >> 3, slot e = idx & 7): w0 = rp_hash(seed, group), then w1..w3 from the MWC64X
+// stream seeded x = w0, c = w0 >> 1; slot e reads the 16-bit half (e & 1) of w(e >> 1) as int16
+// and is kept iff it is >= thresh16 - 32768 (probability 1 - p to 2^-16).  Returns the 8 keep bits
+// (bit e).  One hash + 3 one-multiply MWC steps per 8 elements (rounds 1-3: 3 xorshift32 steps,
+// six shift / xor ops each); the keep test is a saturating packed 16-bit subtract + arithmetic
+// shift per pair (no 32-bit multiply per element).
 __device__ __forceinline__ uint32_t rp_keep8(uint32_t seed, uint32_t group, uint32_t thresh16) {
   uint32_t w = rp_hash(seed, group);
+  uint64_t st = (uint64_t)w | ((uint64_t)(w >> 1) << 32);
   const short ts = (short)((int)thresh16 - 32768);
   const i16x2 t2 = {ts, ts};
   uint32_t acc = 0u;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    if (j) {
-      w ^= w << 13;
-      w ^= w >> 17;
-      w ^= w << 5;
-    }
+    if (j) w = rp_mwc_next(st);
     const i16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w), t2);  // < 0: dropped
     const uint32_t m = __builtin_bit_cast(uint32_t, (i16x2)(d >> (short)15));
     acc |= ~m & ((1u << (2 * j)) | (1u << (16 + 2 * j + 1)));

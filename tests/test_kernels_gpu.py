@@ -22,20 +22,17 @@ def rp_hash(seed, idx):
     return h
 
 
-def xorshift32(w):
-    w = (w ^ (w << 13)) & M32
-    w = w ^ (w >> 17)
-    return (w ^ (w << 5)) & M32
-
-
 def keep_mask(seed, idx, p):
     """GEMM / LayerNorm element dropout (csrc/rp_common.h rp_keep8): per aligned group of 8
-    elements one rp_hash + xorshift32 stream; 16-bit halves read as int16."""
+    elements one rp_hash word w0, then three MWC64X words (x ^ c) from x = w0, c = w0 >> 1; 16-bit
+    halves read as int16."""
     thr = int(p * 65536 + 0.5)
     w0 = rp_hash(seed, idx >> 3)
     words = [w0]
+    x, c = w0, w0 >> 1
     for _ in range(3):
-        words.append(xorshift32(words[-1]))
+        x, c = mwc_step(x, c)
+        words.append(x ^ c)
     W = torch.stack(words, -1)
     e = idx & 7
     w = torch.gather(W, -1, (e >> 1).unsqueeze(-1)).squeeze(-1)
