@@ -15,11 +15,15 @@ softmax and accumulators), dropout 0.1 active.  One step = forward + losses + ba
 all-reduce over RCCL (N > 1) + fused Adam (lr 1e-3, weight decay 1e-4).  Synthetic seeded inputs
 with the feature statistics of SURVEY §8d, random-init weights (seed 1234); inputs resident in HBM.
 
-Prints ONE JSON line (rank 0).  The timed steps replay the step captured as a HIP graph
-(repurpose_amd/graph.py) at every N: under RCCL the bucketed gradient all-reduces are captured with
-the step (gloo rehearsals stay eager).  `roofline` is the dominant kernel's achieved MFMA rate
-measured with HIP events on its launch stream over eager steps of the same workload right after the
-timed region; `cpu_baseline` is the oracle (stock torch CPU modules, fp32, the reference's own
+Prints ONE JSON line (rank 0).  At N = 1 the timed steps replay the step captured as a HIP graph
+(repurpose_amd/graph.py); at N > 1 they run the eager DP step (the bucketed RCCL all-reduces issued
+from the backward, as DDP does) unless ``--graph on`` asks for the captured DP step (its all-reduces
+captured with the step: run on one rank only so far, so it stays opt-in).  ``ms_per_step`` is the MEAN
+over the K timed steps (one barrier-bracketed region: a replay loop cannot be split per step without
+syncs).  Every rank reports an exact checksum of its parameters after its last step
+(``param_checksums``): data parallelism must leave them identical.  `roofline` is the dominant
+kernel's achieved MFMA rate measured with HIP events on its launch stream over eager steps of the same
+workload right after the timed region; `cpu_baseline` is the oracle (stock torch CPU modules, fp32, the reference's own
 arithmetic) timed on this host.  At N = 1 the same run also reports `parity_mode` (the fp32 step,
 the reference's precision, as a graph replay) and `fresh_batch` (the trainer-shaped loop: a new
 pinned ragged batch per step through the device collate and CapturedTrainStep.load()).
@@ -197,7 +201,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="replay the step as a captured HIP graph (auto: on unless the collectives are gloo)")
+                    help="replay the step as a captured HIP graph (auto: at N = 1 only; on: also the DP step "
+                         "with its RCCL all-reduces captured)")
     ap.add_argument("--roofline-kernel", default="attn_bwd_dkdv", choices=list(KERNEL_FLOPS))
     args = ap.parse_args()
 
@@ -249,11 +254,14 @@ def main():
         return loss
 
     # the whole step is captured once as a HIP graph and replayed (repurpose_amd/graph.py; fresh
-    # dropout streams and the Adam step / LR per replay through a device parameter block); under RCCL
-    # the bucketed all-reduces issued from the backward are captured with it, so N ranks replay the
-    # same graph-mode step as one GPU.  A gloo rehearsal (CPU collectives) stays eager.
+    # dropout streams and the Adam step / LR per replay through a device parameter block).  The DP
+    # step (bucketed all-reduces issued from the backward) can be captured with its RCCL collectives
+    # (--graph on); by default N > 1 runs it eagerly, the path tested with two ranks.  A gloo
+    # rehearsal (CPU collectives) cannot be captured.
     capturable = not dp or reducer.backend == "nccl"
-    use_graph = args.graph == "on" or (args.graph == "auto" and capturable)
+    if args.graph == "on" and not capturable:
+        raise SystemExit("bench.py: --graph on needs RCCL collectives (backend nccl), not gloo")
+    use_graph = args.graph == "on" or (args.graph == "auto" and not dp)
     runner = None
     if use_graph:
         from repurpose_amd.graph import CapturedTrainStep
@@ -299,14 +307,21 @@ def main():
     if (world == 1 and not args.no_fresh_batch) or args.fresh_batch:
         fresh = fresh_batch_loop(runner, eager_step, batch, B, T, dev, rank, args.steps,
                                  world, dp)
+    # exact parameter checksum after this rank's last step (int64 sum of the fp32 words and an
+    # order-sensitive fold): data parallelism must leave every rank's parameters identical
+    csum = param_checksum(model)
+    checksums = [csum]
     if dp:
+        allc = [None] * ranks_seen
+        dist.all_gather_object(allc, csum)
+        checksums = allc
         dist.barrier()
 
     if rank == 0:
         fpt = flops_per_timestep(T)
         H, dk = 8, 64
         peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_FP32_TFLOPS
-        traffic = pmc_traffic()
+        traffic = pmc_traffic(B, T)
         roof = roofline_of(args.roofline_kernel, kern_ms, B, T, peak, traffic)
         roof["step_tflops"] = fpt * value / world / 1e12
         roof["step_frac"] = roof["step_tflops"] / peak
@@ -332,6 +347,8 @@ def main():
                           "model": "MMCTransformer (configs/Repurpose.yaml)", "global_batch": B * world,
                           "seq_len": T, "parallelism": f"dp{world}"},
                "loss": loss_val, "roofline": roof, "ranks_seen": ranks_seen,
+               "timing": "mean ms over the K timed steps (barrier + synchronize on both sides, max over ranks)",
+               "param_checksums": checksums,
                "rank_ms_per_step": [x / args.steps * 1e3 for x in per_rank],
                "rank_spread_ms": (max(per_rank) - min(per_rank)) / args.steps * 1e3,
                "execution": ("hip-graph replay of the captured step" + (" (RCCL all-reduces captured)" if dp else ""))
@@ -360,16 +377,33 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic():
-    """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    (scripts/pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE doubled per the gfx950 correction)."""
-    for name in ("r03_pmc_traffic.json", "r02_pmc_traffic.json"):
+PMC_TRAFFIC_FILES = ("r04_pmc_traffic.json", "r04_pmc_traffic_T4096_B1.json", "r04_pmc_traffic_T1024_B8.json")
+
+
+def pmc_traffic(B, T, files=PMC_TRAFFIC_FILES, root=None):
+    """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of THIS round's
+    kernels (scripts/pmc.sh + scripts/pmc_traffic.py; FETCH_SIZE doubled per the gfx950 correction),
+    keyed by the workload shape they were measured on: {} (traffic null) when no committed file
+    holds a measurement at (B, T)."""
+    for name in files:
         try:
-            with open(os.path.join(ROOT, "profiles", name)) as f:
-                return {k: v["hbm_bytes"] for k, v in json.load(f).items()}
-        except (OSError, ValueError, KeyError):
+            with open(os.path.join(root or os.path.join(ROOT, "profiles"), name)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
             continue
+        shape = d.get("shape") or {}
+        if shape.get("B") == B and shape.get("T") == T:
+            return {k: v["hbm_bytes"] for k, v in d.get("kernels", {}).items()}
     return {}
+
+
+def param_checksum(model):
+    """Exact checksum of the trained parameters: the int64 sum of their fp32 bit patterns and of the
+    bit patterns weighted by position mod 65521 (order-sensitive)."""
+    n = model.trainable_numel()
+    w = model.flat_params()[:n].detach().contiguous().view(torch.int32).to(torch.int64)
+    pos = torch.arange(n, device=w.device, dtype=torch.int64) % 65521
+    return [int(w.sum().item()), int((w * pos).sum().item())]
 
 
 def roofline_of(name, kern_ms, B, T, peak, traffic, H=8, dk=64):

@@ -302,9 +302,11 @@ extern "C" int rp_softnms(const float* scores, const float* segs, const int* cou
   if (cap <= NMS_LDS_CAP) {
     const size_t lds = (size_t)5 * (cap > 0 ? cap : 1) * sizeof(float);
     if (lds > 65536) {  // above 64 KiB of dynamic LDS (up to 120 KiB of the CU's 160): opt the kernel in
-      static const hipError_t opt = hipFuncSetAttribute((const void*)softnms_kernel<false>,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                        (int)(5 * NMS_LDS_CAP * sizeof(float)));
+      // the attribute is per device: set it on every such launch (cheap), not once per process, so a
+      // later launch on another device is opted in as well
+      const hipError_t opt = hipFuncSetAttribute((const void*)softnms_kernel<false>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)(5 * NMS_LDS_CAP * sizeof(float)));
       RP_REQUIRE(opt == hipSuccess, "rp_softnms: cannot enable %zu bytes of dynamic LDS: %s", lds,
                  hipGetErrorString(opt));
     }

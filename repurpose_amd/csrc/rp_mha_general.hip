@@ -156,9 +156,10 @@ extern "C" int rp_mha_general_bwd(const rp_mha_general_args* p, void* stream) {
   const int rc = gen_dev("rp_mha_general_bwd", p, true, a);
   if (rc) return rc;
   const int64_t rq = (int64_t)a.B * a.H * a.Tq, rk = (int64_t)a.B * a.H * a.Tk;
-  if (rq == 0) return RP_OK;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(gen_bwd_q_kernel, dim3((unsigned)((rq + GW - 1) / GW)), dim3(64 * GW), 0, s, a);
-  hipLaunchKernelGGL(gen_bwd_kv_kernel, dim3((unsigned)((rk + GW - 1) / GW)), dim3(64 * GW), 0, s, a);
+  if (rq > 0) hipLaunchKernelGGL(gen_bwd_q_kernel, dim3((unsigned)((rq + GW - 1) / GW)), dim3(64 * GW), 0, s, a);
+  // no queries (Tq = 0): the key-side kernel still runs and writes dK = dV = 0 (sums over no queries),
+  // as the reference's autograd gives; the caller's dk / dv are never left unwritten
+  if (rk > 0) hipLaunchKernelGGL(gen_bwd_kv_kernel, dim3((unsigned)((rk + GW - 1) / GW)), dim3(64 * GW), 0, s, a);
   return rp_check_launch("rp_mha_general_bwd");
 }

@@ -524,6 +524,8 @@ def mha_general_fwd(q, k, v, mask4, B, Tq, Tk, H, dk, scale):
             raise TypeError("mha_general: fp32 row views with unit column stride")
     out = torch.empty(B * Tq, H * dk, device=q.device, dtype=torch.float32)
     probs = torch.empty(B, H, Tq, Tk, device=q.device, dtype=torch.float32)
+    if B * Tq == 0:
+        return out, probs
     a = _general_args(q, k, v, mask4, B, Tq, Tk, H, dk, scale, probs)
     a.out, a.ldo = _p(out).value, out.stride(0)
     N.call("rp_mha_general_fwd", ctypes.byref(a), _stream(q))
@@ -535,6 +537,9 @@ def mha_general_bwd(q, k, v, dout, probs, mask4, B, Tq, Tk, H, dk, scale):
     _gpu(q, k, v, dout, probs, mask4)
     dev = q.device
     dq = torch.empty(B * Tq, H * dk, device=dev, dtype=torch.float32)
+    if B * Tq == 0:  # no queries: dK = dV = 0, as the reference's autograd gives (never uninitialised)
+        z = torch.zeros(B * Tk, H * dk, device=dev, dtype=torch.float32)
+        return dq, z, z.clone()
     dkk = torch.empty(B * Tk, H * dk, device=dev, dtype=torch.float32)
     dv = torch.empty(B * Tk, H * dk, device=dev, dtype=torch.float32)
     ds = torch.empty_like(probs)

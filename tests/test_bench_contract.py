@@ -71,3 +71,24 @@ def test_launcher_relays_only_the_result_line_and_the_exit_status(monkeypatch, t
     assert out.out.strip() == json.dumps({"metric": "m", "value": 1})
     assert "rank chatter" in out.err
     assert b.launch(2, ["3"]) == 3
+
+
+def test_traffic_is_keyed_by_the_measured_shape(tmp_path):
+    """roofline.traffic comes from a committed PMC file of the SAME (B, T) workload, else null."""
+    b = _bench()
+    (tmp_path / "a.json").write_text(json.dumps({"shape": {"B": 8, "T": 2048},
+                                                 "kernels": {"attn_bwd_dkdv": {"hbm_bytes": 123.0}}}))
+    (tmp_path / "b.json").write_text(json.dumps({"shape": {"B": 1, "T": 4096},
+                                                 "kernels": {"attn_bwd_dkdv": {"hbm_bytes": 45.0}}}))
+    assert b.pmc_traffic(8, 2048, files=("a.json", "b.json"), root=str(tmp_path)) == {"attn_bwd_dkdv": 123.0}
+    assert b.pmc_traffic(1, 4096, files=("a.json", "b.json"), root=str(tmp_path)) == {"attn_bwd_dkdv": 45.0}
+    assert b.pmc_traffic(8, 1024, files=("a.json", "b.json"), root=str(tmp_path)) == {}
+    assert b.roofline_of("attn_bwd_dkdv", {"attn_bwd_dkdv": 0.1}, 8, 1024, 2500.0, {})["traffic"] is None
+    # an old-format (shape-less) file never matches
+    (tmp_path / "c.json").write_text(json.dumps({"attn_bwd_dkdv": {"hbm_bytes": 1.0}}))
+    assert b.pmc_traffic(8, 2048, files=("c.json",), root=str(tmp_path)) == {}
+
+
+def test_committed_traffic_files_are_this_rounds():
+    """bench.py reads only r04 PMC files (the kernels changed in round 3 and 4)."""
+    assert all(n.startswith("r04_") for n in _bench().PMC_TRAFFIC_FILES)

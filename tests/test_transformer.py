@@ -4,6 +4,7 @@ import pytest
 import torch
 
 from oracle import transformer_oracle as O
+from repurpose_amd import kernels as K
 from repurpose_amd import transformer as R
 
 D, H, DFF = 128, 2, 256  # head dim 64, as the kernels implement
@@ -207,3 +208,19 @@ def test_batch_key_mask_broadcasts_like_the_reference(dev):
 def test_indivisible_model_width_is_refused():
     with pytest.raises(ValueError):
         R.MultiHeadAttention(250, 4)
+
+
+@pytest.mark.gpu
+def test_general_core_without_queries_gives_zero_key_value_gradients(dev):
+    """Tq = 0 on the general attention core (any d_k): dK = dV = 0 as the reference's autograd gives,
+    never uninitialised memory."""
+    B, Tk, H, dk = 2, 9, 2, 128
+    g = torch.Generator().manual_seed(6)
+    k = torch.randn(B * Tk, H * dk, generator=g).to(dev)
+    v = torch.randn(B * Tk, H * dk, generator=g).to(dev)
+    q = torch.empty(0, H * dk, device=dev)
+    out, probs = K.mha_general_fwd(q, k, v, None, B, 0, Tk, H, dk, 0.1)
+    assert out.shape[0] == 0
+    dq, dkk, dv = K.mha_general_bwd(q, k, v, torch.empty(0, H * dk, device=dev), probs, None, B, 0, Tk, H, dk, 0.1)
+    assert dq.shape[0] == 0
+    assert torch.equal(dkk, torch.zeros_like(dkk)) and torch.equal(dv, torch.zeros_like(dv))
