@@ -300,7 +300,7 @@ enum { RP_ATTN_Q_PRESCALED = 0x100 };
  * times per 64-key tile, tiles in order, each step giving the word x ^ c; in tile t word j (1..8th of the tile)
  * holds the keys 64t + 16*(j>>1) + 4g + 2*(j&1) + {0: low 16 bits, 1: high 16 bits}; a key is kept iff its 16 bits
  * read as int16 are >= round(p*65536) - 32768 (rp_hash: repurpose_amd/csrc/rp_common.h).
- * The forward writes the keep bits to `dropmask` (uint16 [B*H][ceil(T/64)][4][roundup(T,128)],
+ * The forward writes the keep bits to `dropmask` (uint16 [B*H][ceil(T/64)][4][roundup(T,256)],
  * bit (kt*4 + r) of word (bh, tile, g, q) = keep(q, 64*tile + 16*kt + 4*g + r);
  * rp_attn_dropmask_elems() words), the backward reads them back.  dropmask may be NULL when
  * p == 0. */
@@ -313,7 +313,7 @@ int64_t rp_attn_dropmask_elems(int B, int T, int H);
  * a sequence has no valid key at all).  out [B*Tq, ldo]; lse [B, H, Tq] fp32.  Backward: dout
  * [B*Tq, lddo]; dq [B*Tq, lddq], dk / dv [B*Tk, lddk / lddv] are fully overwritten; delta_ws
  * [3, B, H, Tq] fp32 (plane 0 = delta; see rp_attn_bwd).  Dropout keep bits (forward -> backward) as for rp_attn_fwd with T -> (Tq, Tk):
- * rp_mha_dropmask_elems(B, Tq, Tk, H) uint16 words [B*H][ceil(Tk/64)][4][roundup(Tq,128)].
+ * rp_mha_dropmask_elems(B, Tq, Tk, H) uint16 words [B*H][ceil(Tk/64)][4][roundup(Tq,256)].
  * Replaces models/transformer.py:37-81 MultiHeadAttention's score/softmax/PV core (self attention
  * of EncoderLayer :84-102, cross attention of CrossAttentionEncoderLayer :105-130 and
  * CrossSelfEncoderLayer :133-176). */

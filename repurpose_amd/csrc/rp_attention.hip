@@ -65,11 +65,11 @@ __device__ __forceinline__ int lds_off(int row, int byte) {
 }
 
 // keep-bit mask layout (the forward's register layout, so the forward and dQ kernels move one
-// 16-bit word per lane and key tile): [B*H][KT = ceil(T/64)][4 lane groups g][ldm = roundup(T,128)]
-// (a row covers every query of the last 128-query block, so block-wide stores and DMA pieces of a
-// row never reach the next one)
+// 16-bit word per lane and key tile): [B*H][KT = ceil(T/64)][4 lane groups g][ldm = roundup(T,256)]
+// (a row covers every query of the last 256-query block of the ping-pong forward, so block-wide
+// stores and DMA pieces of a row never reach the next one)
 // uint16; bit (kt*4 + r) of word (bh, tile, g, q) = keep(q, key = 64*tile + 16*kt + 4*g + r)
-__host__ __device__ inline int64_t mask_ld(int T) { return ((int64_t)T + 127) / 128 * 128; }
+__host__ __device__ inline int64_t mask_ld(int T) { return ((int64_t)T + 255) / 256 * 256; }
 __host__ __device__ inline int mask_kt(int T) { return (T + 63) / 64; }
 
 // ----- problem description (device side of rp_mha_args) ------------------------------------------
@@ -2515,6 +2515,731 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_dma_kernel(MhaDev a) {
   }
 }
 
+// =================================================================================================
+// 32x32x16 forward and dQ kernels (bf16, 128-query workgroups, LDS-DMA three-slot ring).
+//
+// The 16x16x32 kernels above spend half of every MFMA's 16 cycles holding the SIMD's vector issue
+// port (MI355X_MICROARCH.md: an MFMA holds vector issue for 8 of its cycles), and their tile loops are
+// vector-issue bound: forward p = 0.1 ~1,460 issue cycles per wave and 64-key tile against 576 MFMA
+// cycles.  v_mfma_f32_32x32x16_bf16 does the same work as two 16x16x32 MFMAs for one 8-cycle issue
+// slot, and with the QUERY on the MFMA column (S^T = K Q^T: lane (h = l / 32, c = l % 32) holds query c
+// and keys 4h + 8j + r, j, r = 0..3, of a 32-key tile) every per-query quantity is one value per lane:
+//  * the running maximum / lse / delta enter the S^T and dP^T products as the first MFMA's C operand, a
+//    16-register tile holding the lane's value (the forward rebuilds it only on a rescale; the dQ kernel
+//    builds its two once);
+//  * the row maximum is lane-local over the lane's 32 scores plus one permlane32 swap with its partner
+//    lane (only inside the rare rescale branch);
+//  * the accumulator rows ARE the next product's k slots: packed to bf16, registers 8s'..8s'+7 of a
+//    32-key tile are the B operand of k-step s' of O^T += V^T P^T (forward) / dQ^T += K^T dS^T (dQ), with
+//    the k order k = 8h + 4jj + r <-> key 16s' + 8jj + 4h + r; the A operand's transposed fragments
+//    (ds_read_b64_tr_b16, keys 4h..4h+3 and 8+4h..8+4h+3) follow the same order.
+// LDS image of a [64 rows][64] bf16 tile: 128-byte rows, 16-byte chunk c of row r stored at chunk
+// c ^ swz32(r), swz32(r) = ((r & 2) << 1) | ((r >> 3) & 3): conflict-free for both 32x32x16 operand
+// reads — ds_read_b128 row fragments (16 rows x one chunk per lane group) and ds_read_b64_tr_b16
+// column fragments (4 rows x 64 bytes per 32-lane half) — found by exhaustive search over XOR maps of
+// the row bits (the 16x16 swizzle lds_swz leaves the 32-row fragment 4-way conflicted).
+// Dropout: lane (h, c) runs the MWC streams of (query c, lane groups g = h and h + 2) — exactly the
+// streams and keep bits of the 16x16 forward (attn_fwd_kernel), so the stored mask layout and every
+// reader are unchanged; one stream word covers one packed bf16 P pair.
+// =================================================================================================
+__device__ __forceinline__ int swz32(int row) { return ((row & 2) << 1) | ((row >> 3) & 3); }
+__device__ __forceinline__ int off32(int row, int chunk) { return row * 128 + ((chunk ^ swz32(row)) << 4); }
+
+__device__ __forceinline__ f32x16 splat16(float v) {
+  f32x16 r;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) r[j] = v;
+  return r;
+}
+
+// 32x32x16 row fragment (A or B operand): lane (h, m) holds X[r0 + m][16 s + 8 h + 0..7]
+__device__ __forceinline__ bf16x8 row32_lds(const char* lds, int r0, int s, int lane) {
+  const int m = lane & 31, h = lane >> 5;
+  return *reinterpret_cast<const bf16x8*>(lds + off32(r0 + m, 2 * s + h));
+}
+// 32x32x16 transposed fragment of a [key][col] tile (A operand of O^T += V^T P^T, dQ^T += K^T dS^T):
+// lane (h, m) holds X[R + 4h + {0..3}][c0 + m] and X[R + 8 + 4h + {0..3}][c0 + m] (k = 8h + 4jj + r <->
+// row R + 8jj + 4h + r, the accumulator k order above).  Per 16-lane group one 4-row x 16-column
+// block: lane 4q + p supplies row q, columns 4p..4p+3.
+__device__ __forceinline__ bf16x8 col32_lds(const char* lds, int R, int c0, int lane) {
+  const int h = lane >> 5, gg = (lane >> 4) & 1, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = R + 4 * h + q;
+  const int byte = 2 * (c0 + 16 * gg + 4 * p);
+  const char* p0 = lds + off32(row, byte >> 4) + (byte & 15);
+  const char* p1 = lds + off32(row + 8, byte >> 4) + (byte & 15);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+// registers 8k..8k+7 of a 32x32 accumulator -> bf16x8 (the B operand of k-step k of the next product)
+__device__ __forceinline__ bf16x8 pack8_32(const f32x16& a, int k) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * k + j];
+  return r;
+}
+
+// rows [row0, row0 + 64) of a [rows][64] bf16 operand -> the swz32 image (LDS-DMA, two 1 KB pieces
+// per wave, clamped source rows); descriptor form as Rows64
+__device__ __forceinline__ void dma_rows64_s32(const bf16* __restrict__ base, int64_t ld, int row0, int nrows,
+                                               char* tile, int w, int lane) {
+  const uint32_t t = lds_addr(tile);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int I = w * 2 + j;
+    const int r = I * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz32(r);
+    int rr = row0 + r;
+    rr = rr < nrows ? rr : nrows - 1;
+    dma16(base + (int64_t)rr * ld + c * 8, t + I * 1024);
+  }
+}
+struct Rows64S32 {
+  rp_srd srd;
+  uint32_t vo0, vo1, rowbytes;
+  bool fast;
+  __device__ __forceinline__ void init(const bf16* b, int64_t ld_, int nrows, int w, int lane) {
+    srd = make_srd(b);
+    const int r0 = (w * 2) * 8 + (lane >> 3), r1 = r0 + 8;
+    const int c0 = (lane & 7) ^ swz32(r0), c1 = (lane & 7) ^ swz32(r1);
+    vo0 = (uint32_t)((r0 * ld_ + c0 * 8) * 2);
+    vo1 = (uint32_t)((r1 * ld_ + c1 * 8) * 2);
+    rowbytes = (uint32_t)(ld_ * 2);
+    fast = ((int64_t)nrows + 64) * ld_ * 2 < ((int64_t)1 << 31);
+  }
+};
+
+// ---- forward ----
+template <bool DROP>
+__global__ __launch_bounds__(NT, 2) void attn_fwd32_kernel(MhaDev a) {
+  constexpr int QB = NW * 32;  // 128 queries per workgroup, 32 per wave
+  constexpr int TILE = FW_KT * 128;
+  constexpr int BUF = 2 * TILE;
+  constexpr int NBUF = 3;
+  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
+  __shared__ __attribute__((aligned(16))) uint8_t kvl[FD_TKMAX];
+  __shared__ int kfull[FD_TKMAX / FW_KT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, c = lane & 31;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const uint32_t drop_thresh = a.drop_thresh;
+  const float drop_scale = a.drop_scale;
+  const float scale = a.scale;
+  const int nqb = (Tq + QB - 1) / QB;
+  const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
+  const int bh = L / nqb, qb = L % nqb;
+  const int b = bh / H, hh = bh % H;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv;
+  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + hh * HD;
+  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + hh * HD;
+  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + hh * HD;
+  const int q0 = qb * QB + w * 32;
+  const int q = q0 + c;
+  const uint32_t seed_bh = rp_hash(rp_seed_eff(a.seed_base, a.seed), (uint32_t)bh);
+  const float cq = scale * LOG2E;
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
+  uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
+  const bool novalid = seq_has_no_key(a, b, tid);
+
+  // Q'^T as the B operand of S^T = K Q'^T: k-step s holds Q'[q][16 s + 8 h + 0..7]
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (q < Tq && !novalid) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(Qg + (int64_t)q * ldq + 16 * s + 8 * h);
+      if (!a.qpre) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * cq);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)0.f;
+    }
+  }
+  const int nkt = (Tk + FW_KT - 1) / FW_KT;
+  for (int k = tid; k < nkt * FW_KT; k += NT)
+    kvl[k] = k < Tk ? (novalid || a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
+  __syncthreads();
+  for (int t = tid; t < nkt; t += NT) {
+    int ok = 1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t v = reinterpret_cast<const uint32_t*>(kvl)[t * 16 + j];
+      ok &= ((v - 0x01010101u) & ~v & 0x80808080u) == 0u;
+    }
+    kfull[t] = ok;
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]));
+  __syncthreads();
+
+  // O^T[d = 32 dt + 8 j + 4 h + r][q]; ls: every row = the running sum of P (before dropout) of query c
+  f32x16 o[2], ls;
+  o[0] = o[1] = ls = splat16(0.f);
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  float m = 0.f;          // reference max (log2 units) subtracted through the S^T start
+  bool mset = false;
+  float gthr = -INFINITY;  // the lane-local grow bound: -inf until the reference is set, then RESCALE_LOG2
+  f32x16 negm = splat16(0.f);
+  uint64_t st0 = 0, st1 = 0;  // MWC streams of (query, lane group h) and (query, lane group h + 2)
+  if constexpr (DROP) {
+    st0 = mwc_seed(rp_hash(seed_bh, (uint32_t)q * 4u + (uint32_t)h));
+    st1 = mwc_seed(rp_hash(seed_bh, (uint32_t)q * 4u + (uint32_t)(h + 2)));
+  }
+  const short ts = (short)((int)drop_thresh - 32768);
+  const i16x2 t2 = {ts, ts};
+
+  auto ring = [&](auto bi) -> char* {
+    constexpr int BI = decltype(bi)::value;
+    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
+  };
+  Rows64S32 rk, rv;
+  rk.init(Kg, ldk, Tk, w, lane);
+  rv.init(Vg, ldv, Tk, w, lane);
+  const bool xfast = rk.fast && rv.fast;
+  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
+  auto issue = [&](int it, auto bi) {
+    constexpr int BI = decltype(bi)::value;
+    const int k0 = it * FW_KT;
+    if (xfast && k0 + FW_KT <= Tk) {
+      const uint32_t pk = slot_lds[BI] + (uint32_t)(w * 2) * 1024u;
+      dma16b_x4(rk.srd, rk.vo0, rk.vo1, (uint32_t)k0 * rk.rowbytes, rv.srd, rv.vo0, rv.vo1,
+                (uint32_t)k0 * rv.rowbytes, pk);
+    } else {
+      char* buf = ring(bi);
+      dma_rows64_s32(Kg, ldk, k0, Tk, buf, w, lane);
+      dma_rows64_s32(Vg, ldv, k0, Tk, buf + TILE, w, lane);
+    }
+  };
+  // step it waits for DMA(it); issued after it: (it >= 2) the 2 keep-bit stores of step it - 2,
+  // DMA(it + 1) (4), the 2 stores of step it - 1 (it >= 1)
+  auto wait_tile = [&](int it) {
+    if (it + 1 >= nkt)
+      wait_vm<0>();
+    else if (!DROP || it == 0)
+      wait_vm<4>();
+    else if (it == 1)
+      wait_vm<6>();
+    else
+      wait_vm<8>();
+  };
+  issue(0, std::integral_constant<int, 0>());
+  if (nkt > 1) issue(1, std::integral_constant<int, 1>());
+
+  auto step = [&](auto bi, int kt_i) {
+    constexpr int BI = decltype(bi)::value;
+    wait_tile(kt_i);
+    raw_barrier();
+    if (kt_i + 2 < nkt) issue(kt_i + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    const char* Kl = ring(bi);
+    const char* Vl = Kl + TILE;
+    const bool full = kfull[kt_i] != 0;
+    // ---- S^T[key][q] = K Q'^T - m, two 32-key tiles ----
+    f32x16 s[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s[t] = mfma32(row32_lds(Kl, 32 * t, ks, lane), qf[ks], ks == 0 ? negm : s[t]);
+    if (!full) {  // key bias 0 / -inf: register 4 j + r of tile t is key 32 t + 8 j + 4 h + r
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t vb = *reinterpret_cast<const uint32_t*>(kvl + kt_i * FW_KT + 32 * t + 8 * j + 4 * h);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (((vb >> (8 * r)) & 0xFFu) == 0u) s[t][4 * j + r] = -INFINITY;
+        }
+    }
+    // ---- lane-local max against the reference; deferred rescale (attn_fwd_kernel) ----
+    float mx = s[0][0];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) mx = fmaxf(mx, s[t][v]);
+    if (__ballot(mx > gthr) != 0) {
+      // the query's row max: this lane's 32 keys and its partner lane's (l ^ 32)
+      auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      const float rel = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      const bool gq = mset ? rel > RESCALE_LOG2 : rel > -INFINITY;
+      const float alpha = gq ? (mset ? rp_exp2(-rel) : 0.f) : 1.f;
+      const float sub = gq ? rel : 0.f;
+      ls *= alpha;
+      o[0] *= alpha;
+      o[1] *= alpha;
+      m += sub;
+      mset = mset || gq;
+      gthr = mset ? RESCALE_LOG2 : -INFINITY;
+      negm = splat16(-m);
+      s[0] -= sub;
+      s[1] -= sub;
+    }
+    // ---- P = exp2(acc), packed: pf[2 t + s'] = registers 8 s'..8 s' + 7 of tile t ----
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) s[t][v] = rp_exp2(s[t][v]);
+    bf16x8 pf[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pf[k] = pack8_32(s[k >> 1], k & 1);
+    // row sums of P (before dropout) on the matrix core
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ls = mfma32(ones, pf[k], ls);
+    if constexpr (DROP) {
+      // stream words in order jw = 2 k + e (k = 2 t + s', e = 0, 1): stream 0 masks pair words e of
+      // pf[k] (register row j = 2 s'), stream 1 pair words 2 + e (j = 2 s' + 1); keep bit of the low /
+      // high half -> bit 4 k + 2 e / + 1 of the stream's 16-bit word (drop_masks)
+      uint32_t acc0 = 0u, acc1 = 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint4 u = __builtin_bit_cast(uint4, pf[k]);
+        uint32_t mk[4];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint32_t w0 = rp_mwc_next(st0), w1 = rp_mwc_next(st1);
+          const i16x2 d0 = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w0), t2);
+          const i16x2 d1 = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w1), t2);
+          mk[e] = __builtin_bit_cast(uint32_t, (i16x2)(d0 >> (short)15));
+          mk[2 + e] = __builtin_bit_cast(uint32_t, (i16x2)(d1 >> (short)15));
+          const int bb = 4 * k + 2 * e;
+          acc0 |= ~mk[e] & ((1u << bb) | (1u << (16 + bb + 1)));
+          acc1 |= ~mk[2 + e] & ((1u << bb) | (1u << (16 + bb + 1)));
+        }
+        u.x &= ~mk[0];
+        u.y &= ~mk[1];
+        u.z &= ~mk[2];
+        u.w &= ~mk[3];
+        pf[k] = __builtin_bit_cast(bf16x8, u);
+      }
+      uint16_t* mr = mrow + ((int64_t)kt_i * 4 + h) * ldm + q;
+      mr[0] = (uint16_t)((acc0 & 0xFFFFu) | (acc0 >> 16));
+      mr[2 * ldm] = (uint16_t)((acc1 & 0xFFFFu) | (acc1 >> 16));
+    }
+    // ---- O^T[d][q] += V^T P^T ----
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(col32_lds(Vl, 16 * k, 32 * dt, lane), pf[k], o[dt]);
+  };
+  for (int it = 0; it < nkt; it += NBUF) {
+    step(std::integral_constant<int, 0>(), it);
+    if (it + 1 < nkt) step(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < nkt) step(std::integral_constant<int, 2>(), it + 2);
+  }
+
+  // ---- epilogue: O[q][d] = O^T / l (16-byte stores after a permlane32 swap of register rows), lse ----
+  const float l = ls[0];
+  const float inv = drop_scale / l;
+  const int64_t ldo = a.ldo;
+  const bool qok = q < Tq;  // the same for both partner lanes of a query (the swaps below pair them)
+  bf16* orow = (bf16*)a.out + ((int64_t)b * Tq + q) * ldo + hh * HD;
+  bf16* lorow = a.out_lo ? (bf16*)a.out_lo + ((int64_t)b * Tq + q) * ldo + hh * HD : nullptr;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      // rows j = 2u (d 16u + 4h + r) and j = 2u + 1 (d 16u + 8 + 4h + r) of d tile dt
+      uint32_t A[2], Bv[2], Al[2], Bl[2];
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const float x0 = o[dt][8 * u + 2 * pr] * inv, x1 = o[dt][8 * u + 2 * pr + 1] * inv;
+        const float y0 = o[dt][8 * u + 4 + 2 * pr] * inv, y1 = o[dt][8 * u + 4 + 2 * pr + 1] * inv;
+        const bf16 bx0 = (bf16)x0, bx1 = (bf16)x1, by0 = (bf16)y0, by1 = (bf16)y1;
+        A[pr] = (uint32_t)__builtin_bit_cast(uint16_t, bx0) | ((uint32_t)__builtin_bit_cast(uint16_t, bx1) << 16);
+        Bv[pr] = (uint32_t)__builtin_bit_cast(uint16_t, by0) | ((uint32_t)__builtin_bit_cast(uint16_t, by1) << 16);
+        const bf16 lx0 = (bf16)(x0 - (float)bx0), lx1 = (bf16)(x1 - (float)bx1);
+        const bf16 ly0 = (bf16)(y0 - (float)by0), ly1 = (bf16)(y1 - (float)by1);
+        Al[pr] = (uint32_t)__builtin_bit_cast(uint16_t, lx0) | ((uint32_t)__builtin_bit_cast(uint16_t, lx1) << 16);
+        Bl[pr] = (uint32_t)__builtin_bit_cast(uint16_t, ly0) | ((uint32_t)__builtin_bit_cast(uint16_t, ly1) << 16);
+      }
+      // lanes 32..63 of A <-> lanes 0..31 of Bv: lane h = 0 then holds d 16u + 0..7, h = 1 d 16u + 8..15
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        auto r = __builtin_amdgcn_permlane32_swap(A[pr], Bv[pr], false, false);
+        A[pr] = r[0];
+        Bv[pr] = r[1];
+        auto rl = __builtin_amdgcn_permlane32_swap(Al[pr], Bl[pr], false, false);
+        Al[pr] = rl[0];
+        Bl[pr] = rl[1];
+      }
+      const int d0 = 32 * dt + 16 * u + 8 * h;
+      if (qok) {
+        *reinterpret_cast<uint4*>(orow + d0) = make_uint4(A[0], A[1], Bv[0], Bv[1]);
+        if (lorow) *reinterpret_cast<uint4*>(lorow + d0) = make_uint4(Al[0], Al[1], Bl[0], Bl[1]);
+      }
+    }
+  if (qok && h == 0) a.lse[(int64_t)bh * Tq + q] = m * 0.6931471805599453f + logf(l);
+}
+
+// =================================================================================================
+// forward, 8-wave ping-pong (bf16, 256 queries per workgroup, one workgroup per CU): the 32x32x16 data
+// flow of attn_fwd32_kernel with the two waves that share a SIMD (waves w and w + 4) offset by half a
+// key tile, so that on every SIMD one wave's MFMA segment runs beside its partner's softmax / dropout
+// VALU segment (MI355X_MICROARCH.md "Two waves per SIMD", cdna_hip_programming.md T15/T16):
+//   MFMA step t:    issue the LDS-DMA of key tile t + 2; O^T += V^T P^T of tile t - 1 (8 MFMAs);
+//                   S^T(t) = K Q'^T - m (8 MFMAs); wait for this wave's pieces of tile t + 1; barrier
+//   softmax step t: key mask, lane-local max / deferred rescale, P = exp2, pack to bf16, row sums on
+//                   the matrix core (4 MFMAs), dropout keep bits (mask + store); barrier
+// Waves 0..3 run MFMA step t while waves 4..7 run softmax step t - 1 and the reverse in the next
+// segment: waves 4..7 enter one barrier late (their first segment is idle) and waves 0..3 leave with
+// one barrier more, so every wave executes the same number of s_barrier.  Tile t is read by S(t)
+// (segments 2t / 2t + 1 for the two halves) and by P V(t) (segments 2t + 2 / 2t + 3): a four-slot ring,
+// the DMA of tile t + 2 issued at the start of MFMA step t (its slot's last reader, P V(t - 2) of waves
+// 4..7, ended with segment 2t - 1), landing before segment 2t + 4.  Each wave moves one 1 KB piece of K
+// and one of V per tile (16 KB per tile for 256 queries: half the LDS-DMA traffic per query of the
+// 128-query kernels).  Static priority for the younger half (waves 4..7: s_setprio 1 once, T5 static
+// form).  Keep bits, outputs and lse as attn_fwd32_kernel.
+// =================================================================================================
+constexpr int PP_NW = 8, PP_NT = PP_NW * 64, PP_QB = PP_NW * 32, PP_SLOT = 2 * FW_KT * 128;
+
+// two LDS-DMA pieces (one per descriptor) with m0 saved once
+__device__ __forceinline__ void dma16b_x2(const rp_srd& s0, uint32_t v0, uint32_t o0, uint32_t l0, const rp_srd& s1,
+                                          uint32_t v1, uint32_t o1, uint32_t l1) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %5, %7 offen lds\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %6, %8 offen lds\n\t"
+      "s_nop 0\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(l0), "s"(l1), "v"(v0), "v"(v1), "s"(s0), "s"(s1), "s"(o0), "s"(o1)
+      : "memory");
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
+  __shared__ __attribute__((aligned(1024))) char ring[4 * PP_SLOT];
+  __shared__ __attribute__((aligned(16))) uint8_t kvl[FD_TKMAX];
+  __shared__ int kfull[FD_TKMAX / FW_KT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // the younger wave of each SIMD pair runs half a tile behind its partner: pair by the SIMD each wave
+  // actually runs on (hardware register HW_ID, SIMD_ID bits) — dispatch order is not an architectural
+  // guarantee; any assignment stays correct (both roles execute the same barriers), only the overlap
+  // depends on it
+  __shared__ int simd_of[PP_NW];
+  {
+    uint32_t sid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID, 4, 2)" : "=s"(sid));
+    if (lane == 0) simd_of[w] = (int)sid;
+  }
+  __syncthreads();
+  bool young = false;
+  {
+    const int mine = __builtin_amdgcn_readfirstlane(simd_of[w]);
+#pragma unroll
+    for (int v = 0; v < PP_NW; ++v)
+      if (v < w && __builtin_amdgcn_readfirstlane(simd_of[v]) == mine) young = true;
+  }
+  const int h = lane >> 5, c = lane & 31;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const uint32_t drop_thresh = a.drop_thresh;
+  const float drop_scale = a.drop_scale;
+  const float scale = a.scale;
+  const int nqb = (Tq + PP_QB - 1) / PP_QB;
+  const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
+  const int bh = L / nqb, qb = L % nqb;
+  const int b = bh / H, hh = bh % H;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv;
+  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + hh * HD;
+  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + hh * HD;
+  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + hh * HD;
+  const int q = qb * PP_QB + w * 32 + c;
+  const uint32_t seed_bh = rp_hash(rp_seed_eff(a.seed_base, a.seed), (uint32_t)bh);
+  const float cq = scale * LOG2E;
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
+  uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
+  bool novalid;
+  {  // empty_uniform: does the sequence have no valid key?  (512 threads)
+    int any = 0;
+    if (a.empty_uniform)
+      for (int k = tid; k < Tk; k += PP_NT) any |= a.kvalid[(int64_t)b * Tk + k];
+    novalid = a.empty_uniform && __syncthreads_or(any) == 0;
+  }
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (q < Tq && !novalid) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(Qg + (int64_t)q * ldq + 16 * s + 8 * h);
+      if (!a.qpre) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * cq);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)0.f;
+    }
+  }
+  const int nkt = (Tk + FW_KT - 1) / FW_KT;
+  for (int k = tid; k < nkt * FW_KT; k += PP_NT)
+    kvl[k] = k < Tk ? (novalid || a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
+  __syncthreads();
+  // per-tile "no masked key" flags as one 64-bit scalar mask (nkt <= FD_TKMAX / 64 = 64): wave 0's lane t
+  // tests tile t, a ballot makes the mask, LDS hands it to the other waves
+  if (w == 0) {
+    int ok = 0;
+    if (lane < nkt) {
+      ok = 1;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t v = reinterpret_cast<const uint32_t*>(kvl)[lane * 16 + j];
+        ok &= ((v - 0x01010101u) & ~v & 0x80808080u) == 0u;
+      }
+    }
+    const uint64_t bal = __ballot(ok);
+    if (lane == 0) {
+      kfull[0] = (int)(uint32_t)bal;
+      kfull[1] = (int)(uint32_t)(bal >> 32);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]));
+  __syncthreads();
+  const uint64_t fullmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(kfull[1]) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane(kfull[0]);
+
+  f32x16 o[2], ls;
+  o[0] = o[1] = ls = splat16(0.f);
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  float m = 0.f;
+  bool mset = false;
+  float gthr = -INFINITY;
+  f32x16 negm = splat16(0.f);
+  uint64_t st0 = 0, st1 = 0;
+  if constexpr (DROP) {
+    st0 = mwc_seed(rp_hash(seed_bh, (uint32_t)q * 4u + (uint32_t)h));
+    st1 = mwc_seed(rp_hash(seed_bh, (uint32_t)q * 4u + (uint32_t)(h + 2)));
+  }
+  const short ts = (short)((int)drop_thresh - 32768);
+  const i16x2 t2 = {ts, ts};
+
+  // LDS-DMA: wave w moves rows 8w..8w+7 of the K tile and of the V tile (one 1 KB piece each)
+  const rp_srd srd_k = make_srd(Kg), srd_v = make_srd(Vg);
+  const int prow = 8 * w + (lane >> 3), pch = (lane & 7) ^ swz32(prow);
+  const uint32_t vo_k = (uint32_t)((prow * ldk + pch * 8) * 2), vo_v = (uint32_t)((prow * ldv + pch * 8) * 2);
+  const bool xfast = ((int64_t)Tk + 64) * ldk * 2 < ((int64_t)1 << 31) && ((int64_t)Tk + 64) * ldv * 2 < ((int64_t)1 << 31);
+  const uint32_t ring_lds = lds_addr(ring);
+  auto issue = [&](int it) {
+    const int k0 = it * FW_KT;
+    const uint32_t dst = ring_lds + (uint32_t)(it & 3) * PP_SLOT + (uint32_t)w * 1024u;
+    if (xfast && k0 + FW_KT <= Tk) {
+      dma16b_x2(srd_k, vo_k, (uint32_t)k0 * (uint32_t)(ldk * 2), dst, srd_v, vo_v, (uint32_t)k0 * (uint32_t)(ldv * 2),
+                dst + 8192u);
+    } else {  // partial tile: clamped source rows (their keys are masked through kvl)
+      int rr = k0 + prow;
+      rr = rr < Tk ? rr : Tk - 1;
+      dma16(Kg + (int64_t)rr * ldk + pch * 8, dst);
+      dma16(Vg + (int64_t)rr * ldv + pch * 8, dst + 8192u);
+    }
+  };
+  issue(0);
+  if (nkt > 1) issue(1);
+  if (nkt > 1) wait_vm<2>(); else wait_vm<0>();
+  raw_barrier();
+  if (young) {
+    __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (T5 static form)
+    raw_barrier();                  // the younger half starts one segment late
+  }
+
+  f32x16 s[2];
+  bf16x8 pf[4];
+  // operands in registers: vA = the V^T fragments of the next P V (read at the start of the softmax
+  // step, landing during its VALU), kA = the K fragments of S (read at the start of the MFMA step,
+  // landing under its P V MFMAs)
+  bf16x8 vA[8], kA[8];
+  auto mfma_step = [&](auto bi, int t) {
+    constexpr int SL = decltype(bi)::value;   // slot of tile t
+    if (t + 2 < nkt) issue(t + 2);
+    {
+      const char* Kl = ring + SL * PP_SLOT;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) kA[4 * tt + ks] = row32_lds(Kl, 32 * tt, ks, lane);
+    }
+    if (t > 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(vA[2 * k + dt], pf[k], o[dt]);
+    }
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s[tt] = mfma32(kA[4 * tt + ks], qf[ks], ks == 0 ? negm : s[tt]);
+    // this wave's pieces of tile t + 1 have landed (issued at MFMA step t - 1, or before the loop);
+    // issued after them: the keep-bit stores of softmax step t - 1 and the pieces of tile t + 2
+    if (t + 1 < nkt) {
+      const int n = (DROP && t > 0 ? 2 : 0) + (t + 2 < nkt ? 2 : 0);
+      if (n == 4)
+        wait_vm<4>();
+      else if (n == 2)
+        wait_vm<2>();
+      else
+        wait_vm<0>();
+    }
+    raw_barrier();
+  };
+  auto softmax_step = [&](auto bi, int t) {
+    constexpr int SL = decltype(bi)::value;
+    {  // V^T fragments of tile t for the P V of the next MFMA step
+      const char* Vl = ring + SL * PP_SLOT + 8192;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) vA[2 * k + dt] = col32_lds(Vl, 16 * k, 32 * dt, lane);
+    }
+    if (((fullmask >> t) & 1u) == 0) {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t vb = *reinterpret_cast<const uint32_t*>(kvl + t * FW_KT + 32 * tt + 8 * j + 4 * h);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (((vb >> (8 * r)) & 0xFFu) == 0u) s[tt][4 * j + r] = -INFINITY;
+        }
+    }
+    float mx = s[0][0];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) mx = fmaxf(mx, s[tt][v]);
+    if (__ballot(mx > gthr) != 0) {
+      auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      const float rel = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      const bool gq = mset ? rel > RESCALE_LOG2 : rel > -INFINITY;
+      const float alpha = gq ? (mset ? rp_exp2(-rel) : 0.f) : 1.f;
+      const float sub = gq ? rel : 0.f;
+      ls *= alpha;
+      o[0] *= alpha;
+      o[1] *= alpha;
+      m += sub;
+      mset = mset || gq;
+      gthr = mset ? RESCALE_LOG2 : -INFINITY;
+      negm = splat16(-m);
+      s[0] -= sub;
+      s[1] -= sub;
+    }
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) s[tt][v] = rp_exp2(s[tt][v]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pf[k] = pack8_32(s[k >> 1], k & 1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ls = mfma32(ones, pf[k], ls);
+    if constexpr (DROP) {
+      uint32_t acc0 = 0u, acc1 = 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint4 u = __builtin_bit_cast(uint4, pf[k]);
+        uint32_t mk[4];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint32_t w0 = rp_mwc_next(st0), w1 = rp_mwc_next(st1);
+          const i16x2 d0 = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w0), t2);
+          const i16x2 d1 = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w1), t2);
+          mk[e] = __builtin_bit_cast(uint32_t, (i16x2)(d0 >> (short)15));
+          mk[2 + e] = __builtin_bit_cast(uint32_t, (i16x2)(d1 >> (short)15));
+          const int bb = 4 * k + 2 * e;
+          acc0 |= ~mk[e] & ((1u << bb) | (1u << (16 + bb + 1)));
+          acc1 |= ~mk[2 + e] & ((1u << bb) | (1u << (16 + bb + 1)));
+        }
+        u.x &= ~mk[0];
+        u.y &= ~mk[1];
+        u.z &= ~mk[2];
+        u.w &= ~mk[3];
+        pf[k] = __builtin_bit_cast(bf16x8, u);
+      }
+      uint16_t* mr = mrow + ((int64_t)t * 4 + h) * ldm + q;
+      mr[0] = (uint16_t)((acc0 & 0xFFFFu) | (acc0 >> 16));
+      mr[2 * ldm] = (uint16_t)((acc1 & 0xFFFFu) | (acc1 >> 16));
+    }
+    raw_barrier();
+  };
+  for (int t = 0; t < nkt; t += 4) {
+    mfma_step(std::integral_constant<int, 0>(), t);
+    softmax_step(std::integral_constant<int, 0>(), t);
+    if (t + 1 < nkt) {
+      mfma_step(std::integral_constant<int, 1>(), t + 1);
+      softmax_step(std::integral_constant<int, 1>(), t + 1);
+    }
+    if (t + 2 < nkt) {
+      mfma_step(std::integral_constant<int, 2>(), t + 2);
+      softmax_step(std::integral_constant<int, 2>(), t + 2);
+    }
+    if (t + 3 < nkt) {
+      mfma_step(std::integral_constant<int, 3>(), t + 3);
+      softmax_step(std::integral_constant<int, 3>(), t + 3);
+    }
+  }
+  // the last P V (its V^T fragments were read by the last softmax step)
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(vA[2 * k + dt], pf[k], o[dt]);
+  if (!young) raw_barrier();  // the older half's extra barrier (matches the younger half's late start)
+
+  const float l = ls[0];
+  const float inv = drop_scale / l;
+  const int64_t ldo = a.ldo;
+  const bool qok = q < Tq;
+  bf16* orow = (bf16*)a.out + ((int64_t)b * Tq + q) * ldo + hh * HD;
+  bf16* lorow = a.out_lo ? (bf16*)a.out_lo + ((int64_t)b * Tq + q) * ldo + hh * HD : nullptr;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      uint32_t A[2], Bv[2], Al[2], Bl[2];
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const float x0 = o[dt][8 * u + 2 * pr] * inv, x1 = o[dt][8 * u + 2 * pr + 1] * inv;
+        const float y0 = o[dt][8 * u + 4 + 2 * pr] * inv, y1 = o[dt][8 * u + 4 + 2 * pr + 1] * inv;
+        const bf16 bx0 = (bf16)x0, bx1 = (bf16)x1, by0 = (bf16)y0, by1 = (bf16)y1;
+        A[pr] = (uint32_t)__builtin_bit_cast(uint16_t, bx0) | ((uint32_t)__builtin_bit_cast(uint16_t, bx1) << 16);
+        Bv[pr] = (uint32_t)__builtin_bit_cast(uint16_t, by0) | ((uint32_t)__builtin_bit_cast(uint16_t, by1) << 16);
+        const bf16 lx0 = (bf16)(x0 - (float)bx0), lx1 = (bf16)(x1 - (float)bx1);
+        const bf16 ly0 = (bf16)(y0 - (float)by0), ly1 = (bf16)(y1 - (float)by1);
+        Al[pr] = (uint32_t)__builtin_bit_cast(uint16_t, lx0) | ((uint32_t)__builtin_bit_cast(uint16_t, lx1) << 16);
+        Bl[pr] = (uint32_t)__builtin_bit_cast(uint16_t, ly0) | ((uint32_t)__builtin_bit_cast(uint16_t, ly1) << 16);
+      }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        auto r = __builtin_amdgcn_permlane32_swap(A[pr], Bv[pr], false, false);
+        A[pr] = r[0];
+        Bv[pr] = r[1];
+        auto rl = __builtin_amdgcn_permlane32_swap(Al[pr], Bl[pr], false, false);
+        Al[pr] = rl[0];
+        Bl[pr] = rl[1];
+      }
+      const int d0 = 32 * dt + 16 * u + 8 * h;
+      if (qok) {
+        *reinterpret_cast<uint4*>(orow + d0) = make_uint4(A[0], A[1], Bv[0], Bv[1]);
+        if (lorow) *reinterpret_cast<uint4*>(lorow + d0) = make_uint4(Al[0], Al[1], Bl[0], Bl[1]);
+      }
+    }
+  if (qok && h == 0) a.lse[(int64_t)bh * Tq + q] = m * 0.6931471805599453f + logf(l);
+}
+
 // 128-row blocks (the LDS-DMA kernels) from this many workgroups up; 64-row blocks below
 constexpr int64_t ATTN_SMALL_GRID = 256;
 
@@ -2586,6 +3311,18 @@ static bool attn_dma_f_enabled() {
   return v != 0 && attn_dma_enabled();
 }
 
+// RP_ATTN_FWD_PP=1 selects the 8-wave ping-pong forward (A/B; read per launch; off by default until it
+// beats the 16x16x32 kernel)
+static bool attn_fwd_pp_enabled() {
+  const char* e = getenv("RP_ATTN_FWD_PP");
+  return e && e[0] == '1';
+}
+// RP_ATTN_FWD32=1 selects the 4-wave 32x32x16 forward (A/B; read per launch; off by default)
+static bool attn_fwd32_enabled() {
+  const char* e = getenv("RP_ATTN_FWD32");
+  return e && e[0] == '1';
+}
+
 template <typename T>
 int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
   // 128-query blocks unless that leaves fewer than one workgroup per CU (256 CUs): then 64.  At one
@@ -2601,6 +3338,20 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
       hipLaunchKernelGGL((attn_fwd_kernel<T, true, 1>), grid, dim3(NT), 0, s, a);
     else
       hipLaunchKernelGGL((attn_fwd_kernel<T, false, 1>), grid, dim3(NT), 0, s, a);
+  } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX && attn_dma_f_enabled() && attn_fwd_pp_enabled() &&
+             (int64_t)((a.Tq + PP_QB - 1) / PP_QB) * a.B * a.H >= ATTN_SMALL_GRID) {
+    // the 8-wave ping-pong forward (256-query blocks) while its grid still fills every CU
+    const dim3 gpp((unsigned)((a.Tq + PP_QB - 1) / PP_QB * a.B * a.H));
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_fwd_pp_kernel<true>), gpp, dim3(PP_NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_pp_kernel<false>), gpp, dim3(PP_NT), 0, s, a);
+  } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX && attn_dma_f_enabled() && attn_fwd32_enabled()) {
+    // the 32x32x16 forward (query on the MFMA column)
+    if (a.drop_thresh)
+      hipLaunchKernelGGL((attn_fwd32_kernel<true>), grid, dim3(NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_fwd32_kernel<false>), grid, dim3(NT), 0, s, a);
   } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX && attn_dma_f_enabled()) {
     // RP_ATTN_FWD_LDS_PAD (bytes of unused dynamic LDS): tuning knob for the workgroups per CU
     // (53.8 KB static -> three per CU, a fourth of the metric grid then runs as a one-per-CU tail)

@@ -25,9 +25,13 @@ for s in $STEPS; do
     benchfull) step benchfull 500 python -u bench.py ;;
     gloo2)   RP_DIST_BACKEND=gloo step gloo2 400 python -u bench.py --gpus 2 --steps 3 --warmup 1 ;;
     dp1)     RP_BENCH_DP=1 step dp1 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
-               --master-addr 127.0.0.1 --master-port 29533 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+               --master-addr 127.0.0.1 --master-port 29533 bench.py --steps 10 --warmup 3 --no-cpu-baseline --graph on ;;
     dp1eager) RP_BENCH_DP=1 step dp1eager 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                --master-addr 127.0.0.1 --master-port 29534 bench.py --steps 10 --warmup 3 --no-cpu-baseline --graph off ;;
+    dptests) step dptests 900 $PYT --timeout 450 tests/test_dp_gpu.py ;;
+    cfg2)    step cfg2 700 $PYT --timeout 650 tests/test_configs_gpu.py -k config2 ;;
+    tq0)     step tq0 300 $PYT tests/test_transformer.py -k "without_queries or parity" ;;
+    prof)    step prof 450 bash scripts/prof.sh ${TAG}_prof ;;
     b1)      step b1 400 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-parity-mode --no-fresh-batch ;;
   esac
 done

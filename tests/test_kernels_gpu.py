@@ -254,7 +254,7 @@ def test_attention_fwd_bwd(dev, dtype, T, p):
     ftol = 2e-5 if dtype == torch.float32 else 2e-2
     close(o, ref.detach(), atol=ftol, rtol=ftol, what="attn fwd")
     if p > 0:  # the stored keep bits are exactly the restated ones
-        KT, ldm = (T + 63) // 64, (T + 127) // 128 * 128
+        KT, ldm = (T + 63) // 64, (T + 255) // 256 * 256
         words = mask.view(B * H, KT, 4, ldm)[..., :T].to(torch.int64) & 0xFFFF  # [bh, tile, g, q]
         bits = (words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1       # [bh, tile, g, q, kt*4+r]
         bits = bits.view(B * H, KT, 4, T, 4, 4)                                  # [bh, tile, g, q, kt, r]
@@ -343,7 +343,7 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
     close(o, ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd (128 blocks)")
     # hi + lo carries the output to ~2^-17
     close(o.double() + olo.double(), ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd hi+lo")
-    KT, ldm = (T + 63) // 64, (T + 127) // 128 * 128
+    KT, ldm = (T + 63) // 64, (T + 255) // 256 * 256
     words = mask.view(B * H, KT, 4, ldm)[..., :T].to(torch.int64) & 0xFFFF
     bits = ((words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1).view(B * H, KT, 4, T, 4, 4)
     got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, T, KT * 64)[:, :, :T].bool()
