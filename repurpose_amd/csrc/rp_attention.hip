@@ -2880,6 +2880,241 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd32_kernel(MhaDev a) {
   if (qok && h == 0) a.lse[(int64_t)bh * Tq + q] = m * 0.6931471805599453f + logf(l);
 }
 
+// ---- backward dQ (+ delta), 32x32x16 (bf16, 128-query workgroups, LDS-DMA ring) ----
+// The data flow of attn_bwd_q_dma_kernel on 32x32x16 MFMAs with the query on the MFMA column (see the
+// forward above): S^T = K Q'^T - lse and dP^T = V dO^T - delta/ds start from two 16-register C tiles
+// built once per kernel (every register of a lane holds its query's constant); dS^T = P^T * ds *
+// (keep ? dP^T : -delta/ds); dQ^T += K^T dS^T with the packed dS^T as the B operand and the K^T
+// fragments through ds_read_b64_tr_b16 (the k order of the accumulator rows).  The keep bits of lane
+// (h, c) are the words (g = h, query c) and (g = h + 2, query c) of the tile: register 4 j + r of
+// 32-key tile t reads bit (2 t + (j >> 1)) * 4 + r of word g = h + 2 (j & 1) — compile-time positions.
+template <bool DROP>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_q32_kernel(MhaDev a) {
+  constexpr int QB = NW * 32;            // 128 queries per workgroup
+  constexpr int TILE = FW_KT * 128;      // one 64-key K or V image (8 KB)
+  constexpr int MASKB = 1024;            // keep bits of the tile: 4 lane groups x 128 queries x u16
+  constexpr int BUF = 2 * TILE + MASKB;
+  constexpr int NBUF = 3;
+  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
+  __shared__ __attribute__((aligned(16))) uint8_t kvl[QD_TKMAX];
+  __shared__ int kfull[QD_TKMAX / FW_KT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, c = lane & 31;
+  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
+  const float scale = a.scale, drop_scale = a.drop_scale;
+  const float* __restrict__ lse = a.lse;
+  const int nqb = (Tq + QB - 1) / QB;
+  const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
+  const int bh = L / nqb, qb = L % nqb;
+  const int b = bh / H, hh = bh % H;
+  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
+  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + hh * HD;
+  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + hh * HD;
+  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + hh * HD;
+  const bf16* dOg = (const bf16*)a.dout + (int64_t)b * Tq * lddo + hh * HD;
+  const int q = qb * QB + w * 32 + c;
+  const bool qok = q < Tq;
+  const float cq = scale * LOG2E;
+  const int KT = mask_kt(Tk);
+  const int64_t ldm = mask_ld(Tq);
+  const uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
+
+  // ---- prologue: Q', dO as B operands (k-step s: columns 16 s + 8 h + 0..7), lse, delta ----
+  bf16x8 qf[4], df[4];
+  float part = 0.f;
+  {
+    const bf16* orow = (const bf16*)a.out + ((int64_t)b * Tq + q) * a.ldo + hh * HD;
+    const bf16* lrow = a.out_lo ? (const bf16*)a.out_lo + ((int64_t)b * Tq + q) * a.ldo + hh * HD : nullptr;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int col = 16 * s + 8 * h;
+      if (qok) {
+        qf[s] = *reinterpret_cast<const bf16x8*>(Qg + (int64_t)q * ldq + col);
+        df[s] = *reinterpret_cast<const bf16x8*>(dOg + (int64_t)q * lddo + col);
+        const bf16x8 of = *reinterpret_cast<const bf16x8*>(orow + col);
+        if (lrow) {  // O = hi + lo: delta from the unrounded output
+          const bf16x8 ol = *reinterpret_cast<const bf16x8*>(lrow + col);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) part += (float)df[s][j] * ((float)of[j] + (float)ol[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) part += (float)df[s][j] * (float)of[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[s][j] = df[s][j] = (bf16)0.f;
+      }
+    }
+  }
+  // the query's other 32 dims live in the partner lane l ^ 32
+  auto psw = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
+  const float dl = __uint_as_float(psw[0]) + __uint_as_float(psw[1]);
+  const float lq = qok ? lse[(int64_t)bh * Tq + q] * LOG2E - (DROP ? log2f(drop_scale) : 0.f) : INFINITY;
+  const float dq = qok ? -dl * (DROP ? 1.f / drop_scale : 1.f) : 0.f;
+  if (h == 0 && qok) {  // delta and the dK/dV kernel's row constants (planes 1, 2)
+    const int64_t plane = (int64_t)B * H * Tq;
+    a.delta[(int64_t)bh * Tq + q] = dl;
+    a.delta[plane + (int64_t)bh * Tq + q] = dq;
+    a.delta[2 * plane + (int64_t)bh * Tq + q] = -lq;
+  }
+  if (seq_has_no_key(a, b, tid)) {  // empty_uniform: dQ = 0 (delta above is still written)
+    bf16* dQz = (bf16*)a.dq + ((int64_t)b * Tq + q) * a.lddq + hh * HD;
+    if (qok)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(dQz + 16 * u + 8 * h) = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
+  if (!a.qpre) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * cq);
+  }
+  const int nkt = (Tk + FW_KT - 1) / FW_KT;
+  for (int k = tid; k < nkt * FW_KT; k += NT) kvl[k] = k < Tk ? (a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
+  __syncthreads();
+  for (int t = tid; t < nkt; t += NT) {
+    int ok = 1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t v = reinterpret_cast<const uint32_t*>(kvl)[t * 16 + j];
+      ok &= ((v - 0x01010101u) & ~v & 0x80808080u) == 0u;
+    }
+    kfull[t] = ok;
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]), "v"(df[s]));
+  __syncthreads();
+
+  const f32x16 nls = splat16(-lq), ndq = splat16(dq);
+  f32x16 dqa[2];
+  dqa[0] = dqa[1] = splat16(0.f);
+
+  auto ring = [&](auto bi) -> char* {
+    constexpr int BI = decltype(bi)::value;
+    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
+  };
+  Rows64S32 rk, rv;
+  rk.init(Kg, ldk, Tk, w, lane);
+  rv.init(Vg, ldv, Tk, w, lane);
+  // keep bits (wave 1): lane (g, cc) reads words [tile][g][this block's 128 queries], column chunk cc
+  const rp_srd srd_m = make_srd(mrow);
+  int64_t mcol = (int64_t)qb * QB + (lane & 15) * 8;
+  mcol = mcol < ldm - 8 ? mcol : ldm - 8;
+  const uint32_t vo_m = (uint32_t)((((int64_t)(lane >> 4)) * ldm + mcol) * 2);
+  const bool xfast = (int64_t)KT * 4 * ldm * 2 < ((int64_t)1 << 31) && rk.fast && rv.fast;
+  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
+  auto issue = [&](int it, auto bi) {
+    constexpr int BI = decltype(bi)::value;
+    char* buf = ring(bi);
+    const int k0 = it * FW_KT;
+    if (xfast && k0 + FW_KT <= Tk) {
+      const uint32_t t = slot_lds[BI];
+      const uint32_t pk = t + (uint32_t)(w * 2) * 1024u;
+      dma16b_x4(rk.srd, rk.vo0, rk.vo1, (uint32_t)k0 * rk.rowbytes, rv.srd, rv.vo0, rv.vo1,
+                (uint32_t)k0 * rv.rowbytes, pk);
+      if (DROP && w == 1) dma16b(srd_m, vo_m, (uint32_t)it * 8u * (uint32_t)ldm, t + 2 * TILE);
+    } else {
+      dma_rows64_s32(Kg, ldk, k0, Tk, buf, w, lane);
+      dma_rows64_s32(Vg, ldv, k0, Tk, buf + TILE, w, lane);
+      if (DROP && w == 1) dma16(mrow + ((int64_t)it * 4 + (lane >> 4)) * ldm + mcol, lds_addr(buf + 2 * TILE));
+    }
+  };
+  auto wait_tile = [&](bool next) {
+    if (!next)
+      wait_vm<0>();
+    else if (DROP && w == 1)
+      wait_vm<5>();
+    else
+      wait_vm<4>();
+  };
+  issue(0, std::integral_constant<int, 0>());
+  if (nkt > 1) issue(1, std::integral_constant<int, 1>());
+
+  auto step = [&](auto bi, int it) {
+    constexpr int BI = decltype(bi)::value;
+    wait_tile(it + 1 < nkt);
+    raw_barrier();
+    if (it + 2 < nkt) issue(it + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    const char* Kl = ring(bi);
+    const char* Vl = Kl + TILE;
+    uint32_t kw0 = 0u, kw1 = 0u;
+    if constexpr (DROP) {
+      const uint16_t* mw = reinterpret_cast<const uint16_t*>(Kl + 2 * TILE);
+      kw0 = mw[h * QB + w * 32 + c];
+      kw1 = mw[(h + 2) * QB + w * 32 + c];
+    }
+    const bool full = kfull[it] != 0;
+    // one 32-key half at a time (halves the live S / dP accumulators)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 s, dp;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma32(row32_lds(Kl, 32 * t, ks, lane), qf[ks], ks == 0 ? nls : s);
+        dp = mfma32(row32_lds(Vl, 32 * t, ks, lane), df[ks], ks == 0 ? ndq : dp);
+      }
+      if (!full) {  // masked keys: P = 0
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t vb = *reinterpret_cast<const uint32_t*>(kvl + it * FW_KT + 32 * t + 8 * j + 4 * h);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (((vb >> (8 * r)) & 0xFFu) == 0u) s[4 * j + r] = -INFINITY;
+        }
+      }
+      // dS^T = P^T * ds * (keep ? acc : -delta/ds)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const float p = rp_exp2(s[v]);
+        if constexpr (DROP) {
+          const int j = v >> 2, r = v & 3;
+          const uint32_t km = keep_mask((j & 1) ? kw1 : kw0, (2 * t + (j >> 1)) * 4 + r);
+          s[v] = p * bfi_select(km, dp[v], dq);
+        } else {
+          s[v] = p * dp[v];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 sf = pack8_32(s, kk);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) dqa[dt] = mfma32(col32_lds(Kl, 32 * t + 16 * kk, 32 * dt, lane), sf, dqa[dt]);
+      }
+    }
+  };
+  for (int it = 0; it < nkt; it += NBUF) {
+    step(std::integral_constant<int, 0>(), it);
+    if (it + 1 < nkt) step(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < nkt) step(std::integral_constant<int, 2>(), it + 2);
+  }
+  // store dQ[q][d] = scale * dQ^T (16-byte stores after a permlane32 swap, as the forward's O)
+  bf16* dQ = (bf16*)a.dq + ((int64_t)b * Tq + q) * a.lddq + hh * HD;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      uint32_t A[2], Bv[2];
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const bf16 x0 = (bf16)(dqa[dt][8 * u + 2 * pr] * scale), x1 = (bf16)(dqa[dt][8 * u + 2 * pr + 1] * scale);
+        const bf16 y0 = (bf16)(dqa[dt][8 * u + 4 + 2 * pr] * scale), y1 = (bf16)(dqa[dt][8 * u + 4 + 2 * pr + 1] * scale);
+        A[pr] = (uint32_t)__builtin_bit_cast(uint16_t, x0) | ((uint32_t)__builtin_bit_cast(uint16_t, x1) << 16);
+        Bv[pr] = (uint32_t)__builtin_bit_cast(uint16_t, y0) | ((uint32_t)__builtin_bit_cast(uint16_t, y1) << 16);
+      }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        auto r = __builtin_amdgcn_permlane32_swap(A[pr], Bv[pr], false, false);
+        A[pr] = r[0];
+        Bv[pr] = r[1];
+      }
+      if (qok) *reinterpret_cast<uint4*>(dQ + 32 * dt + 16 * u + 8 * h) = make_uint4(A[0], A[1], Bv[0], Bv[1]);
+    }
+}
+
 // =================================================================================================
 // forward, 8-wave ping-pong (bf16, 256 queries per workgroup, one workgroup per CU): the 32x32x16 data
 // flow of attn_fwd32_kernel with the two waves that share a SIMD (waves w and w + 4) offset by half a
@@ -2920,7 +3155,7 @@ __device__ __forceinline__ void dma16b_x2(const rp_srd& s0, uint32_t v0, uint32_
       : "memory");
 }
 
-template <bool DROP>
+template <bool DROP, bool LOCK>
 __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
   __shared__ __attribute__((aligned(1024))) char ring[4 * PP_SLOT];
   __shared__ __attribute__((aligned(16))) uint8_t kvl[FD_TKMAX];
@@ -3054,11 +3289,25 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
   if (nkt > 1) issue(1);
   if (nkt > 1) wait_vm<2>(); else wait_vm<0>();
   raw_barrier();
-  if (young) {
+  if (young && !LOCK) {  // (LOCK: diagnostic variant without the offset — both halves in step)
     __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (T5 static form)
     raw_barrier();                  // the younger half starts one segment late
   }
 
+  // -DRP_PP_STAMPS diagnostic build only (never the shipped library): s_memtime after every barrier of
+  // workgroup 0, written over the lse output ([wave][64 stamps] uint64)
+#ifdef RP_PP_STAMPS
+  int nst = 0;
+  uint64_t* stamps = reinterpret_cast<uint64_t*>(a.lse) + (int64_t)w * 64;
+  auto stamp = [&]() {
+    const uint64_t tt = __builtin_amdgcn_s_memtime();
+    if (blockIdx.x == 0 && lane == 0 && nst < 64) stamps[nst] = tt;
+    ++nst;
+  };
+#else
+  auto stamp = [&]() {};
+#endif
+  stamp();
   f32x16 s[2];
   bf16x8 pf[4];
   // operands in registers: vA = the V^T fragments of the next P V (read at the start of the softmax
@@ -3085,6 +3334,7 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) s[tt] = mfma32(kA[4 * tt + ks], qf[ks], ks == 0 ? negm : s[tt]);
+    stamp();
     // this wave's pieces of tile t + 1 have landed (issued at MFMA step t - 1, or before the loop);
     // issued after them: the keep-bit stores of softmax step t - 1 and the pieces of tile t + 2
     if (t + 1 < nkt) {
@@ -3097,6 +3347,7 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
         wait_vm<0>();
     }
     raw_barrier();
+    stamp();
   };
   auto softmax_step = [&](auto bi, int t) {
     constexpr int SL = decltype(bi)::value;
@@ -3174,7 +3425,9 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
       mr[0] = (uint16_t)((acc0 & 0xFFFFu) | (acc0 >> 16));
       mr[2 * ldm] = (uint16_t)((acc1 & 0xFFFFu) | (acc1 >> 16));
     }
+    stamp();
     raw_barrier();
+    stamp();
   };
   for (int t = 0; t < nkt; t += 4) {
     mfma_step(std::integral_constant<int, 0>(), t);
@@ -3197,7 +3450,7 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
   for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(vA[2 * k + dt], pf[k], o[dt]);
-  if (!young) raw_barrier();  // the older half's extra barrier (matches the younger half's late start)
+  if (!young && !LOCK) raw_barrier();  // the older half's extra barrier (matches the younger half's late start)
 
   const float l = ls[0];
   const float inv = drop_scale / l;
@@ -3237,7 +3490,9 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
         if (lorow) *reinterpret_cast<uint4*>(lorow + d0) = make_uint4(Al[0], Al[1], Bl[0], Bl[1]);
       }
     }
+#ifndef RP_PP_STAMPS
   if (qok && h == 0) a.lse[(int64_t)bh * Tq + q] = m * 0.6931471805599453f + logf(l);
+#endif
 }
 
 // 128-row blocks (the LDS-DMA kernels) from this many workgroups up; 64-row blocks below
@@ -3342,10 +3597,17 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
              (int64_t)((a.Tq + PP_QB - 1) / PP_QB) * a.B * a.H >= ATTN_SMALL_GRID) {
     // the 8-wave ping-pong forward (256-query blocks) while its grid still fills every CU
     const dim3 gpp((unsigned)((a.Tq + PP_QB - 1) / PP_QB * a.B * a.H));
-    if (a.drop_thresh)
-      hipLaunchKernelGGL((attn_fwd_pp_kernel<true>), gpp, dim3(PP_NT), 0, s, a);
-    else
-      hipLaunchKernelGGL((attn_fwd_pp_kernel<false>), gpp, dim3(PP_NT), 0, s, a);
+    const char* lk = getenv("RP_ATTN_PP_LOCK");  // diagnostic: both wave halves in step
+    if (lk && lk[0] == '1') {
+      if (a.drop_thresh)
+        hipLaunchKernelGGL((attn_fwd_pp_kernel<true, true>), gpp, dim3(PP_NT), 0, s, a);
+      else
+        hipLaunchKernelGGL((attn_fwd_pp_kernel<false, true>), gpp, dim3(PP_NT), 0, s, a);
+    } else if (a.drop_thresh) {
+      hipLaunchKernelGGL((attn_fwd_pp_kernel<true, false>), gpp, dim3(PP_NT), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((attn_fwd_pp_kernel<false, false>), gpp, dim3(PP_NT), 0, s, a);
+    }
   } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX && attn_dma_f_enabled() && attn_fwd32_enabled()) {
     // the 32x32x16 forward (query on the MFMA column)
     if (a.drop_thresh)
@@ -3387,6 +3649,12 @@ void launch_bwd_q(bool delta, const MhaDev& a, hipStream_t s) {
   }
 }
 
+// RP_ATTN_DQ32=1 selects the 32x32x16 dQ kernel (A/B; read per launch)
+static bool attn_dq32_enabled() {
+  const char* e = getenv("RP_ATTN_DQ32");
+  return e && e[0] == '1';
+}
+
 template <typename T>
 int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   const int64_t rows = (int64_t)a.B * a.Tq;
@@ -3398,6 +3666,13 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   if (fused) {
     if (small) {
       launch_bwd_q<T, 1>(true, a, s);
+    } else if (std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX && attn_dma_q_enabled() && attn_dq32_enabled()) {
+      // bf16, 128-query blocks: the 32x32x16 dQ kernel
+      const dim3 grid((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
+      if (a.drop_thresh)
+        hipLaunchKernelGGL((attn_bwd_q32_kernel<true>), grid, dim3(NT), 0, s, a);
+      else
+        hipLaunchKernelGGL((attn_bwd_q32_kernel<false>), grid, dim3(NT), 0, s, a);
     } else if (std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX && attn_dma_q_enabled()) {
       // bf16, 128-query blocks: the LDS-DMA staged dQ kernel (RP_ATTN_DMA=0: register staged)
       const dim3 grid((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
