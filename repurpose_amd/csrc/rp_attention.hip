@@ -1178,8 +1178,12 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
   uint32_t vo_x = (uint32_t)(lane & 15) * 16u;
   const uint32_t bpr_x = xmask ? 2u : 4u;  // source bytes per query row
   const uint32_t xo = (uint32_t)(2 * TILE + XR * (w == 1 ? 0 : (w == 2 ? 1 : (xmask ? 2 : 3))));
+  // keep-bit region: LDS row r (= tile half * 4 + lane group) holds 64 queries' words; its 16-byte chunks
+  // are XOR-swizzled by mswz(r) = (r >> 1) & 1 so that the readers' rows r and r + 2 (128 bytes x 2 =
+  // the same banks) land 16 bytes apart: the dropout path's ds_read_b64 of the bits is conflict-free
+  // (it was 2-way: 6.3 M conflict cycles per launch at p = 0.1, 0 at p = 0)
   if (xmask) {
-    const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
+    const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = (lane & 7) ^ ((lane >> 4) & 1);
     int tile = kb * (KB / 64) + (r >> 2);
     tile = tile < KT ? tile : KT - 1;  // keys past Tk: their dK / dV rows are written as zeros
     // KB = 64: lanes 32..63 repeat lanes 0..31's words into the unused second half of the region
@@ -1203,7 +1207,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
       dma_rows64(dOg, lddo, qs0, Tq, buf + TILE, w, lane);
       const int q = qs0 + lane;
       if (xmask) {
-        const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
+        const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = (lane & 7) ^ ((lane >> 4) & 1);
         int tile = kb * (KB / 64) + (r >> 2);
         tile = tile < KT ? tile : KT - 1;
         dma16(dmask + (((int64_t)bh * KT + tile) * 4 + (r & 3)) * ldm + qs0 + cch * 8, lds_addr(buf + xo));
@@ -1275,7 +1279,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
           const int mrow_l = (kw >> 6) * 4 + ((ko & 15) >> 2);
           const int bit = (ko >> 4) * 4 + (ko & 3);
           uint2 bits = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-          if constexpr (DROP) bits = *reinterpret_cast<const uint2*>(mw + mrow_l * KV_QT + qrow);
+          if constexpr (DROP)
+            bits = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(mw) + mrow_l * (KV_QT * 2) +
+                                                   ((((qrow >> 3) ^ ((mrow_l >> 1) & 1)) << 4) | ((qrow & 7) << 1)));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float pr = rp_exp2(s[qq][kt][r]);  // with dropout: p * ds
@@ -2582,6 +2588,18 @@ __device__ __forceinline__ bf16x8 pack8_32(const f32x16& a, int k) {
   return r;
 }
 
+// lane-local maximum of two 32x32 accumulators as a v_max3 tree (depth 4 instead of a 16-long chain)
+__device__ __forceinline__ float max32x2(const f32x16& x, const f32x16& y) {
+  float l1[11];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) l1[i] = fmaxf(fmaxf(x[3 * i], x[3 * i + 1]), x[3 * i + 2]);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) l1[5 + i] = fmaxf(fmaxf(y[3 * i], y[3 * i + 1]), y[3 * i + 2]);
+  l1[10] = fmaxf(x[15], y[15]);
+  const float a0 = fmaxf(fmaxf(l1[0], l1[1]), l1[2]), a1 = fmaxf(fmaxf(l1[3], l1[4]), l1[5]);
+  const float a2 = fmaxf(fmaxf(l1[6], l1[7]), l1[8]), a3 = fmaxf(l1[9], l1[10]);
+  return fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
+}
 // rows [row0, row0 + 64) of a [rows][64] bf16 operand -> the swz32 image (LDS-DMA, two 1 KB pieces
 // per wave, clamped source rows); descriptor form as Rows64
 __device__ __forceinline__ void dma_rows64_s32(const bf16* __restrict__ base, int64_t ld, int row0, int nrows,
@@ -2761,11 +2779,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd32_kernel(MhaDev a) {
         }
     }
     // ---- lane-local max against the reference; deferred rescale (attn_fwd_kernel) ----
-    float mx = s[0][0];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) mx = fmaxf(mx, s[t][v]);
+    const float mx = max32x2(s[0], s[1]);
     if (__ballot(mx > gthr) != 0) {
       // the query's row max: this lane's 32 keys and its partner lane's (l ^ 32)
       auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
@@ -3249,11 +3263,13 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
   const uint64_t fullmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(kfull[1]) << 32) |
                             (uint32_t)__builtin_amdgcn_readfirstlane(kfull[0]);
 
-  f32x16 o[2], ls;
-  o[0] = o[1] = ls = splat16(0.f);
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  // row sums of P (before dropout) on the VALU, per lane over its 32 keys of each tile (the partner lane
+  // l ^ 32 holds the query's other 32): an MFMA in the softmax segment would queue behind the partner
+  // wave's MFMA segment on the shared matrix pipe (measured: the softmax segment stretched to ~1,600
+  // cycles with four row-sum MFMAs in it)
+  f32x16 o[2];
+  o[0] = o[1] = splat16(0.f);
+  float lsum = 0.f;
   float m = 0.f;
   bool mset = false;
   float gthr = -INFINITY;
@@ -3369,18 +3385,14 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
             if (((vb >> (8 * r)) & 0xFFu) == 0u) s[tt][4 * j + r] = -INFINITY;
         }
     }
-    float mx = s[0][0];
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) mx = fmaxf(mx, s[tt][v]);
+    const float mx = max32x2(s[0], s[1]);
     if (__ballot(mx > gthr) != 0) {
       auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
       const float rel = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
       const bool gq = mset ? rel > RESCALE_LOG2 : rel > -INFINITY;
       const float alpha = gq ? (mset ? rp_exp2(-rel) : 0.f) : 1.f;
       const float sub = gq ? rel : 0.f;
-      ls *= alpha;
+      lsum *= alpha;
       o[0] *= alpha;
       o[1] *= alpha;
       m += sub;
@@ -3394,10 +3406,14 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int v = 0; v < 16; ++v) s[tt][v] = rp_exp2(s[tt][v]);
+    {
+      float t8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t8[u] = (s[0][2 * u] + s[0][2 * u + 1]) + (s[1][2 * u] + s[1][2 * u + 1]);
+      lsum += ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) pf[k] = pack8_32(s[k >> 1], k & 1);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ls = mfma32(ones, pf[k], ls);
     if constexpr (DROP) {
       uint32_t acc0 = 0u, acc1 = 0u;
 #pragma unroll
@@ -3452,7 +3468,8 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
     for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(vA[2 * k + dt], pf[k], o[dt]);
   if (!young && !LOCK) raw_barrier();  // the older half's extra barrier (matches the younger half's late start)
 
-  const float l = ls[0];
+  auto lsw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+  const float l = __uint_as_float(lsw[0]) + __uint_as_float(lsw[1]);
   const float inv = drop_scale / l;
   const int64_t ldo = a.ldo;
   const bool qok = q < Tq;

@@ -363,6 +363,18 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("switch", ["RP_ATTN_FWD32", "RP_ATTN_FWD_PP", "RP_ATTN_DQ32"])
+def test_attention_32x32_options(dev, monkeypatch, switch):
+    """The opt-in 32x32x16 kernels (measured slower than the 16x16x32 defaults at the bench shape,
+    DESIGN.md §8 round 4, kept as options): 4-wave forward, 8-wave ping-pong forward, dQ.  Same checks
+    as test_attention_128_blocks_ragged_dropout (ragged down to one valid key, dropout keep bits bit for
+    bit against the restatement — the 32x32 forwards run the same per-(query, lane group) streams — fwd
+    and every gradient vs fp64)."""
+    monkeypatch.setenv(switch, "1")
+    test_attention_128_blocks_ragged_dropout(dev, True)
+
+
+@pytest.mark.gpu
 def test_attention_kv32_option(dev, monkeypatch):
     """RP_ATTN_KV32=1 (the 32x32x16 dK/dV kernel): ragged lengths down to one valid key, dropout, the
     128-key-block path; dQ bitwise the default path's (same dQ kernel), dK / dV within bf16 rounding of
