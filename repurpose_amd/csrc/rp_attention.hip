@@ -3169,7 +3169,7 @@ __device__ __forceinline__ void dma16b_x2(const rp_srd& s0, uint32_t v0, uint32_
       : "memory");
 }
 
-template <bool DROP, bool LOCK>
+template <bool DROP, bool LOCK, int PRIO = 1>
 __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
   __shared__ __attribute__((aligned(1024))) char ring[4 * PP_SLOT];
   __shared__ __attribute__((aligned(16))) uint8_t kvl[FD_TKMAX];
@@ -3305,10 +3305,9 @@ __global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
   if (nkt > 1) issue(1);
   if (nkt > 1) wait_vm<2>(); else wait_vm<0>();
   raw_barrier();
-  if (young && !LOCK) {  // (LOCK: diagnostic variant without the offset — both halves in step)
-    __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (T5 static form)
-    raw_barrier();                  // the younger half starts one segment late
-  }
+  // static priority (T5 static form): PRIO 1 the younger half (default), 2 the older half, 0 none
+  if ((PRIO == 1 && young) || (PRIO == 2 && !young)) __builtin_amdgcn_s_setprio(1);
+  if (young && !LOCK) raw_barrier();  // the younger half starts one segment late (LOCK: diagnostic, in step)
 
   // -DRP_PP_STAMPS diagnostic build only (never the shipped library): s_memtime after every barrier of
   // workgroup 0, written over the lse output ([wave][64 stamps] uint64)
@@ -3615,7 +3614,20 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
     // the 8-wave ping-pong forward (256-query blocks) while its grid still fills every CU
     const dim3 gpp((unsigned)((a.Tq + PP_QB - 1) / PP_QB * a.B * a.H));
     const char* lk = getenv("RP_ATTN_PP_LOCK");  // diagnostic: both wave halves in step
-    if (lk && lk[0] == '1') {
+    const char* pr = getenv("RP_ATTN_PP_PRIO");  // diagnostic: 0 no priority, 2 the older half
+    if (pr && (pr[0] == '0' || pr[0] == '2')) {
+      if (pr[0] == '0') {
+        if (a.drop_thresh)
+          hipLaunchKernelGGL((attn_fwd_pp_kernel<true, false, 0>), gpp, dim3(PP_NT), 0, s, a);
+        else
+          hipLaunchKernelGGL((attn_fwd_pp_kernel<false, false, 0>), gpp, dim3(PP_NT), 0, s, a);
+      } else {
+        if (a.drop_thresh)
+          hipLaunchKernelGGL((attn_fwd_pp_kernel<true, false, 2>), gpp, dim3(PP_NT), 0, s, a);
+        else
+          hipLaunchKernelGGL((attn_fwd_pp_kernel<false, false, 2>), gpp, dim3(PP_NT), 0, s, a);
+      }
+    } else if (lk && lk[0] == '1') {
       if (a.drop_thresh)
         hipLaunchKernelGGL((attn_fwd_pp_kernel<true, true>), gpp, dim3(PP_NT), 0, s, a);
       else

@@ -1,7 +1,8 @@
 #!/bin/bash
 # HBM traffic per launch of every kernel of the training step: two rocprofv3 --pmc passes (FETCH_SIZE,
 # WRITE_SIZE: separate runs, the TCC slots do not hold both) over a short eager bench at (B, T), then
-# scripts/pmc_traffic.py -> profiles/<out>.  usage: scripts/pmc_step.sh <out.json> [B T]
+# scripts/pmc_traffic.py -> gpurun_out/<out> (only gpurun_out/ comes back from the box; copy the file
+# into profiles/ to commit it).  usage: scripts/pmc_step.sh <out.json> [B T]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=$1; B=${2:-8}; T=${3:-2048}
@@ -13,4 +14,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   echo "pass $c rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc_${c}_${T}.log; exit $rc; fi
 done
-python3 scripts/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE_${T} gpurun_out/pmc_WRITE_SIZE_${T} profiles/$OUT $B $T
+python3 scripts/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE_${T} gpurun_out/pmc_WRITE_SIZE_${T} gpurun_out/$OUT $B $T
