@@ -93,7 +93,47 @@ struct MhaDev {
   void* dq; int64_t lddq; void* dk; int64_t lddk; void* dv; int64_t lddv;
   int qpre;  // RP_ATTN_Q_PRESCALED: q holds Q * scale * log2(e) (see include/rp_api.h)
   int empty_uniform;  // a sequence with no valid key attends uniformly to all keys (masked_fill(-1e9))
+  uint64_t mwc_jump;  // split forward: A^(8 n) * 2^64 mod M, n = the first half's key tiles (mwc_jump)
 };
+
+// MWC64X skip-ahead.  The state S = c * 2^32 + x steps as S' = A * S mod M, M = A * 2^32 - 1, so n
+// steps are one multiplication by A^n mod M.  mwc_mulmod(s, p) = s * p * 2^-64 mod M by two reduction
+// steps of the form Y * 2^-32 = (Y >> 32) + (Y mod 2^32) * A (mod M, as A * 2^32 = 1); the host folds
+// the 2^64 into the multiplier (mwc_jump).  s, p < M.
+constexpr uint64_t RP_MWC_M = ((uint64_t)RP_MWC_A << 32) - 1u;
+__host__ __device__ inline uint64_t mwc_mulmod(uint64_t s, uint64_t p) {
+  const uint64_t lo = s * p;
+#ifdef __HIP_DEVICE_COMPILE__
+  const uint64_t hi = __umul64hi(s, p);
+#else
+  const uint64_t hi = (uint64_t)(((unsigned __int128)s * p) >> 64);
+#endif
+  // Y1 = X * 2^-32 = (hi:lo >> 32) + (lo mod 2^32) * A  (< 2^96 + 2^64: y1h never wraps, hi < 2^64 - 2^33)
+  const uint64_t t = (uint64_t)(uint32_t)lo * RP_MWC_A;
+  const uint64_t mid = (hi << 32) | (lo >> 32);
+  const uint64_t y1l = mid + t;
+  const uint64_t y1h = (hi >> 32) + (y1l < t ? 1u : 0u);
+  // Z = Y1 * 2^-32 = (Y1 >> 32) + (Y1 mod 2^32) * A  (< 2^65)
+  const uint64_t u = (uint64_t)(uint32_t)y1l * RP_MWC_A;
+  const uint64_t v = (y1h << 32) | (y1l >> 32);
+  uint64_t r = v + u;
+  if (r < u) {  // Z >= 2^64: Z - M = r + (2^64 - M), once more if that still wraps
+    const uint64_t k64 = 0u - RP_MWC_M;
+    const uint64_t r2 = r + k64;
+    r = r2 < r ? r2 + k64 : r2;
+  }
+  return r >= RP_MWC_M ? r - RP_MWC_M : r;
+}
+// host: A^(8 n) * 2^64 mod M (the multiplier that advances a stream by n 64-key tiles, 8 steps each)
+static inline uint64_t mwc_jump(int n) {
+  const unsigned __int128 m = RP_MWC_M;
+  unsigned __int128 r = ((unsigned __int128)1 << 64) % m, b = RP_MWC_A;
+  for (uint64_t e = 8u * (uint64_t)n; e; e >>= 1) {
+    if (e & 1u) r = r * b % m;
+    b = b * b % m;
+  }
+  return (uint64_t)r;
+}
 
 // empty_uniform: does sequence b have no valid key at all?  (whole workgroup; uniform result)
 __device__ __forceinline__ bool seq_has_no_key(const MhaDev& a, int b, int tid) {
@@ -1093,8 +1133,12 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool DROP, int KTW, bool PIPE>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
+// SPL = 2 (grids that fill the CUs only once: config 4, B = 1, T = 4096): eight waves, waves 4-7 run
+// the same key block over the second half of the query tiles on a ring of their own, and the two
+// halves' dK / dV partials are added through LDS at the end (dK = own + partner on half 0, which stores
+// dK; dV likewise on half 1) — two waves per SIMD where one 4-wave workgroup per CU had one
+template <bool DROP, int KTW, bool PIPE, int SPL = 1>
+__global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_kv_dma_kernel(MhaDev a) {
   constexpr int KB = NW * 16 * KTW;  // keys per workgroup
   using C = AttnCfg<bf16>;
   constexpr int TILE = KV_QT * C::ROWB;
@@ -1108,11 +1152,14 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
   constexpr int NBUF = 3;
   // three separate arrays rather than one indexed ring: every LDS address of a step is then a per-lane
   // base plus an immediate offset
-  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
+  __shared__ __attribute__((aligned(1024))) char ring0[SPL * BUF];
+  __shared__ __attribute__((aligned(1024))) char ring1[SPL * BUF];
+  __shared__ __attribute__((aligned(1024))) char ring2[SPL * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wq = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = wq & (NW - 1);                // wave within its query half
+  const int hv = SPL == 1 ? 0 : wq / NW;      // query half (SPL = 2)
+  const int hoff = hv * BUF;                  // the half's ring region
   const int g = lane >> 4, i = lane & 15;
   const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
   const uint8_t* __restrict__ kvalid = a.kvalid;
@@ -1162,8 +1209,15 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
 
   auto ring = [&](auto bi) -> char* {
     constexpr int BI = decltype(bi)::value;
-    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
+    return (BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2)) + hoff;
   };
+  // query tiles: this half's nqt tiles start at tile qt0; both halves run nsteps ring steps (the half
+  // with one tile fewer idles through the last one: every wave passes every barrier)
+  const int nqt_all = (Tq + KV_QT - 1) / KV_QT;
+  const int nh0 = SPL == 1 ? nqt_all : (nqt_all + 1) / 2;
+  const int qt0 = hv * nh0;
+  const int nqt = SPL == 1 ? nqt_all : (hv == 0 ? nh0 : nqt_all - nh0);
+  const int nsteps = nh0;
   // LDS-DMA of query tile it into ring slot BI: Q and dO (two 1 KB pieces each per wave), the S start
   // (wave 1; -inf past Tq) and dP start (wave 2) rows and the keep-bit words (wave 3, with dropout):
   // D = 4 DMA instructions per wave, 5 for waves 1, 2 and (with dropout) 3
@@ -1190,11 +1244,12 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
     vo_x = (uint32_t)((((int64_t)tile * 4 + (r & 3)) * ldm + cch * 8) * 2);
   }
   const bool xfast = (int64_t)KT * 4 * ldm * 2 < ((int64_t)1 << 31) && rq.fast && rdo.fast;
-  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
+  const uint32_t slot_lds[3] = {lds_addr(ring0) + (uint32_t)hoff, lds_addr(ring1) + (uint32_t)hoff,
+                                 lds_addr(ring2) + (uint32_t)hoff};
   auto issue = [&](int it, auto bi) {
     constexpr int BI = decltype(bi)::value;
     char* buf = ring(bi);
-    const int qs0 = it * KV_QT;
+    const int qs0 = (qt0 + it) * KV_QT;
     if (xfast && qs0 + KV_QT <= Tq) {
       const uint32_t t = slot_lds[BI];
       const uint32_t pq = t + (uint32_t)(w * 2) * 1024u;
@@ -1226,13 +1281,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
       wait_vm<5>();
   };
 
-  const int nqt = (Tq + KV_QT - 1) / KV_QT;
-  issue(0, std::integral_constant<int, 0>());
+  if (nqt > 0) issue(0, std::integral_constant<int, 0>());
   if (nqt > 1) issue(1, std::integral_constant<int, 1>());
   auto step = [&](auto bi, int it) {
     constexpr int BI = decltype(bi)::value;
     wait_tile(it + 1 < nqt);
     raw_barrier();
+    if (SPL > 1 && it >= nqt) return;
     if (it + 2 < nqt) issue(it + 2, std::integral_constant<int, (BI + 2) % NBUF>());
     const char* cur = ring(bi);
     const char* Ql = cur;
@@ -1338,13 +1393,43 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
       }
     }
   };
-  for (int it = 0; it < nqt; it += NBUF) {
+  for (int it = 0; it < nsteps; it += NBUF) {
     step(std::integral_constant<int, 0>(), it);
-    if (it + 1 < nqt) step(std::integral_constant<int, 1>(), it + 1);
-    if (it + 2 < nqt) step(std::integral_constant<int, 2>(), it + 2);
+    if (it + 1 < nsteps) step(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < nsteps) step(std::integral_constant<int, 2>(), it + 2);
+  }
+  if constexpr (SPL > 1) {
+    // every DMA has landed (each half's last step waited vmcnt(0)); after this barrier no wave reads a
+    // ring again.  Half 1 hands its dK partial over in ring0, half 0 its dV partial in ring1 (lane-major
+    // rows of 64 floats: conflict-free), and each half adds the other's (a + b: the same sum on
+    // either side)
+    static_assert(NW * 64 * 4 * KTW * 16 <= SPL * BUF, "a partial fits one ring array");
+    raw_barrier();
+    float* xo_ = reinterpret_cast<float*>(hv == 1 ? ring0 : ring1) + w * (KTW * 16 * 64) + lane;
+#pragma unroll
+    for (int kt = 0; kt < KTW; ++kt)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xo_[((kt * 4 + dt) * 4 + r) * 64] = hv == 1 ? dk[kt][dt][r] : dv[kt][dt][r];
+    __syncthreads();
+    const float* xi = reinterpret_cast<const float*>(hv == 0 ? ring0 : ring1) + w * (KTW * 16 * 64) + lane;
+#pragma unroll
+    for (int kt = 0; kt < KTW; ++kt)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float o = xi[((kt * 4 + dt) * 4 + r) * 64];
+          if (hv == 0)
+            dk[kt][dt][r] += o;
+          else
+            dv[kt][dt][r] += o;
+        }
   }
   // store: dk[kt][dt][r] = dK[key = kw0 + kt*16 + 4g + r][dk = dt*16 + i]; masked keys -> 0;
-  // dK = dS^T Q' / log2(e)
+  // dK = dS^T Q' / log2(e).  SPL = 2: half 0 stores dK, half 1 dV
+  const bool st_k = SPL == 1 || hv == 0, st_v = SPL == 1 || hv == 1;
   bf16* dK = (bf16*)a.dk + (int64_t)b * Tk * a.lddk + h * HD;
   bf16* dV = (bf16*)a.dv + (int64_t)b * Tk * a.lddv + h * HD;
 #pragma unroll
@@ -1356,8 +1441,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_dma_kernel(MhaDev a) {
       const bool ok = kvalid[(int64_t)b * Tk + key] != 0;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        rp_st(dK + (int64_t)key * a.lddk + dt * 16 + i, ok ? dk[kt][dt][r] * (1.f / LOG2E) : 0.f);
-        rp_st(dV + (int64_t)key * a.lddv + dt * 16 + i, ok ? dv[kt][dt][r] : 0.f);
+        if (st_k) rp_st(dK + (int64_t)key * a.lddk + dt * 16 + i, ok ? dk[kt][dt][r] * (1.f / LOG2E) : 0.f);
+        if (st_v) rp_st(dV + (int64_t)key * a.lddv + dt * 16 + i, ok ? dv[kt][dt][r] : 0.f);
       }
     }
 }
@@ -1964,21 +2049,29 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
 // =================================================================================================
 constexpr int QD_TKMAX = 8192;
 
-template <bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
+// SPL = 2 (grids that fill the CUs once but not twice): eight waves, waves 4-7 the same 128 queries over
+// the second half of the key tiles on a ring of their own; both halves form the prologue's row
+// constants (half 0 writes delta), the dQ partials are added through LDS (half 0 stores query rows
+// qt = 0, half 1 qt = 1; own + partner on either side)
+template <bool DROP, int SPL = 1>
+__global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDev a) {
   constexpr int QT = 2, QB = NW * 16 * QT;  // 128 queries per workgroup
   using C = AttnCfg<bf16>;
   constexpr int TILE = FW_KT * C::ROWB;  // one 64-key K or V image (8 KB)
   constexpr int MASKB = 1024;            // keep bits of the tile: 4 lane groups x 128 queries x u16
   constexpr int BUF = 2 * TILE + MASKB;
   constexpr int NBUF = 3;
-  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
+  constexpr int NTS = NT * SPL;
+  __shared__ __attribute__((aligned(1024))) char ring0[SPL * BUF];
+  __shared__ __attribute__((aligned(1024))) char ring1[SPL * BUF];
+  __shared__ __attribute__((aligned(1024))) char ring2[SPL * BUF];
   __shared__ __attribute__((aligned(16))) uint8_t kvl[QD_TKMAX];
   __shared__ int kfull[QD_TKMAX / FW_KT];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wq = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = wq & (NW - 1);            // wave within its key half
+  const int hv = SPL == 1 ? 0 : wq / NW;  // key half (SPL = 2)
+  const int hoff = hv * BUF;
   const int g = lane >> 4, i = lane & 15;
   const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
   const float scale = a.scale, drop_scale = a.drop_scale;
@@ -2024,7 +2117,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
     }
     const float dl = quad_sum(part);
     dq[qt] = q < Tq ? -dl * (DROP ? 1.f / drop_scale : 1.f) : 0.f;
-    if (g == 0 && q < Tq) {  // delta and the dK/dV kernel's row constants (planes 1, 2)
+    if (g == 0 && q < Tq && hv == 0) {  // delta and the dK/dV kernel's row constants (planes 1, 2)
       const int64_t plane = (int64_t)B * H * Tq;
       a.delta[(int64_t)bh * Tq + q] = dl;
       a.delta[plane + (int64_t)bh * Tq + q] = dq[qt];
@@ -2057,9 +2150,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
   }
   // key-valid bytes of the sequence (0 past Tk) and per-tile "no masked key" flags, staged once
   const int nkt = (Tk + FW_KT - 1) / FW_KT;
-  for (int k = tid; k < nkt * FW_KT; k += NT) kvl[k] = k < Tk ? (a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
+  for (int k = tid; k < nkt * FW_KT; k += NTS) kvl[k] = k < Tk ? (a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
   __syncthreads();
-  for (int t = tid; t < nkt; t += NT) {
+  for (int t = tid; t < nkt; t += NTS) {
     int ok = 1;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -2084,8 +2177,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
 
   auto ring = [&](auto bi) -> char* {
     constexpr int BI = decltype(bi)::value;
-    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
+    return (BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2)) + hoff;
   };
+  // key tiles: this half's nkh tiles start at tile kt0; both halves run nsteps ring steps (the half
+  // with one tile fewer idles through the last one: every wave passes every barrier)
+  const int nh0 = SPL == 1 ? nkt : (nkt + 1) / 2;
+  const int kt0 = hv * nh0;
+  const int nkh = SPL == 1 ? nkt : (hv == 0 ? nh0 : nkt - nh0);
   // LDS-DMA of key tile it into slot BI: K and V (two 1 KB pieces each per wave) and, with dropout,
   // wave 1 the 4 x 128 keep-bit words of this query block (columns past ldm clamped: their queries
   // are past Tq and never read)
@@ -2098,10 +2196,12 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
   mcol = mcol < ldm - 8 ? mcol : ldm - 8;
   const uint32_t vo_m = (uint32_t)((((int64_t)(lane >> 4)) * ldm + mcol) * 2);
   const bool xfast = (int64_t)KT * 4 * ldm * 2 < ((int64_t)1 << 31) && rk.fast && rv.fast;
-  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
-  auto issue = [&](int it, auto bi) {
+  const uint32_t slot_lds[3] = {lds_addr(ring0) + (uint32_t)hoff, lds_addr(ring1) + (uint32_t)hoff,
+                                 lds_addr(ring2) + (uint32_t)hoff};
+  auto issue = [&](int itl, auto bi) {
     constexpr int BI = decltype(bi)::value;
     char* buf = ring(bi);
+    const int it = kt0 + itl;
     const int k0 = it * FW_KT;
     if (xfast && k0 + FW_KT <= Tk) {
       const uint32_t t = slot_lds[BI];
@@ -2124,14 +2224,16 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
     else
       wait_vm<4>();
   };
-  issue(0, std::integral_constant<int, 0>());
-  if (nkt > 1) issue(1, std::integral_constant<int, 1>());
+  if (nkh > 0) issue(0, std::integral_constant<int, 0>());
+  if (nkh > 1) issue(1, std::integral_constant<int, 1>());
 
-  auto step = [&](auto bi, int it) {
+  auto step = [&](auto bi, int itl) {
     constexpr int BI = decltype(bi)::value;
-    wait_tile(it + 1 < nkt);
+    wait_tile(itl + 1 < nkh);
     raw_barrier();
-    if (it + 2 < nkt) issue(it + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    if (SPL > 1 && itl >= nkh) return;
+    if (itl + 2 < nkh) issue(itl + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    const int it = kt0 + itl;
     const char* Kl = ring(bi);
     const char* Vl = Kl + TILE;
     uint32_t kwd[QT];
@@ -2206,19 +2308,40 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
     }
     RP_PRIO(0);
   };
-  for (int it = 0; it < nkt; it += NBUF) {
+  const int nsteps = SPL == 1 ? nkt : nh0;
+  for (int it = 0; it < nsteps; it += NBUF) {
     step(std::integral_constant<int, 0>(), it);
-    if (it + 1 < nkt) step(std::integral_constant<int, 1>(), it + 1);
-    if (it + 2 < nkt) step(std::integral_constant<int, 2>(), it + 2);
+    if (it + 1 < nsteps) step(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < nsteps) step(std::integral_constant<int, 2>(), it + 2);
   }
-  // store: dqa[qt][dt][r] = dQ[q = q0 + qt*16 + 4g + r][dk = dt*16 + i]
+  if constexpr (SPL > 1) {
+    // every DMA has landed (each half's last step waited vmcnt(0)); after this barrier no wave reads a
+    // ring again.  Half 1 hands over its qt = 0 partial in ring0, half 0 its qt = 1 partial in ring1
+    // (lane-major rows of 64 floats)
+    static_assert(NW * 64 * 16 * 4 <= SPL * BUF, "a partial fits one ring array");
+    raw_barrier();
+    float* xo_ = reinterpret_cast<float*>(hv == 1 ? ring0 : ring1) + w * (16 * 64) + lane;
+    const int qo = hv == 1 ? 0 : 1;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xo_[(dt * 4 + r) * 64] = dqa[qo][dt][r];
+    __syncthreads();
+    const float* xi = reinterpret_cast<const float*>(hv == 0 ? ring0 : ring1) + w * (16 * 64) + lane;
+    const int qm = hv;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dqa[qm][dt][r] += xi[(dt * 4 + r) * 64];
+  }
+  // store: dqa[qt][dt][r] = dQ[q = q0 + qt*16 + 4g + r][dk = dt*16 + i]  (SPL = 2: half hv rows qt = hv)
   bf16* dQ = (bf16*)a.dq + (int64_t)b * Tq * a.lddq + h * HD;
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int q = q0 + qt * 16 + 4 * g + r;
-      if (q >= Tq) continue;
+      if (q >= Tq || (SPL > 1 && qt != hv)) continue;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) dQ[(int64_t)q * a.lddq + dt * 16 + i] = (bf16)(dqa[qt][dt][r] * scale);
     }
@@ -2236,20 +2359,28 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_dma_kernel(MhaDev a) {
 // =================================================================================================
 constexpr int FD_TKMAX = 4096;
 
-template <bool DROP>
-__global__ __launch_bounds__(NT, 3) void attn_fwd_dma_kernel(MhaDev a) {
+// SPL = 2 (grids that fill the CUs once but not twice): eight waves, waves 4-7 the same 128 queries over
+// the second half of the key tiles on a ring of their own, their dropout streams advanced to that half
+// by mwc_mulmod (the keep bits are the unsplit kernel's); the two halves' (max, row sum, O) are merged
+// through LDS — half 0 finishes query rows qt = 0, half 1 qt = 1, both from (half 0, half 1) in that order
+template <bool DROP, int SPL = 1>
+__global__ __launch_bounds__(NT * SPL, 3 / (2 * SPL - 1)) void attn_fwd_dma_kernel(MhaDev a) {
   constexpr int QT = 2, QB = NW * 16 * QT;  // 128 queries per workgroup
   using C = AttnCfg<bf16>;
   constexpr int TILE = FW_KT * C::ROWB;  // 8 KB
   constexpr int BUF = 2 * TILE;
   constexpr int NBUF = 3;
-  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
+  constexpr int NTS = NT * SPL;
+  __shared__ __attribute__((aligned(1024))) char ring0[SPL * BUF];
+  __shared__ __attribute__((aligned(1024))) char ring1[SPL * BUF];
+  __shared__ __attribute__((aligned(1024))) char ring2[SPL * BUF];
   __shared__ __attribute__((aligned(16))) uint8_t kvl[FD_TKMAX];
   __shared__ int kfull[FD_TKMAX / FW_KT];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wq = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = wq & (NW - 1);            // wave within its key half
+  const int hv = SPL == 1 ? 0 : wq / NW;  // key half (SPL = 2)
+  const int hoff = hv * BUF;
   const int g = lane >> 4, i = lane & 15;
   const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
   const uint32_t drop_thresh = a.drop_thresh;
@@ -2289,10 +2420,10 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_dma_kernel(MhaDev a) {
   }
   // key-valid bytes (every key < Tk when the sequence has none: masked_fill semantics) and flags
   const int nkt = (Tk + FW_KT - 1) / FW_KT;
-  for (int k = tid; k < nkt * FW_KT; k += NT)
+  for (int k = tid; k < nkt * FW_KT; k += NTS)
     kvl[k] = k < Tk ? (novalid || a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
   __syncthreads();
-  for (int t = tid; t < nkt; t += NT) {
+  for (int t = tid; t < nkt; t += NTS) {
     int ok = 1;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -2331,20 +2462,27 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_dma_kernel(MhaDev a) {
     mset[qt] = false;
     gthr[qt] = -INFINITY;
     dst[qt] = DROP ? mwc_seed(rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g)) : 0u;
+    if (DROP && SPL > 1 && hv == 1) dst[qt] = mwc_mulmod(dst[qt], a.mwc_jump);  // to key tile nh0
   }
+  // key tiles: this half's nkh tiles start at tile kt0; both halves run nsteps ring steps (the half
+  // with one tile fewer idles through the last one: every wave passes every barrier)
+  const int nh0 = SPL == 1 ? nkt : (nkt + 1) / 2;
+  const int kt0 = hv * nh0;
+  const int nkh = SPL == 1 ? nkt : (hv == 0 ? nh0 : nkt - nh0);
 
   auto ring = [&](auto bi) -> char* {
     constexpr int BI = decltype(bi)::value;
-    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
+    return (BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2)) + hoff;
   };
   Rows64 rk, rv;
   rk.init(Kg, ldk, Tk, w, lane);
   rv.init(Vg, ldv, Tk, w, lane);
   const bool xfast = rk.fast && rv.fast;
-  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
-  auto issue = [&](int it, auto bi) {  // K and V of key tile it: two 1 KB pieces each per wave
+  const uint32_t slot_lds[3] = {lds_addr(ring0) + (uint32_t)hoff, lds_addr(ring1) + (uint32_t)hoff,
+                                 lds_addr(ring2) + (uint32_t)hoff};
+  auto issue = [&](int itl, auto bi) {  // K and V of key tile kt0 + itl: two 1 KB pieces each per wave
     constexpr int BI = decltype(bi)::value;
-    const int k0 = it * FW_KT;
+    const int k0 = (kt0 + itl) * FW_KT;
     if (xfast && k0 + FW_KT <= Tk) {
       const uint32_t pk = slot_lds[BI] + (uint32_t)(w * 2) * 1024u;
       static_assert(TILE == 8192, "dma16b_x4 places the second operand 8 KB on");
@@ -2359,7 +2497,7 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_dma_kernel(MhaDev a) {
   // step it waits for DMA(it).  Issued after it, in order: (it >= 2) the 2 keep-bit stores of step
   // it - 2, DMA(it + 1) (4), the 2 stores of step it - 1 (it >= 1).
   auto wait_tile = [&](int it) {
-    if (it + 1 >= nkt)
+    if (it + 1 >= nkh)
       wait_vm<0>();
     else if (!DROP || it == 0)
       wait_vm<4>();
@@ -2368,14 +2506,16 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_dma_kernel(MhaDev a) {
     else
       wait_vm<8>();
   };
-  issue(0, std::integral_constant<int, 0>());
-  if (nkt > 1) issue(1, std::integral_constant<int, 1>());
+  if (nkh > 0) issue(0, std::integral_constant<int, 0>());
+  if (nkh > 1) issue(1, std::integral_constant<int, 1>());
 
-  auto step = [&](auto bi, int kt_i) {
+  auto step = [&](auto bi, int itl) {
     constexpr int BI = decltype(bi)::value;
-    wait_tile(kt_i);
+    wait_tile(itl);
     raw_barrier();
-    if (kt_i + 2 < nkt) issue(kt_i + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    if (SPL > 1 && itl >= nkh) return;
+    if (itl + 2 < nkh) issue(itl + 2, std::integral_constant<int, (BI + 2) % NBUF>());
+    const int kt_i = kt0 + itl;
     const char* Kl = ring(bi);
     const char* Vl = Kl + TILE;
     const bool full = kfull[kt_i] != 0;
@@ -2488,10 +2628,52 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_dma_kernel(MhaDev a) {
       }
     RP_PRIO(0);
   };
-  for (int it = 0; it < nkt; it += NBUF) {
+  const int nsteps = SPL == 1 ? nkt : nh0;
+  for (int it = 0; it < nsteps; it += NBUF) {
     step(std::integral_constant<int, 0>(), it);
-    if (it + 1 < nkt) step(std::integral_constant<int, 1>(), it + 1);
-    if (it + 2 < nkt) step(std::integral_constant<int, 2>(), it + 2);
+    if (it + 1 < nsteps) step(std::integral_constant<int, 1>(), it + 1);
+    if (it + 2 < nsteps) step(std::integral_constant<int, 2>(), it + 2);
+  }
+  // the final row sum of query column i for each query tile (every lane of the column holds it)
+  float lsum[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) lsum[qt] = DROP ? ls[qt][0] : quad_sum(lp[qt]);
+  if constexpr (SPL > 1) {
+    // every DMA and keep-bit store has landed (each half's last step waited vmcnt(0)); after this
+    // barrier no wave reads a ring again.  Half 1 hands over its qt = 0 state in ring0, half 0 its
+    // qt = 1 state in ring1: per lane 16 O values, then m, l, mset (lane-major rows of 64 floats)
+    static_assert(NW * 19 * 64 * 4 <= SPL * BUF, "a half's exchange fits one ring array");
+    raw_barrier();
+    const int qo = hv == 1 ? 0 : 1;
+    float* xo_ = reinterpret_cast<float*>(hv == 1 ? ring0 : ring1) + w * (19 * 64) + lane;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xo_[(dt * 4 + r) * 64] = o[qo][dt][r];
+    xo_[16 * 64] = m[qo];
+    xo_[17 * 64] = lsum[qo];
+    xo_[18 * 64] = mset[qo] ? 1.f : 0.f;
+    __syncthreads();
+    const int qm = hv;  // the query tile this half finishes
+    const float* xi = reinterpret_cast<const float*>(hv == 0 ? ring0 : ring1) + w * (19 * 64) + lane;
+    const float pm = xi[16 * 64], pl = xi[17 * 64];
+    const bool pset = xi[18 * 64] != 0.f;
+    // (m, l, O) of half 0 and half 1 in that order on both sides: the same arithmetic either way
+    const float m0 = hv == 0 ? m[qm] : pm, m1 = hv == 0 ? pm : m[qm];
+    const float l0 = hv == 0 ? lsum[qm] : pl, l1 = hv == 0 ? pl : lsum[qm];
+    const bool s0 = hv == 0 ? mset[qm] : pset, s1 = hv == 0 ? pset : mset[qm];
+    const float mm = s0 && s1 ? fmaxf(m0, m1) : (s1 ? m1 : m0);
+    const float a0 = s0 ? rp_exp2(m0 - mm) : 0.f, a1 = s1 ? rp_exp2(m1 - mm) : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float po = xi[(dt * 4 + r) * 64];
+        const float o0 = hv == 0 ? o[qm][dt][r] : po, o1 = hv == 0 ? po : o[qm][dt][r];
+        o[qm][dt][r] = a0 * o0 + a1 * o1;
+      }
+    lsum[qm] = a0 * l0 + a1 * l1;
+    m[qm] = mm;
   }
 
   // ---- epilogue: O[q][dk] = O^T / l ; lse ----
@@ -2499,9 +2681,9 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_dma_kernel(MhaDev a) {
   bf16* __restrict__ out = (bf16*)a.out;
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
-    const float l = DROP ? ls[qt][0] : quad_sum(lp[qt]);
+    const float l = lsum[qt];
     const int q = q0 + qt * 16 + i;
-    if (q >= Tq) continue;
+    if (q >= Tq || (SPL > 1 && qt != hv)) continue;
     const float inv = drop_scale / l;
     bf16* orow = out + ((int64_t)b * Tq + q) * ldo + h * HD;
     bf16* lorow = a.out_lo ? (bf16*)a.out_lo + ((int64_t)b * Tq + q) * ldo + h * HD : nullptr;
@@ -3594,6 +3776,18 @@ static bool attn_fwd32_enabled() {
   return e && e[0] == '1';
 }
 
+// Split workgroups (SPL = 2: eight waves, the reduced sequence range in two halves, partials merged in
+// LDS) for grids of 128-row blocks that fill the CUs once but not twice (config 4: B = 1, T = 4096 is
+// 256 blocks): two waves per SIMD instead of one.  RP_ATTN_SPLIT=0 never, =1 whenever the range has
+// two tiles (tests), unset: 256 <= grid < 384.  Read per launch.
+static bool attn_split(int64_t grid, int tiles) {
+  if (tiles < 2) return false;
+  const char* e = getenv("RP_ATTN_SPLIT");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return grid >= ATTN_SMALL_GRID && grid < ATTN_SMALL_GRID + ATTN_SMALL_GRID / 2;
+}
+
 template <typename T>
 int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
   // 128-query blocks unless that leaves fewer than one workgroup per CU (256 CUs): then 64.  At one
@@ -3647,10 +3841,19 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
     // RP_ATTN_FWD_LDS_PAD (bytes of unused dynamic LDS): tuning knob for the workgroups per CU
     // (53.8 KB static -> three per CU, a fourth of the metric grid then runs as a one-per-CU tail)
     const size_t pad = attn_fwd_pad();
-    if (a.drop_thresh)
+    const int nkt = (a.Tk + FW_KT - 1) / FW_KT;
+    if (attn_split((int64_t)grid.x, nkt)) {
+      MhaDev as = a;
+      as.mwc_jump = mwc_jump((nkt + 1) / 2);
+      if (a.drop_thresh)
+        hipLaunchKernelGGL((attn_fwd_dma_kernel<true, 2>), grid, dim3(2 * NT), 0, s, as);
+      else
+        hipLaunchKernelGGL((attn_fwd_dma_kernel<false, 2>), grid, dim3(2 * NT), 0, s, as);
+    } else if (a.drop_thresh) {
       hipLaunchKernelGGL((attn_fwd_dma_kernel<true>), grid, dim3(NT), pad, s, a);
-    else
+    } else {
       hipLaunchKernelGGL((attn_fwd_dma_kernel<false>), grid, dim3(NT), pad, s, a);
+    }
   } else {
     if (a.drop_thresh)
       hipLaunchKernelGGL((attn_fwd_kernel<T, true, 2>), grid, dim3(NT), 0, s, a);
@@ -3705,10 +3908,16 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     } else if (std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX && attn_dma_q_enabled()) {
       // bf16, 128-query blocks: the LDS-DMA staged dQ kernel (RP_ATTN_DMA=0: register staged)
       const dim3 grid((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
-      if (a.drop_thresh)
+      if (attn_split((int64_t)grid.x, (a.Tk + FW_KT - 1) / FW_KT)) {
+        if (a.drop_thresh)
+          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 2>), grid, dim3(2 * NT), 0, s, a);
+        else
+          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false, 2>), grid, dim3(2 * NT), 0, s, a);
+      } else if (a.drop_thresh) {
         hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true>), grid, dim3(NT), 0, s, a);
-      else
+      } else {
         hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false>), grid, dim3(NT), 0, s, a);
+      }
     } else {
       launch_bwd_q<T, 2>(true, a, s);
     }
@@ -3737,6 +3946,11 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
           hipLaunchKernelGGL((attn_bwd_kv32_kernel<true>), grid, dim3(NT), 0, s, a);
         else
           hipLaunchKernelGGL((attn_bwd_kv32_kernel<false>), grid, dim3(NT), 0, s, a);
+      } else if (attn_split((int64_t)nkb * a.B * a.H, (a.Tq + KV_QT - 1) / KV_QT)) {
+        if (a.drop_thresh)
+          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<true, 2, false, 2>), grid, dim3(2 * NT), 0, s, a);
+        else
+          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<false, 2, false, 2>), grid, dim3(2 * NT), 0, s, a);
       } else {
         if (a.drop_thresh) RP_KVD(true, 2); else RP_KVD(false, 2);
       }

@@ -151,9 +151,12 @@ def attn_ref64(qkv, kv, B, T, H, p, seed, dev):
 
 
 @pytest.mark.timeout(300)
-def test_config4_bf16_attention_T4096_dropout(dev):
-    """rp_attn fwd/bwd at T = 4096, B = 1 (8 heads: 256 query blocks -> the 64-row block path), dropout
-    0.1 with the stored keep bits, the Q columns prescaled as the model's QKV GEMM writes them."""
+def test_config4_bf16_attention_T4096_dropout(dev, monkeypatch):
+    """rp_attn fwd/bwd at T = 4096, B = 1 (8 heads: 256 blocks of 128 rows -> the split 8-wave
+    workgroups, SPL = 2), dropout 0.1 with the stored keep bits, the Q columns prescaled as the model's
+    QKV GEMM writes them; fwd and gradients vs fp64, and against the unsplit 4-wave kernels
+    (RP_ATTN_SPLIT=0): keep bits bit for bit (the second key half's streams are advanced by the
+    skip-ahead multiplier), outputs and gradients within bf16 rounding."""
     from tests.test_kernels_gpu import close, close_per_seq, prescale_q, rnd
     B, H, T, p, seed = 1, 8, 4096, 0.1, 7
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=3).to(torch.bfloat16)
@@ -171,6 +174,15 @@ def test_config4_bf16_attention_T4096_dropout(dev):
     for part, name in enumerate("qkv"):
         cols = slice(part * H * 64, (part + 1) * H * 64)
         close_per_seq(dqkv[:, cols], gref[:, cols], B, atol=6e-2, rtol=6e-2, what=f"attn d{name} T=4096")
+    monkeypatch.setenv("RP_ATTN_SPLIT", "0")
+    o0, lse0, mask0 = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=True, out_lo=olo.clone())
+    assert torch.equal(mask0, mask)
+    close(o, o0.double(), atol=1e-2, rtol=1e-2, what="split vs unsplit fwd")
+    # with dropout the row sums come off the MFMA over the bf16-rounded P (relative to each half's own
+    # running reference), so lse moves by up to ~ln(1 + 2^-8) between the two forms
+    assert (lse - lse0).abs().max().item() < 5e-3
+    dqkv0 = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True, out_lo=olo)
+    close(dqkv, dqkv0.double(), atol=2e-2, rtol=2e-2, what="split vs unsplit bwd")
 
 
 @pytest.mark.timeout(600)

@@ -318,7 +318,7 @@ def prescale_q(qkv, H, scale):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("q_prescaled", [False, True])
-def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
+def test_attention_128_blocks_ragged_dropout(dev, q_prescaled, p=0.1):
     """Self attention on the 128-row block path (B*H*ceil(T/128) >= 512 workgroups; the smaller test
     shapes above take the 64-row path), ragged T and key padding down to one and two valid keys,
     dropout keep bits vs the restatement, fwd and bwd vs fp64.  A sequence with one valid key puts
@@ -327,7 +327,7 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
     kernels, with the prescale done by the kernels or by the producer), and that delta = rowsum(dO * O)
     is taken from the unrounded output (out_lo), without which that key's dK (exactly 0) would collect
     ~1000 rounding residuals of O."""
-    B, H, T, p = 8, 8, 1030, 0.1
+    B, H, T = 8, 8, 1030
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(torch.bfloat16)
     lens = torch.tensor([T, T - 1, 1000, 777, 640, 129, 2, 1], device=dev)
     kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
@@ -343,11 +343,12 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled):
     close(o, ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd (128 blocks)")
     # hi + lo carries the output to ~2^-17
     close(o.double() + olo.double(), ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd hi+lo")
-    KT, ldm = (T + 63) // 64, (T + 255) // 256 * 256
-    words = mask.view(B * H, KT, 4, ldm)[..., :T].to(torch.int64) & 0xFFFF
-    bits = ((words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1).view(B * H, KT, 4, T, 4, 4)
-    got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, T, KT * 64)[:, :, :T].bool()
-    assert torch.equal(got, attn_keep(B, H, T, p, seed, dev).view(B * H, T, T))
+    if p > 0:
+        KT, ldm = (T + 63) // 64, (T + 255) // 256 * 256
+        words = mask.view(B * H, KT, 4, ldm)[..., :T].to(torch.int64) & 0xFFFF
+        bits = ((words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1).view(B * H, KT, 4, T, 4, 4)
+        got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, T, KT * 64)[:, :, :T].bool()
+        assert torch.equal(got, attn_keep(B, H, T, p, seed, dev).view(B * H, T, T))
     do = rnd(B * T, H * 64, dev=dev, seed=T + 1).to(torch.bfloat16)
     dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=q_prescaled, out_lo=olo)
     gref = torch.autograd.grad(ref, ref_in, do.double())[0]
@@ -372,6 +373,19 @@ def test_attention_32x32_options(dev, monkeypatch, switch):
     and every gradient vs fp64)."""
     monkeypatch.setenv(switch, "1")
     test_attention_128_blocks_ragged_dropout(dev, True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.1, 0.0])
+def test_attention_split_workgroups(dev, monkeypatch, p):
+    """RP_ATTN_SPLIT=1 forces the split 8-wave kernels (SPL = 2: the reduced sequence range in two halves,
+    partials merged through LDS; auto-selected when the 128-row grid fills the CUs only once, config 4)
+    on the ragged test: T = 1030 is 17 key / query tiles (the halves get 9 and 8: the second half idles
+    through one ring step), the two shortest sequences have no valid key in the second key half (an
+    empty half in the merge), the dropout keep bits bit for bit against the restatement (the second
+    half's MWC streams start from the skip-ahead multiplier), fwd and every gradient vs fp64."""
+    monkeypatch.setenv("RP_ATTN_SPLIT", "1")
+    test_attention_128_blocks_ragged_dropout(dev, True, p=p)
 
 
 @pytest.mark.gpu
