@@ -219,29 +219,30 @@ constexpr int gemm_lds_bytes() {
 // round trip per chunk — s_memtime stamps put that epilogue at 1.5x the K = 512 main loop
 // (out_proj forward).  Only the residual shapes take it: the batched registers cost the others
 // their occupancy.
-template <typename TC, int MODE, bool HALVES = false, bool RESB = false>
-__device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[4][4], char* lds, int tid, int lane, int wm, int wn,
+template <typename TC, int MODE, bool HALVES = false, bool RESB = false, int MI = 4>
+__device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* lds, int tid, int lane, int wm, int wn,
                                               int64_t m0, int64_t n0, int64_t M, int64_t N, TC* __restrict__ Cout,
                                               int64_t ldc, float alpha, const EpiDev& ep, int split) {
+  static_assert(MI == 4 || !HALVES, "64-row tiles stage whole");
   float* cs = reinterpret_cast<float*>(lds);
   constexpr int OV = 16 / (int)sizeof(TC);
   constexpr int CPRO = BN / OV;
   TC* Cbase = Cout + (MODE == 1 ? (int64_t)split * M * ldc : 0);
   const uint32_t dseed = (MODE == 0 && ep.drop_thresh) ? rp_seed_eff(ep.seed_base, ep.drop_seed) : 0u;
   constexpr int NH = HALVES ? 2 : 1;  // staging passes
-  constexpr int HR = BM / NH;          // rows per pass
+  constexpr int HR = MI * 32 / NH;     // rows per pass
 #pragma unroll 1
   for (int half = 0; half < NH; ++half) {
   if (half) __syncthreads();  // the first half's rows are consumed
   if (!HALVES || wm == half) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          cs[((HALVES ? 0 : wm * 64) + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
+          cs[((HALVES ? 0 : wm * (MI * 16)) + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
   }
   __syncthreads();
   if constexpr (RESB) {
@@ -504,10 +505,11 @@ __device__ __forceinline__ int kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
 __device__ __forceinline__ int kswz32(int r, int c) { return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3); }
 __device__ __forceinline__ int mswz(int k, int c) { return c ^ (2 * ((k & 3) | (((k >> 3) & 1) << 2))); }
 
-template <bool KMAJ, int BK>
+template <bool KMAJ, int BK, int ROWS = BM>
 __device__ __forceinline__ void glds_tile(const bf16* __restrict__ base, int64_t ld, int64_t rows_lim, int64_t row0,
                                           int64_t k0, char* tile, int wid, int lane) {
-  constexpr int PER = BM * BK * 2 / 1024 / (NT / 64);
+  static_assert(KMAJ || ROWS == 128, "m-major images are 128 columns wide");
+  constexpr int PER = ROWS * BK * 2 / 1024 / (NT / 64);
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int I = wid * PER + j;  // wave-instruction index (1 KiB of the tile)
@@ -557,34 +559,38 @@ __device__ __forceinline__ bf16x8 frag_m_swz(const char* t, int rbase, int kbase
   return r;
 }
 
-// main loop of the 128 x 128 LDS-DMA tile over the K range [kbeg, kend) (whole BK steps): acc gets
-// the tile's products; with want_bias, bacc the column sums of the staged m-major A tiles
-template <bool AK, bool BKM, int CFG>
+// main loop of the (32 MI) x 128 LDS-DMA tile over the K range [kbeg, kend) (whole BK steps): acc
+// gets the tile's products; with want_bias, bacc the column sums of the staged m-major A tiles.  MI = 4:
+// 128 x 128 (each wave 64 x 64); MI = 2: 64 x 128 (each wave 32 x 64; k-major A only) for grids of
+// 128-row tiles that leave CUs idle (DmaTile)
+template <bool AK, bool BKM, int CFG, int MI = 4>
 __device__ __forceinline__ void dma_mainloop(const bf16* __restrict__ A, int64_t lda, int64_t M,
                                              const bf16* __restrict__ B, int64_t ldb, int64_t N, int64_t m0,
                                              int64_t n0, int64_t kbeg, int64_t kend, bool want_bias,
-                                             f32x4 (&acc)[4][4], float (&bacc)[8], char* lds, int tid, int lane,
+                                             f32x4 (&acc)[MI][4], float (&bacc)[8], char* lds, int tid, int lane,
                                              int wid, int wm, int wn) {
   using D = DmaCfg<CFG>;
   constexpr int BK = D::BK, GT = D::GT;
+  constexpr int ROWS = MI * 32, GTA = ROWS * BK * 2, SG = GTA + GT;  // A image, stage bytes
+  static_assert(MI == 4 || (AK && D::STAGES == 2), "64-row tiles: k-major A, two stages");
   const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
   if (D::STAGES == 2 && nk > 0) {
-    glds_tile<AK, BK>(A, lda, M, m0, kbeg, lds, wid, lane);
-    glds_tile<BKM, BK>(B, ldb, N, n0, kbeg, lds + GT, wid, lane);
+    glds_tile<AK, BK, ROWS>(A, lda, M, m0, kbeg, lds, wid, lane);
+    glds_tile<BKM, BK>(B, ldb, N, n0, kbeg, lds + GTA, wid, lane);
   }
   if (D::STAGES == 2) __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = lds + (D::STAGES == 2 ? (kt & 1) * 2 * GT : 0);
-    char* nxt = lds + ((kt + 1) & 1) * 2 * GT;
+    const char* cur = lds + (D::STAGES == 2 ? (kt & 1) * SG : 0);
+    char* nxt = lds + ((kt + 1) & 1) * SG;
     if (D::STAGES == 1) {  // one LDS stage: the co-resident workgroups hide the load latency
       if (kt > 0) __syncthreads();
-      glds_tile<AK, BK>(A, lda, M, m0, kbeg + (int64_t)kt * BK, lds, wid, lane);
-      glds_tile<BKM, BK>(B, ldb, N, n0, kbeg + (int64_t)kt * BK, lds + GT, wid, lane);
+      glds_tile<AK, BK, ROWS>(A, lda, M, m0, kbeg + (int64_t)kt * BK, lds, wid, lane);
+      glds_tile<BKM, BK>(B, ldb, N, n0, kbeg + (int64_t)kt * BK, lds + GTA, wid, lane);
       __syncthreads();
     } else if (kt + 1 < nk) {
       const int64_t k1 = kbeg + (int64_t)(kt + 1) * BK;
-      glds_tile<AK, BK>(A, lda, M, m0, k1, nxt, wid, lane);
-      glds_tile<BKM, BK>(B, ldb, N, n0, k1, nxt + GT, wid, lane);
+      glds_tile<AK, BK, ROWS>(A, lda, M, m0, k1, nxt, wid, lane);
+      glds_tile<BKM, BK>(B, ldb, N, n0, k1, nxt + GTA, wid, lane);
     }
     if (want_bias) {  // column sums of the staged dY tile (bias gradient), BK/16 x 16 B per thread
       const int cg = tid & 15;
@@ -598,16 +604,17 @@ __device__ __forceinline__ void dma_mainloop(const bf16* __restrict__ A, int64_t
     }
 #pragma unroll
     for (int ks = 0; ks < BK; ks += 32) {
-      bf16x8 a[4], b[4];
+      bf16x8 a[MI], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[i] = AK ? frag_k_swz<BK>(cur, wm * 64 + i * 16, ks, lane) : frag_m_swz(cur, wm * 64 + i * 16, ks, lane);
+      for (int i = 0; i < MI; ++i)
+        a[i] = AK ? frag_k_swz<BK>(cur, wm * (MI * 16) + i * 16, ks, lane)
+                  : frag_m_swz(cur, wm * (MI * 16) + i * 16, ks, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        b[j] = BKM ? frag_k_swz<BK>(cur + GT, wn * 64 + j * 16, ks, lane)
-                   : frag_m_swz(cur + GT, wn * 64 + j * 16, ks, lane);
+        b[j] = BKM ? frag_k_swz<BK>(cur + GTA, wn * 64 + j * 16, ks, lane)
+                   : frag_m_swz(cur + GTA, wn * 64 + j * 16, ks, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
@@ -617,22 +624,33 @@ __device__ __forceinline__ void dma_mainloop(const bf16* __restrict__ A, int64_t
   if (D::STAGES == 1) __syncthreads();
 }
 
-template <bool AK, bool BKM, typename TC, int MODE, int CFG, bool RESB = false>
+// LDS of a (32 MI) x 128 DMA tile: two (or one) stages of the A and B images, or the staged C tile
+template <int CFG, int MI>
+constexpr int dma_tile_lds() {
+  using D = DmaCfg<CFG>;
+  constexpr int MAIN = D::STAGES * (MI * 32 * D::BK * 2 + D::GT);
+  constexpr int EPI = D::HALVES ? CHALF_BYTES : MI * 32 * CST * 4;
+  return MAIN > EPI ? MAIN : EPI;
+}
+
+template <bool AK, bool BKM, typename TC, int MODE, int CFG, bool RESB = false, int MI = 4>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t N, int64_t K,
                                                               const bf16* __restrict__ A, int64_t lda,
                                                               const bf16* __restrict__ B, int64_t ldb,
                                                               TC* __restrict__ Cout, int64_t ldc, float alpha,
                                                               EpiDev ep, int64_t kchunk, float* __restrict__ bslab) {
   using D = DmaCfg<CFG>;
-  __shared__ __attribute__((aligned(16))) char lds[D::LDS];
+  static_assert(MI != 4 || dma_tile_lds<CFG, 4>() == D::LDS, "128-row LDS as before");
+  __shared__ __attribute__((aligned(16))) char lds[dma_tile_lds<CFG, MI>()];
+  constexpr int TBM = MI * 32;  // tile rows
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_n = (int)((N + BN - 1) / BN);
-  const int tiles_m = (int)((M + BM - 1) / BM);
+  const int tiles_m = (int)((M + TBM - 1) / TBM);
   int t, split;
   tile_split<MODE>(tiles_m * tiles_n, ep.split_major, t, split);
-  const int64_t m0 = (int64_t)(t / tiles_n) * BM;
+  const int64_t m0 = (int64_t)(t / tiles_n) * TBM;
   const int64_t n0 = (int64_t)(t % tiles_n) * BN;
   int64_t kbeg = 0, kend = K;
   if (MODE == 1) {
@@ -640,17 +658,18 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
     kend = kbeg + kchunk < K ? kbeg + kchunk : K;
   }
   const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
-  f32x4 acc[4][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
-  dma_mainloop<AK, BKM, CFG>(A, lda, M, B, ldb, N, m0, n0, kbeg, kend, want_bias, acc, bacc, lds, tid, lane, wid, wm,
-                             wn);
-  gemm_epilogue<TC, MODE, D::HALVES, RESB>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
+  dma_mainloop<AK, BKM, CFG, MI>(A, lda, M, B, ldb, N, m0, n0, kbeg, kend, want_bias, acc, bacc, lds, tid, lane, wid,
+                                 wm, wn);
+  gemm_epilogue<TC, MODE, D::HALVES, RESB, MI>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep,
+                                               split);
   if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab, split);
 }
 
@@ -1296,6 +1315,17 @@ int launch_gemm8(int bn, int64_t M, int64_t N, int64_t K, const bf16* a, int64_t
   return rp_check_launch("rp_gemm");
 }
 
+// 64 x 128 tiles (k-major A, two-stage K = 64 configuration) where the grid of 128 x 128 tiles gives
+// fewer than two workgroups per CU: config 4 (M = 4096) has 128 such tiles on its d_model = 512 GEMMs
+// (half the CUs idle; step 7.92 -> 7.60 ms), config 2 (M = 8192) 256 (7.95 -> 7.66 ms).  RP_GEMM_BM64=0
+// never, =1 wherever legal (tests, A/B), unset: fewer 128 x 128 tiles than twice the CUs.  Per call.
+static bool rp_gemm_bm64(int64_t M, int64_t N) {
+  const char* e = getenv("RP_GEMM_BM64");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return ((M + BM - 1) / BM) * ((N + BN - 1) / BN) < 512;
+}
+
 template <typename T, typename TC>
 int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int ak, const void* B,
                   int64_t ldb, int bk, void* Cp, int64_t ldc, float alpha, const EpiDev& ep,
@@ -1325,6 +1355,26 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
       default: RP_DMA_LAUNCH1(AKV, BKV, MODEV, 2, GRID); break;               \
     }                                                                         \
   } while (0)
+      if (splits == 0 && ak && cfg == 0 && rp_gemm_bm64(M, N)) {
+        const dim3 grid((unsigned)(((M + 63) / 64) * ((N + BN - 1) / BN)));
+        bool done = false;
+        if constexpr (std::is_same<TC, float>::value) {
+          if (bk && ep.residual) {
+            hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, true, TC, 0, 0, true, 2>), grid, dim3(NT), 0, s, M, N, K,
+                               ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
+            done = true;
+          }
+        }
+        if (!done) {
+          if (bk)
+            hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, true, TC, 0, 0, false, 2>), grid, dim3(NT), 0, s, M, N, K,
+                               ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
+          else
+            hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, TC, 0, 0, false, 2>), grid, dim3(NT), 0, s, M, N, K,
+                               ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
+        }
+        return rp_check_launch("rp_gemm");
+      }
       if constexpr (std::is_same<TC, float>::value) {
         if (splits == 0 && ak && bk && ep.residual) {  // the residual (fp32) forward shapes: see RESB
           dim3 grid((unsigned)tiles);

@@ -654,6 +654,36 @@ def test_gemm_metric_shapes_bf16(dev):
         close(db, dy.double().sum(0), atol=1e-3 * math.sqrt(M), what=f"bias grad {n}")
 
 
+@pytest.mark.parametrize("M", [4096, 4000])
+def test_gemm_64_row_tiles_bitwise(dev, monkeypatch, M):
+    """The 64 x 128 tile variant (auto-selected where the 128 x 128 grid leaves CUs idle: config 4's
+    d_model = 512 GEMMs at M = 4096) runs every output element's MFMA chain in the same K order as the
+    128 x 128 kernel: forward with bias + dropout + residual (fp32), the bf16 forward, the fp32 and the
+    gated bf16 dgrad are bitwise the 128-row kernel's (RP_GEMM_BM64=1 vs 0), ragged M included, and
+    match fp64."""
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RP_GEMM_BM64", flag)
+        res = []
+        for (n, k) in [(512, 512), (512, 2048)]:
+            x = rnd(M, k, dev=dev, seed=n + k).to(torch.bfloat16)
+            w = rnd(n, k, dev=dev, seed=n * k, scale=0.05).to(torch.bfloat16)
+            b = rnd(n, dev=dev, seed=3)
+            r = rnd(M, n, dev=dev, seed=5)
+            res.append(K.linear_fwd(x, w, b, out_dtype=torch.float32, dropout_p=0.1, seed=11, residual=r))
+            res.append(K.linear_fwd(x, w, b))
+            dy = rnd(M, n, dev=dev, seed=n - k).to(torch.bfloat16)
+            res.append(K.linear_dgrad(dy, w, out_dtype=torch.float32))
+            gate = rnd(M, k, dev=dev, seed=7).to(torch.bfloat16)
+            res.append(K.linear_dgrad(dy, w, out_dtype=torch.bfloat16, gate=gate, gate_scale=1.25))
+            if flag == "1":
+                close(res[-2], dy.double() @ w.double(), atol=2e-3 * math.sqrt(n), what=f"dgrad {n}x{k} M={M}")
+                close(res[-3], x.double() @ w.double().T + b.double(), atol=2e-2, rtol=1e-2, what=f"fwd {n}x{k}")
+        outs[flag] = res
+    for a, c in zip(outs["1"], outs["0"]):
+        assert torch.equal(a, c)
+
+
 def test_attention_metric_shape_bf16_dropout(dev):
     """Attention at the bench shape (B = 8, T = 2048, H = 8, dk = 64) with dropout 0.1 and ragged key
     padding: forward output and all three gradients against an fp64 torch restatement (same bf16
