@@ -185,12 +185,13 @@ def mwc_step(x, c):
     return lo, x + torch.div(d - lo, 1 << 32, rounding_mode="floor")
 
 
-def attn_keep(B, H, T, p, seed, dev):
+def attn_keep(B, H, T, p, seed, dev, Tk=None):
     """torch restatement of the attention dropout bits (include/rp_api.h, rp_attn_fwd): per (query,
     lane group g) one MWC64X stream seeded x = rp_hash(seed_bh, q*4 + g), c = rp_hash(x, 0x6A09E667)
     >> 1; eight output words (x ^ c after each step) per 64-key tile in tile order; 16-bit halves
-    read as int16."""
-    KT = (T + 63) // 64
+    read as int16.  Tk (cross attention): T queries x Tk keys."""
+    Tk = T if Tk is None else Tk
+    KT = (Tk + 63) // 64
     bh = torch.arange(B * H, device=dev, dtype=torch.int64)
     sbh = rp_hash(seed, bh).view(B * H, 1, 1)
     q = torch.arange(T, device=dev, dtype=torch.int64).view(1, T, 1)
@@ -209,8 +210,8 @@ def attn_keep(B, H, T, p, seed, dev):
     sgn = torch.where(half >= 32768, half - 65536, half)
     keep = sgn >= int(p * 65536 + 0.5) - 32768
     keep = keep.view(B * H, T, KT, 4, 4, 2, 2)                  # [.., g, kt, r>>1, r&1]
-    keep = keep.permute(0, 1, 2, 4, 3, 5, 6).reshape(B * H, T, KT * 64)[:, :, :T]
-    return keep.reshape(B, H, T, T)
+    keep = keep.permute(0, 1, 2, 4, 3, 5, 6).reshape(B * H, T, KT * 64)[:, :, :Tk]
+    return keep.reshape(B, H, T, Tk)
 
 
 def test_mwc_restatement_matches_the_full_product():
@@ -267,15 +268,19 @@ def test_attention_fwd_bwd(dev, dtype, T, p):
     close(dqkv, gref, atol=btol, rtol=btol, what="attn bwd")
 
 
-def mha_ref(q, k, v, kv, B, Tq, Tk, H, scale):
-    """torch restatement of the general attention core (fp64): softmax(scale*QK^T + key mask) V."""
+def mha_ref(q, k, v, kv, B, Tq, Tk, H, scale, keep=None, p=0.0):
+    """torch restatement of the general attention core (fp64): softmax(scale*QK^T + key mask) V, with
+    the stored dropout bits `keep` [B, H, Tq, Tk] applied as (keep / (1 - p)) when given."""
     dk = 64
     qh = q[:, :H * dk].reshape(B, Tq, H, dk).permute(0, 2, 1, 3)
     kh = k[:, :H * dk].reshape(B, Tk, H, dk).permute(0, 2, 1, 3)
     vh = v[:, :H * dk].reshape(B, Tk, H, dk).permute(0, 2, 1, 3)
     s = (qh @ kh.transpose(-1, -2)) * scale
     s = s.masked_fill(~kv.bool().view(B, 1, 1, Tk), float("-inf"))
-    o = torch.softmax(s, -1) @ vh
+    P = torch.softmax(s, -1)
+    if keep is not None:
+        P = torch.where(keep, P / (1 - p), torch.zeros_like(P))
+    o = P @ vh
     return o.permute(0, 2, 1, 3).reshape(B * Tq, H * dk)
 
 
@@ -434,6 +439,42 @@ def test_mha_cross_128_blocks(dev):
     close_per_seq(dq, gq, B, atol=6e-2, rtol=6e-2, what="mha dq (128 blocks)")
     close_per_seq(dkk, gk, B, atol=6e-2, rtol=6e-2, what="mha dk (128 blocks)")
     close_per_seq(dv, gv, B, atol=6e-2, rtol=6e-2, what="mha dv (128 blocks)")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_mha_cross_dropout_prescaled(dev, monkeypatch, split):
+    """Cross attention (Tq = 1100, Tk = 1000, ragged keys) with dropout 0.1 and the producer's Q prescale,
+    so all three phases run the LDS-DMA kernels: forced split 8-wave workgroups (RP_ATTN_SPLIT=1: the
+    forward / dQ split 16 key tiles 8 + 8, dK/dV 18 query tiles 9 + 9) and unsplit.  Keep bits bit for bit
+    against the restatement (Tq x Tk streams), forward and every gradient vs fp64."""
+    monkeypatch.setenv("RP_ATTN_SPLIT", split)
+    B, H, Tq, Tk, p, seed = 8, 8, 1100, 1000, 0.1, 31
+    c = 0.125 * K.LOG2E
+    q = rnd(B * Tq, H * 64, dev=dev, seed=15).to(torch.bfloat16)
+    qp = (q.float() * c).to(torch.bfloat16)
+    kvbuf = rnd(B * Tk, 2 * H * 64, dev=dev, seed=16).to(torch.bfloat16)
+    k, v = kvbuf[:, :H * 64], kvbuf[:, H * 64:]
+    lens = torch.tensor([Tk, 999, 900, 513, 500, 128, 64, 700], device=dev)
+    kv = (torch.arange(Tk, device=dev)[None] < lens[:, None]).to(torch.uint8)
+    o, lse, mask = K.mha_fwd(qp, k, v, kv, B, Tq, Tk, H, 0.125, dropout_p=p, seed=seed, q_prescaled=True)
+    KT, ldm = (Tk + 63) // 64, (Tq + 255) // 256 * 256
+    words = mask.view(B * H, KT, 4, ldm)[..., :Tq].to(torch.int64) & 0xFFFF
+    bits = ((words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1).view(B * H, KT, 4, Tq, 4, 4)
+    got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, Tq, KT * 64)[:, :, :Tk].bool()
+    keep = attn_keep(B, H, Tq, p, seed, dev, Tk=Tk)
+    assert torch.equal(got, keep.view(B * H, Tq, Tk))
+    qd = (qp.double() / c).requires_grad_(True)
+    kd, vd = (t.double().requires_grad_(True) for t in (k, v))
+    ref = mha_ref(qd, kd, vd, kv, B, Tq, Tk, H, 0.125, keep=keep, p=p)
+    close(o, ref.detach(), atol=2e-2, rtol=2e-2, what="mha fwd dropout")
+    do = rnd(B * Tq, H * 64, dev=dev, seed=17).to(torch.bfloat16)
+    dq, dkk, dv = K.mha_bwd(qp, k, v, o, do, lse, kv, B, Tq, Tk, H, 0.125, dropout_p=p, dropmask=mask,
+                            q_prescaled=True)
+    gq, gk, gv = torch.autograd.grad(ref, (qd, kd, vd), do.double())
+    close_per_seq(dq, gq, B, atol=6e-2, rtol=6e-2, what="mha dq dropout")
+    close_per_seq(dkk, gk, B, atol=6e-2, rtol=6e-2, what="mha dk dropout")
+    close_per_seq(dv, gv, B, atol=6e-2, rtol=6e-2, what="mha dv dropout")
 
 
 def test_attention_lse(dev):
