@@ -93,7 +93,7 @@ struct MhaDev {
   void* dq; int64_t lddq; void* dk; int64_t lddk; void* dv; int64_t lddv;
   int qpre;  // RP_ATTN_Q_PRESCALED: q holds Q * scale * log2(e) (see include/rp_api.h)
   int empty_uniform;  // a sequence with no valid key attends uniformly to all keys (masked_fill(-1e9))
-  uint64_t mwc_jump;  // split forward: A^(8 n) * 2^64 mod M, n = the first half's key tiles (mwc_jump)
+  uint64_t mwc_jump;  // split forward: A^(8 n) * 2^64 mod M, n = the key tiles of one part (mwc_jump)
 };
 
 // MWC64X skip-ahead.  The state S = c * 2^32 + x steps as S' = A * S mod M, M = A * 2^32 - 1, so n
@@ -2363,8 +2363,12 @@ constexpr int FD_TKMAX = 4096;
 // the second half of the key tiles on a ring of their own, their dropout streams advanced to that half
 // by mwc_mulmod (the keep bits are the unsplit kernel's); the two halves' (max, row sum, O) are merged
 // through LDS — half 0 finishes query rows qt = 0, half 1 qt = 1, both from (half 0, half 1) in that order
+// SPL = 3: twelve waves, the key tiles in three parts (three waves per SIMD, the unsplit kernel's
+// residency, on one block) for grids of at most one block per CU; parts 1 and 2 hand their whole
+// state to part 0, which merges in part order and stores
 template <bool DROP, int SPL = 1>
-__global__ __launch_bounds__(NT * SPL, 3 / (2 * SPL - 1)) void attn_fwd_dma_kernel(MhaDev a) {
+__global__ __launch_bounds__(NT * SPL, SPL == 1 ? 3 : 1) void attn_fwd_dma_kernel(MhaDev a) {
+  static_assert(SPL >= 1 && SPL <= 3, "one, two or three key parts");
   constexpr int QT = 2, QB = NW * 16 * QT;  // 128 queries per workgroup
   using C = AttnCfg<bf16>;
   constexpr int TILE = FW_KT * C::ROWB;  // 8 KB
@@ -2379,7 +2383,7 @@ __global__ __launch_bounds__(NT * SPL, 3 / (2 * SPL - 1)) void attn_fwd_dma_kern
   const int tid = threadIdx.x, lane = tid & 63;
   const int wq = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int w = wq & (NW - 1);            // wave within its key half
-  const int hv = SPL == 1 ? 0 : wq / NW;  // key half (SPL = 2)
+  const int hv = SPL == 1 ? 0 : wq / NW;  // key part (SPL > 1)
   const int hoff = hv * BUF;
   const int g = lane >> 4, i = lane & 15;
   const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
@@ -2462,13 +2466,14 @@ __global__ __launch_bounds__(NT * SPL, 3 / (2 * SPL - 1)) void attn_fwd_dma_kern
     mset[qt] = false;
     gthr[qt] = -INFINITY;
     dst[qt] = DROP ? mwc_seed(rp_hash(seed_bh, (uint32_t)(q0 + qt * 16 + i) * 4u + (uint32_t)g)) : 0u;
-    if (DROP && SPL > 1 && hv == 1) dst[qt] = mwc_mulmod(dst[qt], a.mwc_jump);  // to key tile nh0
+    if (DROP && SPL > 1)  // to key tile kt0 = hv * nh0
+      for (int pj = 0; pj < hv; ++pj) dst[qt] = mwc_mulmod(dst[qt], a.mwc_jump);
   }
   // key tiles: this half's nkh tiles start at tile kt0; both halves run nsteps ring steps (the half
   // with one tile fewer idles through the last one: every wave passes every barrier)
-  const int nh0 = SPL == 1 ? nkt : (nkt + 1) / 2;
+  const int nh0 = SPL == 1 ? nkt : (nkt + SPL - 1) / SPL;
   const int kt0 = hv * nh0;
-  const int nkh = SPL == 1 ? nkt : (hv == 0 ? nh0 : nkt - nh0);
+  const int nkh = SPL == 1 ? nkt : (nkt - kt0 < nh0 ? (nkt - kt0 > 0 ? nkt - kt0 : 0) : nh0);
 
   auto ring = [&](auto bi) -> char* {
     constexpr int BI = decltype(bi)::value;
@@ -2638,7 +2643,7 @@ __global__ __launch_bounds__(NT * SPL, 3 / (2 * SPL - 1)) void attn_fwd_dma_kern
   float lsum[QT];
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) lsum[qt] = DROP ? ls[qt][0] : quad_sum(lp[qt]);
-  if constexpr (SPL > 1) {
+  if constexpr (SPL == 2) {
     // every DMA and keep-bit store has landed (each half's last step waited vmcnt(0)); after this
     // barrier no wave reads a ring again.  Half 1 hands over its qt = 0 state in ring0, half 0 its
     // qt = 1 state in ring1: per lane 16 O values, then m, l, mset (lane-major rows of 64 floats)
@@ -2674,6 +2679,46 @@ __global__ __launch_bounds__(NT * SPL, 3 / (2 * SPL - 1)) void attn_fwd_dma_kern
       }
     lsum[qm] = a0 * l0 + a1 * l1;
     m[qm] = mm;
+  } else if constexpr (SPL > 2) {
+    // parts 1 .. SPL-1 write their (O, m, l, mset) of both query tiles (O: 32 floats per lane in ring0 /
+    // ring1, the rest: 6 per lane in ring2, lane-major rows of 64 floats); part 0 merges in part order
+    static_assert(SPL == 3 && NW * 32 * 64 * 4 <= SPL * BUF && 2 * NW * 6 * 64 * 4 <= SPL * BUF, "exchange fits");
+    raw_barrier();
+    if (hv > 0) {
+      float* xo_ = reinterpret_cast<float*>(hv == 1 ? ring0 : ring1) + w * (32 * 64) + lane;
+      float* xs_ = reinterpret_cast<float*>(ring2) + ((hv - 1) * NW + w) * (6 * 64) + lane;
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xo_[((qt * 4 + dt) * 4 + r) * 64] = o[qt][dt][r];
+        xs_[(qt * 3 + 0) * 64] = m[qt];
+        xs_[(qt * 3 + 1) * 64] = lsum[qt];
+        xs_[(qt * 3 + 2) * 64] = mset[qt] ? 1.f : 0.f;
+      }
+    }
+    __syncthreads();
+    if (hv > 0) return;  // every barrier of the block is behind: part 0 stores
+#pragma unroll
+    for (int pp = 1; pp < SPL; ++pp) {
+      const float* xi = reinterpret_cast<const float*>(pp == 1 ? ring0 : ring1) + w * (32 * 64) + lane;
+      const float* xs = reinterpret_cast<const float*>(ring2) + ((pp - 1) * NW + w) * (6 * 64) + lane;
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        const float pm = xs[(qt * 3 + 0) * 64], pl = xs[(qt * 3 + 1) * 64];
+        const bool pset = xs[(qt * 3 + 2) * 64] != 0.f;
+        const float mm = mset[qt] && pset ? fmaxf(m[qt], pm) : (pset ? pm : m[qt]);
+        const float a0 = mset[qt] ? rp_exp2(m[qt] - mm) : 0.f, a1 = pset ? rp_exp2(pm - mm) : 0.f;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[qt][dt][r] = a0 * o[qt][dt][r] + a1 * xi[((qt * 4 + dt) * 4 + r) * 64];
+        lsum[qt] = a0 * lsum[qt] + a1 * pl;
+        m[qt] = mm;
+        mset[qt] = mset[qt] || pset;
+      }
+    }
   }
 
   // ---- epilogue: O[q][dk] = O^T / l ; lse ----
@@ -2683,7 +2728,7 @@ __global__ __launch_bounds__(NT * SPL, 3 / (2 * SPL - 1)) void attn_fwd_dma_kern
   for (int qt = 0; qt < QT; ++qt) {
     const float l = lsum[qt];
     const int q = q0 + qt * 16 + i;
-    if (q >= Tq || (SPL > 1 && qt != hv)) continue;
+    if (q >= Tq || (SPL == 2 && qt != hv)) continue;
     const float inv = drop_scale / l;
     bf16* orow = out + ((int64_t)b * Tq + q) * ldo + h * HD;
     bf16* lorow = a.out_lo ? (bf16*)a.out_lo + ((int64_t)b * Tq + q) * ldo + h * HD : nullptr;
@@ -3776,6 +3821,20 @@ static bool attn_fwd32_enabled() {
   return e && e[0] == '1';
 }
 
+// compute units of the current device (cached per device)
+static int64_t attn_cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return ATTN_SMALL_GRID;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = (int)ATTN_SMALL_GRID;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 // Split workgroups (SPL = 2: eight waves, the reduced sequence range in two halves, partials merged in
 // LDS) for grids of 128-row blocks that fill the CUs once but not twice (config 4: B = 1, T = 4096 is
 // 256 blocks): two waves per SIMD instead of one.  RP_ATTN_SPLIT=0 never, =1 whenever the range has
@@ -3842,7 +3901,22 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
     // (53.8 KB static -> three per CU, a fourth of the metric grid then runs as a one-per-CU tail)
     const size_t pad = attn_fwd_pad();
     const int nkt = (a.Tk + FW_KT - 1) / FW_KT;
-    if (attn_split((int64_t)grid.x, nkt)) {
+    // grids of at most one block per CU (config 4: 256) on the three-part split kernel (three waves
+    // per SIMD, the unsplit kernel's residency); RP_ATTN_SPLIT=3 forces it.  Measured and dropped: the
+    // metric grid's last partial round (1,024 = 768 + 256 blocks) as a second launch on it: fwd 143 ->
+    // 154 us — the single launch already starts tail blocks as first-round blocks retire
+    const char* se = getenv("RP_ATTN_SPLIT");
+    const bool force3 = se && se[0] == '3';
+    const bool autos = !se || (se[0] != '0' && se[0] != '1' && !force3);  // unset / empty / other: auto
+    const bool split3 = nkt >= 3 && (force3 || (autos && (int64_t)grid.x <= attn_cu_count()));
+    if (split3) {
+      MhaDev as = a;
+      as.mwc_jump = mwc_jump((nkt + 2) / 3);
+      if (a.drop_thresh)
+        hipLaunchKernelGGL((attn_fwd_dma_kernel<true, 3>), grid, dim3(3 * NT), 0, s, as);
+      else
+        hipLaunchKernelGGL((attn_fwd_dma_kernel<false, 3>), grid, dim3(3 * NT), 0, s, as);
+    } else if (attn_split((int64_t)grid.x, nkt)) {
       MhaDev as = a;
       as.mwc_jump = mwc_jump((nkt + 1) / 2);
       if (a.drop_thresh)

@@ -381,15 +381,17 @@ def test_attention_32x32_options(dev, monkeypatch, switch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("split", ["1", "3"])
 @pytest.mark.parametrize("p", [0.1, 0.0])
-def test_attention_split_workgroups(dev, monkeypatch, p):
+def test_attention_split_workgroups(dev, monkeypatch, p, split):
     """RP_ATTN_SPLIT=1 forces the split 8-wave kernels (SPL = 2: the reduced sequence range in two halves,
-    partials merged through LDS; auto-selected when the 128-row grid fills the CUs only once, config 4)
-    on the ragged test: T = 1030 is 17 key / query tiles (the halves get 9 and 8: the second half idles
-    through one ring step), the two shortest sequences have no valid key in the second key half (an
-    empty half in the merge), the dropout keep bits bit for bit against the restatement (the second
-    half's MWC streams start from the skip-ahead multiplier), fwd and every gradient vs fp64."""
-    monkeypatch.setenv("RP_ATTN_SPLIT", "1")
+    partials merged through LDS; auto-selected when the 128-row grid fills the CUs only once, config 4),
+    =3 the three-part 12-wave forward (auto-selected for a grid's last partial round) on the ragged
+    test: T = 1030 is 17 key / query tiles (halves 9 + 8, thirds 6 + 6 + 5: the short part idles through
+    its last ring step), the two shortest sequences have no valid key past the first part (empty parts
+    in the merge), the dropout keep bits bit for bit against the restatement (the later parts' MWC
+    streams start from the skip-ahead multiplier), fwd and every gradient vs fp64."""
+    monkeypatch.setenv("RP_ATTN_SPLIT", split)
     test_attention_128_blocks_ragged_dropout(dev, True, p=p)
 
 
