@@ -7,8 +7,9 @@ models/MMCTransformer.py.
   * config 2 (L = 16, T = 1024, B = 8, bf16): all 8 sequences' logits within 5e-2 of the fp32 oracle
     (reported mode, not the parity gate) and one training step's gradients within the L = 16 bf16-vs-fp32
     gradient tolerances of the fp32 GPU gradients;
-  * config 4 (T = 4096, B = 1): the fp32 L = 16 forward against the oracle, and the bf16 attention
-    kernels (dropout on, keep bits stored) against an fp64 restatement at that length;
+  * config 4 (T = 4096, B = 1): the fp32 L = 16 forward against the oracle, the bf16 model as config 2
+    (its split attention and 64-row GEMM kernels), and the bf16 attention kernels (dropout on, keep bits
+    stored) against an fp64 restatement and the unsplit kernels at that length;
   * config 5 (inference, 64 videos): scripts/val_atiou.py at L = 16 — identical proposals and AtIoU
     against the CPU restatement of inference_ + calculate_tiou.
 """
@@ -97,23 +98,34 @@ def test_config2_bf16_L16_T1024_B8(dev):
     row, so the sub-batches see the padded batch's computation), and one bf16 training step's gradients
     at that shape against the fp32 GPU gradients of the same model and batch (dropout off), with the
     tolerances of the L = 16 grouped-gradient gate (tests/test_depth_gpu.py): per tensor
-    ||g_bf16 - g_fp32|| <= 0.10 ||g_fp32||, flat <= 0.03."""
+    ||g_bf16 - g_fp32|| <= 0.10 ||g_fp32||, flat <= 0.03.  At M = 8192 the d_model GEMMs run on the
+    64 x 128 tiles."""
+    bf16_whole_batch(dev, 8, 1024, [1024, 1024, 1000, 900, 800, 777, 512, 300], seed=22, tag="config 2")
+
+
+@pytest.mark.timeout(600)
+def test_config4_bf16_L16_T4096_B1(dev):
+    """Config 4 (T = 4096, B = 1) in bf16 through the kernels only that shape selects — the three-part
+    split attention forward, the two-part split dQ / dK/dV, 64 x 128 GEMM tiles — checked as config 2:
+    logits against the fp32 oracle, one step's gradients against the fp32 GPU gradients."""
+    bf16_whole_batch(dev, 1, 4096, [4000], seed=45, tag="config 4", sub=1)
+
+
+def bf16_whole_batch(dev, B, T, lens, seed, tag, sub=2):
     _threads()
     ref, m = models("bf16")
     m.to(dev).eval()
-    B, T = 8, 1024
-    lens = [1024, 1024, 1000, 900, 800, 777, 512, 300]
-    b = batch(B, T, lens, seed=22)
+    b = batch(B, T, lens, seed=seed)
     errs = []
     with torch.no_grad():
         out = m(to_dev(b, dev))
-        for s0 in range(0, B, 2):
-            sub = {k: v[s0:s0 + 2] for k, v in b.items()}
-            r = ref(sub)
-            valid = sub["masks"][:, 0, :]
-            for j in range(2):
+        for s0 in range(0, B, sub):
+            sb = {k: v[s0:s0 + sub] for k, v in b.items()}
+            r = ref(sb)
+            valid = sb["masks"][:, 0, :]
+            for j in range(sub):
                 errs.append((out[1][s0 + j].float().cpu() - r[1][j])[valid[j]].abs().max().item())
-    print(f"config 2 bf16 L16: per-sequence logits max err vs fp32 oracle {[f'{e:.2e}' for e in errs]}")
+    print(f"{tag} bf16 L16: per-sequence logits max err vs fp32 oracle {[f'{e:.2e}' for e in errs]}")
     assert len(errs) == B and max(errs) < 5e-2, errs
     del ref
 
@@ -141,7 +153,7 @@ def test_config2_bf16_L16_T1024_B8(dev):
         assert g16[n].abs().max().item() > 0, n
         assert rel <= 0.10, f"{n}: ||bf16 - fp32|| / ||fp32|| = {rel:.3e}"
     flat = ((f16 - f32).norm() / f32.norm()).item()
-    print(f"config 2 step gradients bf16 vs fp32: flat rel {flat:.3e}, worst tensor {worst[0]:.3e} ({worst[1]})")
+    print(f"{tag} step gradients bf16 vs fp32: flat rel {flat:.3e}, worst tensor {worst[0]:.3e} ({worst[1]})")
     assert torch.isfinite(f16).all().item() and flat <= 0.03
 
 
