@@ -838,6 +838,21 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
     }
     __syncthreads();
     constexpr int ITER = 64 * CPRO / NT8;
+    // fp32 C with a residual (the 256 x 128 tile's linear2 forward): the pass's residual chunks are
+    // loaded before its first store (inline, each load would wait behind the previous chunk's store)
+    constexpr bool RESV = std::is_same<TC, float>::value && MODE == 0;
+    float4 rv[RESV ? ITER : 1];
+    if constexpr (RESV) {
+      if (ep.residual) {
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) {
+          const int id = tid + it * NT8;
+          const int64_t m = m0 + pass * 64 + id / CPRO, n = n0 + (id % CPRO) * OV;
+          rv[it] = (m < M && n < N) ? *reinterpret_cast<const float4*>(ep.residual + m * ep.ldr + n)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
     bf16x8 gv[GATEB ? ITER : 1];
     if constexpr (GATEB) {
       static_assert(OV == 8 && MODE == 0, "GATEB: bf16 C");
@@ -896,10 +911,14 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
           }
         }
         if (ep.residual) {
+          if constexpr (RESV) {
+            v[0] += rv[it].x; v[1] += rv[it].y; v[2] += rv[it].z; v[3] += rv[it].w;
+          } else {
 #pragma unroll
-          for (int e = 0; e < OV; e += 4) {
-            float4 q = *reinterpret_cast<const float4*>(ep.residual + m * ep.ldr + n + e);
-            v[e] += q.x; v[e + 1] += q.y; v[e + 2] += q.z; v[e + 3] += q.w;
+            for (int e = 0; e < OV; e += 4) {
+              float4 q = *reinterpret_cast<const float4*>(ep.residual + m * ep.ldr + n + e);
+              v[e] += q.x; v[e + 1] += q.y; v[e + 2] += q.z; v[e + 3] += q.w;
+            }
           }
         }
       }
@@ -1140,6 +1159,130 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
   }
 }
 
+// One 256 x 128 output tile (BNT = 128: the d_model = 512 outputs, 256 tiles at M = 16384 — one per
+// CU — where 256 x 256 tiles would leave half the CUs idle), eight waves: wm = wid >> 2 the 128-row
+// half, wn = wid & 3 the 32-column quarter (acc[8][2] per wave).  A K-tile (64 deep) is TWO phases
+// of 16 MFMAs: phase 0 reads A rows 0-63 of the wave's half and the wave's 32 B columns, phase 1 A
+// rows 64-127 (the B fragments stay in registers); each phase is a read segment and an MFMA segment
+// closed by raw s_barriers, waves 4-7 one barrier behind waves 0-3 (the two waves of a SIMD alternate
+// reading and multiplying).  Two LDS slots (A 2 x 16 KiB + B 16 KiB each), K-tile t in slot t & 1.
+// Barrier events of K-tile t on the leading half's clock: 4t+1 after R0, 4t+2 after M0, 4t+3 after
+// R1, 4t+4 after M1; the lagging half's R0 / M0 / R1 / M1 end at 4t+2 .. 4t+5.  So the B image of
+// K-tile t is last read before event 4t+2 and its A images before 4t+4: B(t+2) is issued in R1(t)
+// (after 4t+2 on both halves), A(t+1) in M0(t) (after 4t+1 > 4t+0, when slot (t+1) & 1's A images
+// of K-tile t-1 died), and every piece of K-tile t+1 must have landed by event 4t+4, the first
+// barrier before any wave reads it: the leading half waits before its fourth barrier of K-tile t,
+// the lagging half before its third (both event 4t+4), vmcnt(2) leaving only B(t+2) in flight.
+// Same MFMA order per output element as the 128 x 128 kernel (K-tiles ascending, 32-deep halves).
+template <bool AK, bool BKM, typename TC, int MODE>
+__device__ __forceinline__ void gemm8_tile128(int64_t M, int64_t N, const bf16* __restrict__ A, int64_t lda,
+                                              const bf16* __restrict__ B, int64_t ldb, TC* __restrict__ Cout,
+                                              int64_t ldc, float alpha, const EpiDev& ep, int64_t kbeg, int64_t kend,
+                                              int64_t m0, int64_t n0, int split, char* lds) {
+  using G = G8<128, 64, 2>;
+  static_assert(G::NBH == 1 && G::JT == 2, "256 x 128 tile");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int bcol = wn * 32;
+  const int nk = kend > kbeg ? (int)((kend - kbeg) / 64) : 0;
+  auto fill_a = [&](int kt) {
+    char* buf = lds + (kt & 1) * G::SLOT;
+    const int64_t k0 = kbeg + (int64_t)kt * 64;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        glds_piece8<AK, 64>(A, lda, M, m0 + 128 * h, k0, buf + h * G::HB, wid * 2 + j, lane);
+  };
+  auto fill_b = [&](int kt) {
+    char* buf = lds + (kt & 1) * G::SLOT;
+    const int64_t k0 = kbeg + (int64_t)kt * 64;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds_piece8<BKM, 64>(B, ldb, N, n0, k0, buf + 2 * G::HB, wid * 2 + j, lane);
+  };
+  auto ra = [&](const char* img, int i, int kk) -> bf16x8 {
+    return AK ? frag_k_swz<64>(img, i * 16, kk, lane) : frag_m_swz(img, i * 16, kk, lane);
+  };
+  auto rb = [&](const char* img, int j, int kk) -> bf16x8 {
+    return BKM ? frag_k_swz<64>(img, bcol + j * 16, kk, lane) : frag_m_swz(img, bcol + j * 16, kk, lane);
+  };
+  if (nk > 0) {
+    fill_a(0);
+    fill_b(0);
+    if (nk > 1) {
+      fill_b(1);
+      rp_waitcnt<2, 15>();  // A(0), B(0) landed; B(1) may stay in flight
+    } else {
+      rp_waitcnt<0, 15>();
+    }
+  }
+  rp_raw_barrier();
+  if (wm == 1) rp_raw_barrier();  // the second wave of each SIMD runs one barrier behind
+
+  bf16x8 fa[4][2], fb[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = lds + (kt & 1) * G::SLOT;
+    const char* ai = cur + wm * G::HB;
+    const char* bi = cur + 2 * G::HB;
+    // ---- phase 0: A rows 0-63 and the B columns ----
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = ra(ai, i, kk * 32);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb[j][kk] = rb(bi, j, kk * 32);
+    rp_raw_barrier();
+    if (kt + 1 < nk) fill_a(kt + 1);  // slot (kt+1)&1's A images (K-tile kt-1) died at event 4kt
+    rp_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    rp_raw_barrier();
+    // ---- phase 1: A rows 64-127; the B pieces of K-tile kt+2 (this slot's B image died at 4kt+2) ----
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = ra(ai, 4 + i, kk * 32);
+    if (kt + 2 < nk) fill_b(kt + 2);
+    auto wait_next = [&]() {
+      if (kt + 2 < nk)
+        rp_waitcnt<2, 15>();  // only B(kt+2) may stay in flight
+      else
+        rp_waitcnt<0, 15>();
+    };
+    if (wm == 1) wait_next();  // the lagging half's third barrier of K-tile kt is event 4kt+4
+    rp_raw_barrier();
+    rp_lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (wm == 0) wait_next();  // the leading half's fourth barrier of K-tile kt is event 4kt+4
+    rp_raw_barrier();
+  }
+  if (wm == 0) rp_raw_barrier();  // match the lagging half's barrier count
+  __syncthreads();
+  gemm8_epilogue<TC, MODE, 128>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
+}
+
 template <bool AK, bool BKM, typename TC, int MODE, int BNT, bool GATEB = false>
 __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int64_t K, const bf16* __restrict__ A,
                                                        int64_t lda, const bf16* __restrict__ B, int64_t ldb,
@@ -1157,9 +1300,14 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
     kbeg = (int64_t)split * kchunk;
     kend = kbeg + kchunk < K ? kbeg + kchunk : K;
   }
-  float* bias_dst = (MODE == 1 && bslab != nullptr && n0 == 0) ? bslab + (int64_t)split * M : nullptr;
-  gemm8_tile<AK, BKM, TC, MODE, BNT, GATEB>(M, N, A, lda, B, ldb, Cout, ldc, alpha, ep, kbeg, kend, m0, n0, split,
-                                            bias_dst, 0, lds);
+  if constexpr (BNT == 128) {
+    static_assert(MODE == 0 && !GATEB, "256 x 128 tiles: plain / fused-epilogue forward and dgrad");
+    gemm8_tile128<AK, BKM, TC, MODE>(M, N, A, lda, B, ldb, Cout, ldc, alpha, ep, kbeg, kend, m0, n0, split, lds);
+  } else {
+    float* bias_dst = (MODE == 1 && bslab != nullptr && n0 == 0) ? bslab + (int64_t)split * M : nullptr;
+    gemm8_tile<AK, BKM, TC, MODE, BNT, GATEB>(M, N, A, lda, B, ldb, Cout, ldc, alpha, ep, kbeg, kend, m0, n0, split,
+                                              bias_dst, 0, lds);
+  }
 }
 
 // grouped weight gradients on 256 x 256 tiles (the WgGroup of wgrad_grouped_kernel, whole K): twice
@@ -1193,6 +1341,12 @@ static int rp_gemm8_mode() {
 }
 static int rp_gemm8_bn(int64_t M, int64_t N, int64_t kext) {
   if (kext % 64 != 0 || kext < 128 || M < 256 || N % 8 != 0) return 0;
+  // RP_GEMM8_128=1 (opt-in): the 256 x 128 phased tile for the d_model = 512 outputs over K >= 1024
+  // (linear2 forward, linear1 and QKV dgrad).  Warm and plain it beats the 128 x 128 kernel by 7-10 %
+  // (scripts/gemm_vs_blas.py), cold with the fused epilogues it loses on the dgrad shapes, and the step
+  // moved 15.16 -> 15.14 ms (three interleaved pairs): off by default.  Read per call.
+  const char* e128 = getenv("RP_GEMM8_128");
+  if (e128 && e128[0] == '1' && N <= 512 && kext >= 1024) return 128;
   const int mode = rp_gemm8_mode();
   if (mode == 0) return 0;
   if (mode == 1) return 256;
@@ -1293,6 +1447,20 @@ int launch_gemm8(int bn, int64_t M, int64_t N, int64_t K, const bf16* a, int64_t
   hipLaunchKernelGGL((gemm8_kernel<AKV, BKV, TC, MODEV, 256>), GRID, dim3(NT8), 0, s, M, N, K, a, lda, b, ldb, c, \
                      ldc, alpha, ep, kchunk, bslab)
 #define RP_G8_LAUNCH(AKV, BKV, MODEV, GRID) RP_G8_LAUNCH1(AKV, BKV, MODEV, 256, GRID)
+  if (bn == 128) {  // 256 x 128 tiles (MODE 0 only)
+    const dim3 grid((unsigned)(((M + 255) / 256) * ((N + 127) / 128)));
+    if (ak && bk)
+      hipLaunchKernelGGL((gemm8_kernel<true, true, TC, 0, 128>), grid, dim3(NT8), 0, s, M, N, K, a, lda, b, ldb, c, ldc,
+                         alpha, ep, kchunk, bslab);
+    else if (ak && !bk)
+      hipLaunchKernelGGL((gemm8_kernel<true, false, TC, 0, 128>), grid, dim3(NT8), 0, s, M, N, K, a, lda, b, ldb, c,
+                         ldc, alpha, ep, kchunk, bslab);
+    else {
+      rp_set_error("rp_gemm: 256 x 128 tiles need a k-major A");
+      return RP_ERR_ARG;
+    }
+    return rp_check_launch("rp_gemm");
+  }
   if constexpr (!std::is_same<TC, float>::value) {
     if (splits == 0 && ak && !bk && ep.gate && ep.gate_bf16) {  // the linear2 dgrad: see GATEB
       hipLaunchKernelGGL((gemm8_kernel<true, false, TC, 0, 256, true>), dim3((unsigned)tiles), dim3(NT8), 0, s, M, N, K,
