@@ -396,6 +396,29 @@ def test_attention_split_workgroups(dev, monkeypatch, p, split):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("T", [200, 130])
+def test_attention_split3_short_ranges(dev, monkeypatch, T):
+    """The three-part forward when a part gets no key tile (T = 200: 4 tiles -> 2 + 2 + 0; T = 130:
+    3 tiles -> 1 + 1 + 1), on the 128-row LDS-DMA path (B = 16: 256 blocks): keep bits bitwise and
+    outputs within bf16 rounding of the unsplit kernel."""
+    B, H, p, seed = 16, 8, 0.1, 5
+    qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(torch.bfloat16)
+    kv = torch.ones(B, T, dtype=torch.uint8, device=dev)
+    kv[1, T - 37:] = 0
+    kv[2, 64:] = 0  # no valid key past the first tile: the later parts are empty in the merge
+    res = {}
+    for flag in ("3", "0"):
+        monkeypatch.setenv("RP_ATTN_SPLIT", flag)
+        res[flag] = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed)
+    (o3, l3, m3), (o0, l0, m0) = res["3"], res["0"]
+    KT, ldm = (T + 63) // 64, (T + 255) // 256 * 256
+    valid = lambda m: m.view(B * H, KT, 4, ldm)[..., :T]  # noqa: E731 (rows past T are never written)
+    assert torch.equal(valid(m3), valid(m0))
+    close(o3, o0.double(), atol=1e-2, rtol=1e-2, what=f"split3 vs unsplit T={T}")
+    assert (l3 - l0).abs().max().item() < 5e-3
+
+
+@pytest.mark.gpu
 def test_attention_kv32_option(dev, monkeypatch):
     """RP_ATTN_KV32=1 (the 32x32x16 dK/dV kernel): ragged lengths down to one valid key, dropout, the
     128-key-block path; dQ bitwise the default path's (same dQ kernel), dK / dV within bf16 rounding of
