@@ -633,6 +633,11 @@ constexpr int dma_tile_lds() {
   return MAIN > EPI ? MAIN : EPI;
 }
 
+#ifdef RP_GEMM_PROBE
+constexpr int RP_PROBE_MAX = 8192;
+__device__ uint64_t g_gemm_probe[RP_PROBE_MAX * 4];
+#endif
+
 template <bool AK, bool BKM, typename TC, int MODE, int CFG, bool RESB = false, int MI = 4>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t N, int64_t K,
                                                               const bf16* __restrict__ A, int64_t lda,
@@ -666,11 +671,27 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
   float bacc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+#ifdef RP_GEMM_PROBE
+  const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
   dma_mainloop<AK, BKM, CFG, MI>(A, lda, M, B, ldb, N, m0, n0, kbeg, kend, want_bias, acc, bacc, lds, tid, lane, wid,
                                  wm, wn);
+#ifdef RP_GEMM_PROBE
+  const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
   gemm_epilogue<TC, MODE, D::HALVES, RESB, MI>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep,
                                                split);
   if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab, split);
+#ifdef RP_GEMM_PROBE
+  // tuning build only (never the shipping library): per-workgroup phase stamps of wave 0 at the
+  // 100 MHz real-time counter, stored by lanes 0..3 (vector stores)
+  const uint64_t ts2 = __builtin_amdgcn_s_memrealtime();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint64_t ts3 = __builtin_amdgcn_s_memrealtime();
+  const int bid = blockIdx.x + blockIdx.y * gridDim.x;
+  if (wid == 0 && lane < 4 && bid < RP_PROBE_MAX)
+    g_gemm_probe[bid * 4 + lane] = lane == 0 ? ts0 : lane == 1 ? ts1 : lane == 2 ? ts2 : ts3;
+#endif
 }
 
 // ============ grouped weight gradients: many (dY, X) pairs over the same token range ============
@@ -2137,3 +2158,10 @@ extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   hipLaunchKernelGGL(gemm_ln_bwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
   return rp_check_launch("rp_gemm_ln_bwd");
 }
+
+#ifdef RP_GEMM_PROBE
+extern "C" int rp_debug_gemm_probe(uint64_t* host, int n) {
+  if (n > RP_PROBE_MAX * 4) n = RP_PROBE_MAX * 4;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_probe), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
