@@ -25,6 +25,39 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _heartbeat(request, msg):
+    """A progress line on the terminal, past pytest's capture: a long multi-process test is not then
+    taken for a hang by a runner that watches the output."""
+    capman = request.config.pluginmanager.getplugin("capturemanager")
+    with capman.global_and_fixture_disabled():
+        print(f"\n[{msg}]", flush=True)
+
+
+def _wait(q, p, request, name, limit, trace=None):
+    """The worker's (status, result), polling every 20 s with a progress line; ("timeout", log tail)
+    when it has not answered within ``limit`` seconds or died without answering."""
+    import queue
+    import time
+    t0 = time.time()
+    try:
+        while True:
+            try:
+                return q.get(timeout=20)
+            except queue.Empty:
+                log = ""
+                if trace and os.path.exists(trace):
+                    with open(trace) as f:
+                        log = f.read()
+                if time.time() - t0 > limit or not p.is_alive():
+                    return "timeout", log[-6000:] or f"{name}: no answer after {time.time() - t0:.0f}s"
+                last = log.strip().splitlines()[-1] if log.strip() else "running"
+                _heartbeat(request, f"{name} {time.time() - t0:.0f}s: {last}")
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -34,14 +67,29 @@ def _port():
 
 
 @pytest.mark.timeout(420)
-def test_bench_two_ranks_gloo(dev):
+def test_bench_two_ranks_gloo(dev, request, tmp_path):
+    import time
     env = dict(os.environ, RP_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.pop("WORLD_SIZE", None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"],
-                       capture_output=True, text=True, env=env, timeout=400, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-4000:]
-    lines = [l for l in r.stdout.strip().splitlines() if l.strip()]
-    assert len(lines) == 1, r.stdout
+    out, err = tmp_path / "bench.out", tmp_path / "bench.err"
+    with open(out, "w") as fo, open(err, "w") as fe:
+        proc = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                                 "--warmup", "1"], stdout=fo, stderr=fe, text=True, env=env, cwd=ROOT)
+        t0 = time.time()
+        while True:
+            try:
+                proc.wait(timeout=20)
+                break
+            except subprocess.TimeoutExpired:
+                if time.time() - t0 > 400:
+                    proc.kill()
+                    proc.wait()
+                    break
+                _heartbeat(request, f"bench.py --gpus 2 (gloo) {time.time() - t0:.0f}s")
+    stdout, stderr = out.read_text(), err.read_text()
+    assert proc.returncode == 0, stderr[-4000:]
+    lines = [l for l in stdout.strip().splitlines() if l.strip()]
+    assert len(lines) == 1, stdout
     res = json.loads(lines[0])
     print({k: res[k] for k in ("value", "ms_per_step", "n_gpus", "ranks_seen", "param_checksums", "execution")})
     assert res["n_gpus"] == 2 and res["ranks_seen"] == 2
@@ -94,7 +142,7 @@ def _tiling_worker(port, q, cases):
 
 
 @pytest.mark.timeout(300)
-def test_dp_buckets_tile_the_gradient_buffer(dev):
+def test_dp_buckets_tile_the_gradient_buffer(dev, request):
     cases = [("tile cut (default)", "bf16", {}),
              ("8-layer groups", "bf16", {"RP_WGRAD_GROUP_LAYERS": "8"}),
              ("4-layer groups", "bf16", {"RP_WGRAD_GROUP_LAYERS": "4"}),
@@ -105,12 +153,7 @@ def test_dp_buckets_tile_the_gradient_buffer(dev):
     q = ctx.Queue()
     p = ctx.Process(target=_tiling_worker, args=(_port(), q, cases))
     p.start()
-    try:
-        status, res = q.get(timeout=280)
-    finally:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
+    status, res = _wait(q, p, request, "bucket tiling worker", 240)
     assert status == "ok", res
     for name, n, launched in res:
         assert launched, name
@@ -123,8 +166,19 @@ def test_dp_buckets_tile_the_gradient_buffer(dev):
         print(f"{name}: {len(launched)} buckets")
 
 
-def _captured_worker(q):
+def _captured_worker(q, trace):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import faulthandler
+    import time
+    tf = open(trace, "w", buffering=1)
+    t0 = time.time()
+
+    def mark(stage):  # stage log (stacks on stderr every 30 s) for a run that does not finish
+        tf.write(f"{time.time() - t0:7.1f}s {stage}\n")
+        sys.stderr.write(f"[captured worker] {time.time() - t0:7.1f}s {stage}\n")
+        sys.stderr.flush()
+
+    faulthandler.dump_traceback_later(30, repeat=True, file=sys.stderr)
     try:
         import torch.distributed as dist
         from repurpose_amd.distributed import GradAllReducer
@@ -134,7 +188,9 @@ def _captured_worker(q):
         from tests.test_model_gpu import TRI, make_batch, to_dev
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
+        mark("init_process_group")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        mark("process group up")
         cfg = dict(TRI, self_num_layers=16)
         batches = [{k: v for k, v in to_dev(make_batch(cfg, 2, 128, [128, 100], seed=40 + i), dev).items()
                     if torch.is_tensor(v)} for i in range(4)]
@@ -146,18 +202,23 @@ def _captured_worker(q):
             return m, FusedAdam(m, lr=1e-3, weight_decay=1e-4), GradAllReducer(m)
 
         me, oe, re_ = fresh()
-        for b in batches:
+        for i, b in enumerate(batches):
             oe.zero_grad()
             (me.losses(*me(b))["cls_loss"] / 2).backward()
             re_.wait()
             oe.step()
+            torch.cuda.synchronize()
+            mark(f"eager DP step {i}")
         mg, og, rg = fresh()
         run = CapturedTrainStep(mg, og, {k: v.clone() for k, v in batches[0].items()}, warmup=1,
                                 capture_collectives=True)
-        for b in batches:
+        torch.cuda.synchronize()
+        mark("captured")
+        for i, b in enumerate(batches):
             run.load(b)
             run.step()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            mark(f"replay {i}")
         n = me.trainable_numel()
         ok = (run._graph is not None, len(rg.launched) > 0,
               torch.equal(mg.flat_params()[:n], me.flat_params()[:n]),
@@ -167,23 +228,21 @@ def _captured_worker(q):
         import traceback
         q.put(("err", traceback.format_exc()))
     finally:
+        faulthandler.cancel_dump_traceback_later()
         import torch.distributed as dist
         if dist.is_initialized():
             dist.destroy_process_group()
+        mark("done")
 
 
 @pytest.mark.timeout(300)
-def test_captured_rccl_dp_step_equals_eager_dp(dev):
+def test_captured_rccl_dp_step_equals_eager_dp(dev, tmp_path, request):
+    trace = str(tmp_path / "captured_worker.log")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_captured_worker, args=(q,))
+    p = ctx.Process(target=_captured_worker, args=(q, trace))
     p.start()
-    try:
-        status, res = q.get(timeout=280)
-    finally:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
+    status, res = _wait(q, p, request, "captured DP worker", 240, trace)
     assert status == "ok", res
     captured, hooked, params, m1, m2 = res
     assert captured, "the DP step was not captured"
