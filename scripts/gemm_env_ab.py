@@ -2,8 +2,9 @@
 K = 2048; M = 16384, N = 512, bias, dropout 0.1, fp32 residual) in ONE process: each variant's 20
 launches are captured as a HIP graph under its own env value (the launcher reads the switch per
 launch), the graphs replay interleaved over several rounds, and the outputs are compared bit for bit.
-Tuning aid, not product.  usage: python scripts/gemm_env_ab.py [VAR] [A] [B]  (default RP_GEMM_CFG 0 1; round 4 measured the
-removed RP_GEMM_RESPRE switch with it)"""
+Tuning aid, not product.  usage: python scripts/gemm_env_ab.py [VAR] [A] [B]  (default RP_GEMM_BM64 0 1: 128- vs
+64-row tiles; the switch must be one the launcher reads per call.  Round 4 measured the removed
+RP_GEMM_RESPRE switch with it)"""
 import os
 import sys
 
@@ -14,7 +15,7 @@ from repurpose_amd import kernels as K  # noqa: E402
 
 
 def main():
-    var, va, vb = (sys.argv[1:4] + ["RP_GEMM_CFG", "0", "1"][len(sys.argv[1:4]):])[:3]
+    var, va, vb = (sys.argv[1:4] + ["RP_GEMM_BM64", "0", "1"][len(sys.argv[1:4]):])[:3]
     dev = torch.device("cuda:0")
     M, N = 16384, 512
     g = torch.Generator().manual_seed(0)
