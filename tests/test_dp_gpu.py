@@ -29,6 +29,9 @@ def _heartbeat(request, msg):
     """A progress line on the terminal, past pytest's capture: a long multi-process test is not then
     taken for a hang by a runner that watches the output."""
     capman = request.config.pluginmanager.getplugin("capturemanager")
+    if capman is None:  # capture disabled (-p no:capture): plain print reaches the terminal
+        print(f"\n[{msg}]", flush=True)
+        return
     with capman.global_and_fixture_disabled():
         print(f"\n[{msg}]", flush=True)
 
