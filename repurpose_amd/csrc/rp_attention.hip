@@ -2053,7 +2053,10 @@ constexpr int QD_TKMAX = 8192;
 // the second half of the key tiles on a ring of their own; both halves form the prologue's row
 // constants (half 0 writes delta), the dQ partials are added through LDS (half 0 stores query rows
 // qt = 0, half 1 qt = 1; own + partner on either side)
-template <bool DROP, int SPL = 1>
+// FD = false: delta was formed by attn_delta_kernel beforehand (the dQ kernel then runs beside the
+// dK/dV kernel instead of before it); the row constants -delta/ds are read from its plane 1 and no O
+// rows are loaded
+template <bool DROP, int SPL = 1, bool FD = true>
 __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDev a) {
   constexpr int QT = 2, QB = NW * 16 * QT;  // 128 queries per workgroup
   using C = AttnCfg<bf16>;
@@ -2103,6 +2106,7 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDe
     for (int s2 = 0; s2 < 2; ++s2) {
       qf[qt][s2] = row_frag_gmem(Qg, ldq, q0 + qt * 16, Tq, s2 * 32, lane);
       df[qt][s2] = row_frag_gmem(dOg, lddo, q0 + qt * 16, Tq, s2 * 32, lane);
+      if constexpr (!FD) continue;
       const bf16x8 of = row_frag_gmem((const bf16*)a.out + (int64_t)b * Tq * a.ldo + h * HD, a.ldo, q0 + qt * 16, Tq,
                                       s2 * 32, lane);
       if (a.out_lo) {  // O = hi + lo: delta from the unrounded output (exact rowsum(dO * O))
@@ -2115,10 +2119,14 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDe
         for (int j = 0; j < 8; ++j) part += (float)df[qt][s2][j] * (float)of[j];
       }
     }
+    const int64_t plane = (int64_t)B * H * Tq;
+    if constexpr (!FD) {
+      dq[qt] = q < Tq ? a.delta[plane + (int64_t)bh * Tq + q] : 0.f;  // -delta/ds, precomputed
+      continue;
+    }
     const float dl = quad_sum(part);
     dq[qt] = q < Tq ? -dl * (DROP ? 1.f / drop_scale : 1.f) : 0.f;
     if (g == 0 && q < Tq && hv == 0) {  // delta and the dK/dV kernel's row constants (planes 1, 2)
-      const int64_t plane = (int64_t)B * H * Tq;
       a.delta[(int64_t)bh * Tq + q] = dl;
       a.delta[plane + (int64_t)bh * Tq + q] = dq[qt];
       a.delta[2 * plane + (int64_t)bh * Tq + q] = -lq[qt];
@@ -4042,7 +4050,20 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     }
   }
   if ((phases & 4) && !fused) {
-    if (small)
+    const dim3 grid((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
+    if (!small && std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX && attn_dma_q_enabled() && !attn_dq32_enabled()) {
+      // bf16, 128-query blocks, delta formed beforehand: the LDS-DMA dQ kernel reading it
+      if (attn_split((int64_t)grid.x, (a.Tk + FW_KT - 1) / FW_KT)) {
+        if (a.drop_thresh)
+          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 2, false>), grid, dim3(2 * NT), 0, s, a);
+        else
+          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false, 2, false>), grid, dim3(2 * NT), 0, s, a);
+      } else if (a.drop_thresh) {
+        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 1, false>), grid, dim3(NT), 0, s, a);
+      } else {
+        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false, 1, false>), grid, dim3(NT), 0, s, a);
+      }
+    } else if (small)
       launch_bwd_q<T, 1>(false, a, s);
     else
       launch_bwd_q<T, 2>(false, a, s);

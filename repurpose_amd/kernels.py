@@ -409,6 +409,18 @@ def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, q_prescaled=
 
 
 _FUSED_DELTA = os.environ.get("RP_ATTN_FUSED_DELTA", "1") != "0"
+# dQ beside dK/dV: delta first (its own small pass), then the dQ kernel on a side stream concurrently
+# with the dK/dV kernel on the launch stream, so each kernel's last partial round of workgroups
+# is filled by the other's (both grids are 4/3 of the CUs' three-per-CU residency at the metric shape)
+_BWD_OVERLAP = os.environ.get("RP_ATTN_BWD_OVERLAP", "0") == "1"
+_SIDE = {}
+
+
+def _side_stream(dev):
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
 
 
 def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, dropmask=None,
@@ -422,6 +434,24 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
     delta = torch.empty(3, B, H, T, device=qkv.device, dtype=torch.float32)  # delta + 2 row-constant planes
     st, dt = _stream(qkv), _adt(qkv, q_prescaled)
     e0 = _tick("attn_bwd")
+    if _BWD_OVERLAP:
+        N.call("rp_attn_bwd_delta", dt, _p(out), _p(out_lo), _p(dout), _p(lse), B, T, H, dk, float(dropout_p),
+               _p(delta), st)
+        main = torch.cuda.current_stream(qkv.device)
+        side = _side_stream(qkv.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            e2 = _tick("attn_bwd_dq")
+            N.call("rp_attn_bwd_dq", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
+                   float(scale), float(dropout_p), _p(dropmask), _p(dqkv), ctypes.c_void_p(side.cuda_stream))
+            _tock(e2)
+        e1 = _tick("attn_bwd_dkdv")
+        N.call("rp_attn_bwd_dkdv", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
+               float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
+        _tock(e1)
+        main.wait_stream(side)  # before any tensor used on the side stream is released or reused
+        _tock(e0)
+        return dqkv
     if _FUSED_DELTA:  # dQ first, with the delta = rowsum(dO * O) pre-pass fused in; dK/dV reads it
         e2 = _tick("attn_bwd_dq")
         N.call("rp_attn_bwd_dq_delta", dt, _p(qkv), _p(out), _p(out_lo), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T,

@@ -784,6 +784,33 @@ def test_attention_metric_shape_bf16_dropout(dev):
         assert torch.count_nonzero(dk[bb, hh][~valid]) == 0 and torch.count_nonzero(dv[bb, hh][~valid]) == 0
 
 
+@pytest.mark.parametrize("B,T", [(8, 2048), (1, 4096)])
+def test_attention_bwd_overlap_matches_sequential(dev, monkeypatch, B, T):
+    """The overlapped backward (delta pass, then the dQ kernel on a side stream beside dK/dV; the dQ
+    kernel reads the precomputed row constants, 128-query and split workgroups) against the sequential
+    one (dQ with the fused delta, then dK/dV) at the bench shape and config 4's, Q prescaled, dropout
+    0.1, ragged keys: the gradients differ only through the rounding of delta (its two producers sum in
+    different orders), and the overlapped form repeats bitwise (no race between the two streams)."""
+    H, p = 8, 0.1
+    qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=31).to(torch.bfloat16)
+    qkv[:, :H * 64] = (qkv[:, :H * 64].float() * (0.125 * K.LOG2E)).to(torch.bfloat16)
+    lens = torch.tensor([T, T - 1, 1900, 1537, T, 1024, 2047, 64][:B], device=dev)
+    kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
+    olo = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 91, q_prescaled=True, out_lo=olo)
+    do = rnd(B * T, H * 64, dev=dev, seed=32).to(torch.bfloat16)
+    outs = {}
+    for mode in (False, True, True):
+        monkeypatch.setattr(K, "_BWD_OVERLAP", mode)
+        r = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True, out_lo=olo)
+        torch.cuda.synchronize()
+        if mode in outs:
+            assert torch.equal(r, outs[mode]), "overlapped backward not repeatable"
+        outs[mode] = r
+    assert torch.isfinite(outs[True]).all()
+    close(outs[True].float(), outs[False].double(), atol=2e-2, rtol=2e-2, what="overlapped vs sequential dqkv")
+
+
 @pytest.mark.parametrize("T", [128, 192, 4096])
 def test_wgrad_grouped_repeat_bitwise(dev, T):
     """Race guard for the 256-row kernel's LDS-DMA pipeline: the grouped weight gradients of the
