@@ -286,6 +286,12 @@ int rp_sumsq_batched(const rp_sumsq_item* items, int n_items, void* stream);
  * backward unchanged.  Without the flag the kernels compute the same bf16(Q * scale * log2 e)
  * themselves (the forward and dQ kernels in registers, the dK/dV kernel as it stages Q tiles). */
 enum { RP_ATTN_Q_PRESCALED = 0x100 };
+/* Also or-ed into the dtype of the backward entry points: keep four-wave workgroups where a grid
+ * that fills the CUs once would otherwise get the eight-wave split ones (config 4: B = 1, T = 4096).
+ * For callers that run the dQ kernel (rp_attn_bwd_dq) beside the dK/dV kernel on another stream:
+ * the two grids then fill the CUs together.  Results are identical either way up to the split
+ * kernels' partial-sum order. */
+enum { RP_ATTN_NO_SPLIT = 0x200 };
 
 /* Multi-head self attention, flash-style (no T x T materialisation).
  * qkv: [B*T, 3*H*dk] rows = (q heads | k heads | v heads), dk == 64.

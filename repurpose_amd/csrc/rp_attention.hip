@@ -94,6 +94,7 @@ struct MhaDev {
   int qpre;  // RP_ATTN_Q_PRESCALED: q holds Q * scale * log2(e) (see include/rp_api.h)
   int empty_uniform;  // a sequence with no valid key attends uniformly to all keys (masked_fill(-1e9))
   uint64_t mwc_jump;  // split forward: A^(8 n) * 2^64 mod M, n = the key tiles of one part (mwc_jump)
+  int nosplit;  // RP_ATTN_NO_SPLIT: the backward keeps four-wave workgroups (dQ runs beside dK/dV)
 };
 
 // MWC64X skip-ahead.  The state S = c * 2^32 + x steps as S' = A * S mod M, M = A * 2^32 - 1, so n
@@ -4028,7 +4029,7 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
           hipLaunchKernelGGL((attn_bwd_kv32_kernel<true>), grid, dim3(NT), 0, s, a);
         else
           hipLaunchKernelGGL((attn_bwd_kv32_kernel<false>), grid, dim3(NT), 0, s, a);
-      } else if (attn_split((int64_t)nkb * a.B * a.H, (a.Tq + KV_QT - 1) / KV_QT)) {
+      } else if (!a.nosplit && attn_split((int64_t)nkb * a.B * a.H, (a.Tq + KV_QT - 1) / KV_QT)) {
         if (a.drop_thresh)
           hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<true, 2, false, 2>), grid, dim3(2 * NT), 0, s, a);
         else
@@ -4053,7 +4054,7 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     const dim3 grid((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
     if (!small && std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX && attn_dma_q_enabled() && !attn_dq32_enabled()) {
       // bf16, 128-query blocks, delta formed beforehand: the LDS-DMA dQ kernel reading it
-      if (attn_split((int64_t)grid.x, (a.Tk + FW_KT - 1) / FW_KT)) {
+      if (!a.nosplit && attn_split((int64_t)grid.x, (a.Tk + FW_KT - 1) / FW_KT)) {
         if (a.drop_thresh)
           hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 2, false>), grid, dim3(2 * NT), 0, s, a);
         else
@@ -4120,7 +4121,7 @@ int make_dev(const char* fn, int dtype, int qpre, const rp_mha_args* p, int phas
 
 // the attention entry points take RP_ATTN_Q_PRESCALED or-ed into their dtype argument
 inline int attn_qpre(int dtype) { return (dtype & RP_ATTN_Q_PRESCALED) ? 1 : 0; }
-inline int attn_dtype(int dtype) { return dtype & ~RP_ATTN_Q_PRESCALED; }
+inline int attn_dtype(int dtype) { return dtype & ~(RP_ATTN_Q_PRESCALED | RP_ATTN_NO_SPLIT); }
 
 int mha_fwd_entry(int flagged, const rp_mha_args* p, void* stream) {
   const int dtype = attn_dtype(flagged);
@@ -4139,6 +4140,7 @@ int mha_bwd_entry(int flagged, const rp_mha_args* p, int phases, void* stream) {
   MhaDev a;
   const int rc = make_dev("rp_mha_bwd", dtype, attn_qpre(flagged), p, phases, a);
   if (rc) return rc;
+  a.nosplit = (flagged & RP_ATTN_NO_SPLIT) ? 1 : 0;
   if (a.B == 0 || a.Tq == 0 || a.Tk == 0) return RP_OK;
   hipStream_t s = (hipStream_t)stream;
   return dtype == RP_BF16 ? launch_mha_bwd<bf16>(phases, a, s) : launch_mha_bwd<float>(phases, a, s);

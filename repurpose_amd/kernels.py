@@ -13,6 +13,7 @@ from . import _native as N
 
 _DT = {torch.float32: N.RP_F32, torch.bfloat16: N.RP_BF16}
 RP_ATTN_Q_PRESCALED = 0x100  # include/rp_api.h: q holds Q * scale * log2(e)
+RP_ATTN_NO_SPLIT = 0x200  # include/rp_api.h: four-wave backward workgroups (dQ runs beside dK/dV)
 LOG2E = 1.4426950408889634
 
 
@@ -413,6 +414,9 @@ _FUSED_DELTA = os.environ.get("RP_ATTN_FUSED_DELTA", "1") != "0"
 # with the dK/dV kernel on the launch stream, so each kernel's last partial round of workgroups
 # is filled by the other's (both grids are 4/3 of the CUs' three-per-CU residency at the metric shape)
 _BWD_OVERLAP = os.environ.get("RP_ATTN_BWD_OVERLAP", "0") == "1"
+# overlapped form on grids that fill the CUs once (config 4): the two four-wave grids side by side
+# instead of the eight-wave split workgroups (RP_ATTN_OVL_SPLIT=1 keeps those)
+_OVL_NOSPLIT = os.environ.get("RP_ATTN_OVL_SPLIT", "0") != "1"
 _SIDE = {}
 
 
@@ -435,6 +439,8 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
     st, dt = _stream(qkv), _adt(qkv, q_prescaled)
     e0 = _tick("attn_bwd")
     if _BWD_OVERLAP:
+        if _OVL_NOSPLIT:
+            dt |= RP_ATTN_NO_SPLIT
         N.call("rp_attn_bwd_delta", dt, _p(out), _p(out_lo), _p(dout), _p(lse), B, T, H, dk, float(dropout_p),
                _p(delta), st)
         main = torch.cuda.current_stream(qkv.device)
