@@ -209,6 +209,90 @@ class DistributedModel(nn.Module):
         return self.module(*args, **kwargs)
 
 
+def _split_batch(batch, n):
+    """Per-replica pieces of a batch dict: every tensor cut along dim 0 as ``torch.chunk`` cuts it
+    (nn.DataParallel's scatter: ceil-sized pieces, fewer when the batch is short); other values are
+    shared.  Returns the list of piece dicts (at most n)."""
+    sizes = {v.shape[0] for v in batch.values() if torch.is_tensor(v) and v.dim() > 0}
+    if len(sizes) != 1:
+        raise ValueError(f"DataParallelModel: batch tensors disagree on dim 0 ({sorted(sizes)})")
+    B = sizes.pop()
+    step = -(-B // max(1, min(n, B)))
+    starts = list(range(0, B, step))
+    return [{k: (v[s:s + step] if torch.is_tensor(v) and v.dim() > 0 else v) for k, v in batch.items()}
+            for s in starts]
+
+
+class DataParallelModel(nn.Module):
+    """``strategy: dp`` (reference ``utils/distributed.py:409-413``, ``nn.DataParallel``): one
+    process drives several GPUs.  The batch is cut along dim 0 (``_split_batch``), replica i runs its
+    piece on ``device_ids[i]``, the six outputs are gathered onto ``output_device`` along dim 0 (with
+    autograd, ``torch.nn.parallel.gather``), so ``.module.losses(*out)`` and ``loss.backward()`` read
+    as the reference trainer's (``main.py:323-326``) and the gradient is that of the whole batch.
+
+    Underneath, not ``nn.DataParallel``'s per-forward module replication: the replicas are built once
+    (flat-buffer models, ``MMCTransformer._build_flat``) and refreshed by one device-to-device copy of
+    the flat fp32 parameters per forward; their flat gradients are summed into ``.module``'s with one
+    copy + add each, queued on the autograd engine to run once the whole backward is done (every
+    replica's HIP backward has written its buffer by then).  A ``device_ids`` entry may repeat (two
+    replicas on one GPU: how the one-GPU box tests this path)."""
+
+    def __init__(self, module, device_ids=None, output_device=None):
+        super().__init__()
+        if device_ids is None:
+            device_ids = list(range(torch.cuda.device_count()))
+        if not device_ids:
+            raise RuntimeError("DataParallelModel: no GPU")
+        self.device_ids = [torch.device("cuda", d) if isinstance(d, int) else torch.device(d) for d in device_ids]
+        self.output_device = self.device_ids[0] if output_device is None else torch.device(
+            "cuda", output_device) if isinstance(output_device, int) else torch.device(output_device)
+        self.module = module.to(self.device_ids[0])
+        self._replicas = []  # replicas 1.. (plain list: not sub-modules, so state_dict / parameters are .module's)
+        self._queued = False
+
+    def _replica(self, i):
+        import copy
+        while len(self._replicas) < i:
+            j = len(self._replicas) + 1
+            r = copy.deepcopy(self.module).to(self.device_ids[j])
+            r._grad_ready_hooks = []
+            r._grad_done_hooks = [self._on_replica_done]
+            self._replicas.append(r)
+        return self._replicas[i - 1]
+
+    def _on_replica_done(self):
+        if not self._queued:  # once per backward: after the engine has run every replica's backward
+            self._queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._reduce)
+
+    def _reduce(self):
+        self._queued = False
+        g0 = self.module.flat_grads()
+        n = self.module.trainable_numel()
+        for r in self._active:
+            g0[:n].add_(r.flat_grads()[:n].to(g0.device))
+
+    def forward(self, batch):
+        pieces = _split_batch(batch, len(self.device_ids))
+        if len(pieces) == 1:
+            return self.module({k: v.to(self.device_ids[0]) if torch.is_tensor(v) else v for k, v in batch.items()})
+        src = self.module.flat_params()
+        self._active = []
+        outs = []
+        for i, piece in enumerate(pieces):
+            dev = self.device_ids[i]
+            m = self.module if i == 0 else self._replica(i)
+            if i:
+                m.train(self.module.training)
+                with torch.no_grad():
+                    m.flat_params().copy_(src)
+                    m.flat_grads().zero_()
+                self._active.append(m)
+            with torch.cuda.device(dev):
+                outs.append(m({k: v.to(dev, non_blocking=True) if torch.is_tensor(v) else v for k, v in piece.items()}))
+        return tuple(torch.nn.parallel.gather(outs, self.output_device, dim=0))
+
+
 class MultiGPUStrategy:
     """Reference ``utils/distributed.py:242-625`` with RCCL underneath."""
 
@@ -239,12 +323,9 @@ class MultiGPUStrategy:
         return "ddp" if torch.cuda.device_count() > 1 else "single"
 
     def _setup_device_info(self):
-        """Reference :313-353.  'dp' (nn.DataParallel in the reference, :409-413) runs on one device:
-        a single process cannot replicate the flat-buffer model across GPUs, and one process per GPU
-        (ddp) is the MI355X path — a documented divergence, with a warning."""
+        """Reference :313-353.  'dp' (nn.DataParallel in the reference, :409-413): one process on
+        cuda:0 that ``wrap_model`` spreads over every visible GPU (``DataParallelModel``)."""
         if self.strategy in ("single", "dp"):
-            if self.strategy == "dp":
-                self.logger.warning("strategy 'dp' runs single-device on MI355X; launch one process per GPU")
             self.device = get_device()
             self.world_size, self.rank, self.local_rank = 1, 0, 0
             return
@@ -283,6 +364,8 @@ class MultiGPUStrategy:
 
     def wrap_model(self, model: nn.Module) -> nn.Module:
         model = model.to(self.device)
+        if self.strategy == "dp" and torch.cuda.is_available() and torch.cuda.device_count() > 1:
+            return DataParallelModel(model)
         if self.strategy == "ddp" and self.world_size > 1:
             return DistributedModel(model)
         return model

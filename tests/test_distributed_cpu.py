@@ -136,16 +136,30 @@ def test_detect_slurm_env_reference_priority(monkeypatch):
     assert detect_slurm_env() == {"is_slurm": False}  # torchrun's variables take priority
 
 
-def test_dp_strategy_is_single_device_with_warning(caplog):
-    """'dp' (nn.DataParallel in the reference, utils/distributed.py:409-413) runs on one device here:
-    the documented divergence — one process per GPU (ddp) is the multi-GPU path."""
+def test_dp_strategy_one_process(monkeypatch):
+    """'dp' (nn.DataParallel in the reference, utils/distributed.py:409-413): one process, world 1;
+    wrap_model returns a DataParallelModel only with more than one GPU (the reference's condition,
+    :409), otherwise the model itself (here: no GPU)."""
     from repurpose_amd.distributed import MultiGPUStrategy
-    with caplog.at_level("WARNING"):
-        s = MultiGPUStrategy(strategy="dp")
+    s = MultiGPUStrategy(strategy="dp")
     assert s.strategy == "dp" and s.world_size == 1 and not s.is_distributed
-    assert any("single-device" in r.getMessage() for r in caplog.records)
+    assert s.get_effective_batch_size(4) == 4  # reference :604, the whole batch on each step
     m = torch.nn.Linear(2, 2)
     assert s.wrap_model(m) is m
+
+
+def test_dp_batch_split_like_scatter():
+    """DataParallelModel's batch cut: torch.chunk along dim 0 (nn.DataParallel's scatter) — ceil-sized
+    pieces, fewer pieces than devices when the batch is short, non-tensor values shared."""
+    from repurpose_amd.distributed import _split_batch
+    b = {"x": torch.arange(5 * 3).view(5, 3), "m": torch.ones(5, 1, 4, dtype=torch.bool), "tag": "v"}
+    pieces = _split_batch(b, 2)
+    assert [p["x"].shape[0] for p in pieces] == [3, 2]
+    assert torch.equal(torch.cat([p["x"] for p in pieces]), b["x"]) and all(p["tag"] == "v" for p in pieces)
+    assert [p["m"].shape[0] for p in _split_batch(b, 8)] == [1] * 5
+    assert [p["x"].shape[0] for p in _split_batch(b, 4)] == [c.shape[0] for c in torch.chunk(b["x"], 4)]
+    with pytest.raises(ValueError):
+        _split_batch({"x": torch.zeros(2, 1), "y": torch.zeros(3, 1)}, 2)
 
 
 def test_single_strategy_passthrough():

@@ -135,3 +135,57 @@ def test_ddp_two_ranks_real_backward(dev, dtype):
                 p.kill()
     bad = [f"rank {rank}: {msg}" for rank, msg in sorted(res) if msg != "ok"]
     assert not bad, "\n".join(bad)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_dp_strategy_replicas_sum_to_whole_batch(dev, dtype):
+    """``strategy: dp`` (reference utils/distributed.py:409-413, nn.DataParallel): DataParallelModel
+    cuts the batch along dim 0, runs one replica per device entry and gathers the outputs, so the
+    trainer's ``model.module.losses(*out)`` / ``backward()`` give the whole batch's loss and gradient.
+    Two replicas share the box's one GPU (device_ids [0, 0]); checked against the plain model on the
+    whole batch over two optimizer steps (replica parameters refreshed, replica gradients re-zeroed)."""
+    from repurpose_amd.distributed import DataParallelModel
+    from repurpose_amd.MMCTransformer import MMCTransformer
+    from repurpose_amd.optim import FusedAdam
+    torch.manual_seed(7)
+    ref = MMCTransformer(**CFG, compute_dtype=dtype).to(dev).train()
+    ref.DROPOUT = 0.0
+    m = MMCTransformer(**CFG, compute_dtype=dtype)
+    m.load_state_dict(ref.state_dict())
+    m.DROPOUT = 0.0
+    w = DataParallelModel(m, device_ids=[0, 0])
+    w.train()
+    opt_ref = FusedAdam(ref.parameters(), lr=1e-3, weight_decay=1e-4)
+    opt = FusedAdam(w.parameters(), lr=1e-3, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(11)
+    B, T = 3, 128  # odd: pieces of 2 and 1 sequences
+    n = m.trainable_numel()
+    for step in range(2):
+        full = _batch(seed=20 + step)
+        full = {k: torch.cat([v, v[:1]]) for k, v in full.items()}  # B = 3
+        full["visual_feats"][2] += 0.1 * torch.randn(T, 512, generator=g)
+        batch = {k: v.to(dev) for k, v in full.items()}
+        opt_ref.zero_grad()
+        o_ref = ref(batch)
+        l_ref = ref.losses(*o_ref)["cls_loss"] / B
+        l_ref.backward()
+        opt.zero_grad()
+        out = w(batch)
+        assert len(out) == 6 and out[1].shape == o_ref[1].shape and out[1].device == dev
+        loss = w.module.losses(*out)["cls_loss"] / B
+        loss.backward()
+        torch.cuda.synchronize()
+        tol = 1e-5 if dtype == "fp32" else 2e-2
+        assert abs(loss.item() - l_ref.item()) <= tol * max(1.0, abs(l_ref.item())), (loss.item(), l_ref.item())
+        ga, gb = m.flat_grads()[:n], ref.flat_grads()[:n]
+        rel = ((ga - gb).abs().max() / gb.abs().max()).item()
+        assert rel < (1e-5 if dtype == "fp32" else 3e-2), f"step {step}: dp gradient rel err {rel:.2e}"
+        opt.step()
+        opt_ref.step()
+    torch.cuda.synchronize()
+    # Adam moves a parameter by up to lr per step whatever its gradient's size, so near-zero gradients
+    # whose sign differs between the two summation orders move apart by up to 2 lr per step; the
+    # replica refresh itself is what the second step's gradient check above covers
+    drift = (m.flat_params() - ref.flat_params()).abs().max().item()
+    assert drift <= 4 * 1e-3 * 1.01, drift
