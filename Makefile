@@ -15,11 +15,6 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -Wall -Wno-unu
 # 0..40 measured alike; 20 kept) schedules the tile loops for latency: fwd p=0.1 160 -> 150 us,
 # bwd p=0.1 310 -> 301 us, p=0 fwd 119 -> 112 us, bwd 299 -> 286 us (interleaved runs, one box)
 build/rp_attention.o: EXTRA := -fno-honor-nans -fno-slp-vectorize -mllvm -amdgpu-schedule-metric-bias=20
-# GEMMs: no SLP packing of the epilogue arithmetic either — bitwise the same outputs (same parameter
-# checksums after a step), step 15.21 -> 15.16 ms (mean of six interleaved bench runs each, round 4,
-# scripts/ab_libs_bench.sh); the machine-scheduler bias on top of it and the same flag on the
-# LayerNorm / elementwise kernels measured within noise (the latter changes their rounding: not kept)
-build/rp_gemm.o: EXTRA := -fno-slp-vectorize
 
 all: $(LIB)
 
