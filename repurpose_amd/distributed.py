@@ -351,9 +351,9 @@ class MultiGPUStrategy:
             addr = s["master_addr"] if s["is_slurm"] else os.environ.get("MASTER_ADDR", "127.0.0.1")
             port = str(s["master_port"]) if s["is_slurm"] else os.environ.get("MASTER_PORT")
             ok = setup_distributed(self.rank, self.world_size, self.backend, addr, port, self.timeout)
-            if not ok:  # reference falls back and reports success (:379-386)
-                self.logger.warning("DDP setup failed, continuing on a single device")
-                self.strategy, self.is_distributed, self.world_size, self.rank = "single", False, 1, 0
+            if not ok:  # reference falls back to DataParallel and reports success (:379-386)
+                self.logger.warning("DDP setup failed, falling back to DataParallel")
+                self.strategy, self.is_distributed, self.world_size, self.rank = "dp", False, 1, 0
                 return True
             return True
         return True

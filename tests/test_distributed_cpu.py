@@ -148,6 +148,20 @@ def test_dp_strategy_one_process(monkeypatch):
     assert s.wrap_model(m) is m
 
 
+def test_ddp_setup_failure_falls_back_to_dp(monkeypatch, caplog):
+    """Reference utils/distributed.py:379-386: a failed DDP init falls back to DataParallel, world 1,
+    and setup() still reports success."""
+    import repurpose_amd.distributed as D
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(D, "setup_distributed", lambda *a, **k: False)
+    s = D.MultiGPUStrategy(strategy="ddp", backend="gloo")
+    with caplog.at_level("WARNING"):
+        assert s.setup() is True
+    assert s.strategy == "dp" and s.world_size == 1 and s.rank == 0 and not s.is_distributed
+    assert any("falling back to DataParallel" in r.getMessage() for r in caplog.records)
+
+
 def test_dp_batch_split_like_scatter():
     """DataParallelModel's batch cut: torch.chunk along dim 0 (nn.DataParallel's scatter) — ceil-sized
     pieces, fewer pieces than devices when the batch is short, non-tensor values shared."""
