@@ -1134,12 +1134,15 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// one ring slot of the dK/dV kernel: Q and dO images of a query tile plus four 1 KB side regions
+constexpr int KV_DMA_BUF = 2 * KV_QT * AttnCfg<bf16>::ROWB + 4 * 1024;
+
 // SPL = 2 (grids that fill the CUs only once: config 4, B = 1, T = 4096): eight waves, waves 4-7 run
 // the same key block over the second half of the query tiles on a ring of their own, and the two
 // halves' dK / dV partials are added through LDS at the end (dK = own + partner on half 0, which stores
 // dK; dV likewise on half 1) — two waves per SIMD where one 4-wave workgroup per CU had one
 template <bool DROP, int KTW, bool PIPE, int SPL = 1>
-__global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_kv_dma_kernel(MhaDev a) {
+__device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int blk, char* lds) {
   constexpr int KB = NW * 16 * KTW;  // keys per workgroup
   using C = AttnCfg<bf16>;
   constexpr int TILE = KV_QT * C::ROWB;
@@ -1153,9 +1156,10 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_kv_dma_kernel(MhaD
   constexpr int NBUF = 3;
   // three separate arrays rather than one indexed ring: every LDS address of a step is then a per-lane
   // base plus an immediate offset
-  __shared__ __attribute__((aligned(1024))) char ring0[SPL * BUF];
-  __shared__ __attribute__((aligned(1024))) char ring1[SPL * BUF];
-  __shared__ __attribute__((aligned(1024))) char ring2[SPL * BUF];
+  static_assert(BUF == KV_DMA_BUF, "KV_DMA_BUF out of date");
+  char* const ring0 = lds;  // the caller's LDS: three slots at 1 KB-aligned constant offsets
+  char* const ring1 = lds + SPL * BUF;
+  char* const ring2 = lds + 2 * SPL * BUF;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wq = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int w = wq & (NW - 1);                // wave within its query half
@@ -1167,7 +1171,7 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_kv_dma_kernel(MhaD
   const float drop_scale = a.drop_scale;
   const uint16_t* __restrict__ dmask = a.dmask;
   const int nkb = (Tk + KB - 1) / KB;
-  const int L = rp_xcd_remap(blockIdx.x, nkb * B * H);
+  const int L = rp_xcd_remap(blk, nkb * B * H);
   const int bh = L / nkb, kb = L % nkb;
   const int b = bh / H, h = bh % H;
   const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
@@ -1446,6 +1450,12 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_kv_dma_kernel(MhaD
         if (st_v) rp_st(dV + (int64_t)key * a.lddv + dt * 16 + i, ok ? dv[kt][dt][r] : 0.f);
       }
     }
+}
+
+template <bool DROP, int KTW, bool PIPE, int SPL = 1>
+__global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_kv_dma_kernel(MhaDev a) {
+  __shared__ __attribute__((aligned(1024))) char lds[3 * SPL * KV_DMA_BUF];
+  attn_bwd_kv_dma_body<DROP, KTW, PIPE, SPL>(a, blockIdx.x, lds);
 }
 
 // =================================================================================================
@@ -2049,6 +2059,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
 //    rows past Tk (clamped DMA sources) are invalid keys there, so they get P = 0.
 // =================================================================================================
 constexpr int QD_TKMAX = 8192;
+// one ring slot of the dQ kernel (a 64-key K and V image plus 1 KB of keep bits) and its whole LDS
+constexpr int QD_DMA_BUF = 2 * FW_KT * AttnCfg<bf16>::ROWB + 1024;
+constexpr int QD_DMA_LDS(int spl) { return 3 * spl * QD_DMA_BUF + QD_TKMAX + QD_TKMAX / FW_KT * 4; }
 
 // SPL = 2 (grids that fill the CUs once but not twice): eight waves, waves 4-7 the same 128 queries over
 // the second half of the key tiles on a ring of their own; both halves form the prologue's row
@@ -2058,7 +2071,7 @@ constexpr int QD_TKMAX = 8192;
 // dK/dV kernel instead of before it); the row constants -delta/ds are read from its plane 1 and no O
 // rows are loaded
 template <bool DROP, int SPL = 1, bool FD = true>
-__global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDev a) {
+__device__ __forceinline__ void attn_bwd_q_dma_body(const MhaDev& a, const int blk, char* lds) {
   constexpr int QT = 2, QB = NW * 16 * QT;  // 128 queries per workgroup
   using C = AttnCfg<bf16>;
   constexpr int TILE = FW_KT * C::ROWB;  // one 64-key K or V image (8 KB)
@@ -2066,11 +2079,12 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDe
   constexpr int BUF = 2 * TILE + MASKB;
   constexpr int NBUF = 3;
   constexpr int NTS = NT * SPL;
-  __shared__ __attribute__((aligned(1024))) char ring0[SPL * BUF];
-  __shared__ __attribute__((aligned(1024))) char ring1[SPL * BUF];
-  __shared__ __attribute__((aligned(1024))) char ring2[SPL * BUF];
-  __shared__ __attribute__((aligned(16))) uint8_t kvl[QD_TKMAX];
-  __shared__ int kfull[QD_TKMAX / FW_KT];
+  static_assert(BUF == QD_DMA_BUF, "QD_DMA_BUF out of date");
+  char* const ring0 = lds;  // the caller's LDS: three slots, then the key-valid bytes and tile flags
+  char* const ring1 = lds + SPL * BUF;
+  char* const ring2 = lds + 2 * SPL * BUF;
+  uint8_t* const kvl = reinterpret_cast<uint8_t*>(lds + 3 * SPL * BUF);
+  int* const kfull = reinterpret_cast<int*>(lds + 3 * SPL * BUF + QD_TKMAX);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wq = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int w = wq & (NW - 1);            // wave within its key half
@@ -2081,7 +2095,7 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDe
   const float scale = a.scale, drop_scale = a.drop_scale;
   const float* __restrict__ lse = a.lse;
   const int nqb = (Tq + QB - 1) / QB;
-  const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
+  const int L = rp_xcd_remap(blk, nqb * B * H);
   const int bh = L / nqb, qb = L % nqb;
   const int b = bh / H, h = bh % H;
   const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
@@ -2354,6 +2368,29 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDe
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) dQ[(int64_t)q * a.lddq + dt * 16 + i] = (bf16)(dqa[qt][dt][r] * scale);
     }
+}
+
+template <bool DROP, int SPL = 1, bool FD = true>
+__global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDev a) {
+  __shared__ __attribute__((aligned(1024))) char lds[QD_DMA_LDS(SPL)];
+  attn_bwd_q_dma_body<DROP, SPL, FD>(a, blockIdx.x, lds);
+}
+
+// dK/dV and dQ as ONE launch of two workgroup roles, delta formed beforehand (attn_delta_kernel):
+// blocks [0, nkv) run the dK/dV body (128-key blocks), the rest the dQ body reading the precomputed row
+// constants (128-query blocks), on one LDS region sized for the larger.  For grids that fill the CUs
+// once but not twice (config 4, B = 1, T = 4096: 256 blocks each), where the two kernels would each run
+// as eight-wave split workgroups one per CU: here 512 four-wave workgroups two per CU, the dQ blocks
+// beside the dK/dV ones, with no partial merge and no cross-stream wait (RP_ATTN_BWD_OVERLAP: 42-68 us).
+constexpr int ROLES_LDS = 3 * KV_DMA_BUF > QD_DMA_LDS(1) ? 3 * KV_DMA_BUF : QD_DMA_LDS(1);
+template <bool DROP>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_roles_kernel(MhaDev a, int nkv) {
+  __shared__ __attribute__((aligned(1024))) char lds[ROLES_LDS];
+  const int blk = blockIdx.x;
+  if (blk < nkv)
+    attn_bwd_kv_dma_body<DROP, 2, true, 1>(a, blk, lds);
+  else
+    attn_bwd_q_dma_body<DROP, 1, false>(a, blk - nkv, lds);
 }
 
 // =================================================================================================
@@ -3970,10 +4007,35 @@ static bool attn_dq32_enabled() {
   return e && e[0] == '1';
 }
 
+// the two-role backward (attn_bwd_roles_kernel): bf16 with the producer's Q prescale on the LDS-DMA
+// kernels, 128-row blocks on both sides, and both grids in the split range (attn_split); RP_ATTN_ROLES=0
+// keeps the two kernels (read per launch)
+static bool attn_roles(const MhaDev& a) {
+  const char* e = getenv("RP_ATTN_ROLES");
+  if (e && e[0] == '0') return false;
+  if (!a.qpre || a.empty_uniform || a.nosplit || a.Tk > QD_TKMAX || attn_block_override()) return false;
+  if (!attn_dma_enabled() || !attn_dma_q_enabled() || attn_kv32_enabled() || attn_dq32_enabled()) return false;
+  const int64_t gkv = (int64_t)((a.Tk + KV_KB - 1) / KV_KB) * a.B * a.H;
+  const int64_t gq = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H;
+  if (gkv < ATTN_SMALL_GRID || gq < ATTN_SMALL_GRID) return false;
+  return attn_split(gkv, (a.Tq + KV_QT - 1) / KV_QT) && attn_split(gq, (a.Tk + FW_KT - 1) / FW_KT);
+}
+
 template <typename T>
 int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   const int64_t rows = (int64_t)a.B * a.Tq;
   const int nkb = (a.Tk + KV_KB - 1) / KV_KB;
+  if (std::is_same<T, bf16>::value && (phases & 6) == 6 && attn_roles(a)) {
+    if (phases & 1)
+      hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
+    const int nkv = nkb * a.B * a.H;
+    const dim3 grid((unsigned)(nkv + (a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
+    if (a.drop_thresh)
+      hipLaunchKernelGGL(attn_bwd_roles_kernel<true>, grid, dim3(NT), 0, s, a, nkv);
+    else
+      hipLaunchKernelGGL(attn_bwd_roles_kernel<false>, grid, dim3(NT), 0, s, a, nkv);
+    return rp_check_launch("rp_mha_bwd");
+  }
   // dQ: 128-query blocks unless that leaves fewer than one workgroup per CU (then 64, as the forward)
   const bool small = attn_block_override() ? attn_block_override() == 64
                                            : (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H < ATTN_SMALL_GRID;

@@ -458,7 +458,14 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
         main.wait_stream(side)  # before any tensor used on the side stream is released or reused
         _tock(e0)
         return dqkv
-    if _FUSED_DELTA:  # dQ first, with the delta = rowsum(dO * O) pre-pass fused in; dK/dV reads it
+    if _FUSED_DELTA and not ({"attn_bwd_dq", "attn_bwd_dkdv"} & set(_timer["names"])):
+        # one entry: the library launches the fused-delta dQ kernel then dK/dV, or, where each grid
+        # fills the CUs once but not twice (config 4), the delta pass and ONE two-role launch
+        N.call("rp_attn_bwd", dt, _p(qkv), _p(out), _p(out_lo), _p(dout), _p(lse), _p(key_valid), B, T, H, dk,
+               float(scale), float(dropout_p), _p(dropmask), _p(dqkv), _p(delta), st)
+        _tock(e0)
+        return dqkv
+    if _FUSED_DELTA:  # per-kernel timing (bench.py roofline): the two kernels as separate calls  # dQ first, with the delta = rowsum(dO * O) pre-pass fused in; dK/dV reads it
         e2 = _tick("attn_bwd_dq")
         N.call("rp_attn_bwd_dq_delta", dt, _p(qkv), _p(out), _p(out_lo), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T,
                H, dk, float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)

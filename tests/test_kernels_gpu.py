@@ -811,6 +811,37 @@ def test_attention_bwd_overlap_matches_sequential(dev, monkeypatch, B, T):
     close(outs[True].float(), outs[False].double(), atol=2e-2, rtol=2e-2, what="overlapped vs sequential dqkv")
 
 
+@pytest.mark.parametrize("B,T,p", [(1, 4096, 0.1), (1, 4096, 0.0), (2, 2048, 0.1), (1, 4000, 0.1)])
+def test_attention_bwd_roles_matches_two_kernels(dev, monkeypatch, B, T, p):
+    """The two-role backward (one launch: dK/dV blocks and dQ blocks side by side, delta formed by its
+    own pass; chosen where each grid alone fills the CUs once but not twice — config 4) against the
+    two-kernel form (RP_ATTN_ROLES=0: fused-delta dQ, then dK/dV, as eight-wave split workgroups), Q
+    prescaled, ragged keys: equal up to delta's rounding, and bitwise repeatable.  Also the key-padded
+    T = 4000 (a partial last 128-block on both sides) and B = 2, T = 2048 (grids of 256 too)."""
+    H = 8
+    qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=41).to(torch.bfloat16)
+    qkv[:, :H * 64] = (qkv[:, :H * 64].float() * (0.125 * K.LOG2E)).to(torch.bfloat16)
+    lens = torch.tensor([T, T - 77][:B], device=dev)
+    kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
+    olo = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 93, q_prescaled=True, out_lo=olo)
+    do = rnd(B * T, H * 64, dev=dev, seed=42).to(torch.bfloat16)
+    outs = {}
+    for flag in ("0", "1", "1"):
+        monkeypatch.setenv("RP_ATTN_ROLES", flag)
+        r = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask if p else None, q_prescaled=True,
+                       out_lo=olo)
+        torch.cuda.synchronize()
+        if flag in outs:
+            assert torch.equal(r, outs[flag]), "two-role backward not repeatable"
+        outs[flag] = r
+    assert torch.isfinite(outs["1"]).all()
+    close(outs["1"].float(), outs["0"].double(), atol=2e-2, rtol=2e-2, what="two-role vs two-kernel dqkv")
+    dkv = outs["1"].view(B, T, 3, H * 64)[:, :, 1:]
+    for bb in range(B):
+        assert torch.count_nonzero(dkv[bb, int(lens[bb]):]) == 0  # padded keys: no gradient
+
+
 @pytest.mark.parametrize("T", [128, 192, 4096])
 def test_wgrad_grouped_repeat_bitwise(dev, T):
     """Race guard for the 256-row kernel's LDS-DMA pipeline: the grouped weight gradients of the
