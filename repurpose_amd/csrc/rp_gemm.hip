@@ -1515,6 +1515,17 @@ static bool rp_gemm_bm64(int64_t M, int64_t N) {
   return ((M + BM - 1) / BM) * ((N + BN - 1) / BN) < 512;
 }
 
+// 32 x 128 tiles (each wave 16 x 64; the same K order per output element, so bitwise the 64- and
+// 128-row kernels) where even the 64 x 128 grid gives fewer than two workgroups per CU: config 4's
+// d_model = 512 GEMMs (M = 4096: 256 -> 512 tiles; step 7.36 -> 7.17 ms).  RP_GEMM_BM32=0 never, =1
+// wherever the 64-row tiles run (tests, A/B), unset: fewer 64 x 128 tiles than twice the CUs.  Per call.
+static bool rp_gemm_bm32(int64_t M, int64_t N) {
+  const char* e = getenv("RP_GEMM_BM32");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return ((M + 63) / 64) * ((N + BN - 1) / BN) < 512;
+}
+
 template <typename T, typename TC>
 int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int ak, const void* B,
                   int64_t ldb, int bk, void* Cp, int64_t ldc, float alpha, const EpiDev& ep,
@@ -1544,6 +1555,26 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
       default: RP_DMA_LAUNCH1(AKV, BKV, MODEV, 2, GRID); break;               \
     }                                                                         \
   } while (0)
+      if (splits == 0 && ak && cfg == 0 && rp_gemm_bm64(M, N) && rp_gemm_bm32(M, N)) {  // 32 x 128 tiles
+        const dim3 grid((unsigned)(((M + 31) / 32) * ((N + BN - 1) / BN)));
+        bool done = false;
+        if constexpr (std::is_same<TC, float>::value) {
+          if (bk && ep.residual) {
+            hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, true, TC, 0, 0, true, 1>), grid, dim3(NT), 0, s, M, N, K,
+                               ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
+            done = true;
+          }
+        }
+        if (!done) {
+          if (bk)
+            hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, true, TC, 0, 0, false, 1>), grid, dim3(NT), 0, s, M, N, K,
+                               ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
+          else
+            hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, TC, 0, 0, false, 1>), grid, dim3(NT), 0, s, M, N, K,
+                               ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
+        }
+        return rp_check_launch("rp_gemm");
+      }
       if (splits == 0 && ak && cfg == 0 && rp_gemm_bm64(M, N)) {
         const dim3 grid((unsigned)(((M + 63) / 64) * ((N + BN - 1) / BN)));
         bool done = false;
