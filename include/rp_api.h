@@ -286,12 +286,6 @@ int rp_sumsq_batched(const rp_sumsq_item* items, int n_items, void* stream);
  * backward unchanged.  Without the flag the kernels compute the same bf16(Q * scale * log2 e)
  * themselves (the forward and dQ kernels in registers, the dK/dV kernel as it stages Q tiles). */
 enum { RP_ATTN_Q_PRESCALED = 0x100 };
-/* Also or-ed into the dtype of the backward entry points: keep four-wave workgroups where a grid
- * that fills the CUs once would otherwise get the eight-wave split ones (config 4: B = 1, T = 4096).
- * For callers that run the dQ kernel (rp_attn_bwd_dq) beside the dK/dV kernel on another stream:
- * the two grids then fill the CUs together.  Results are identical either way up to the split
- * kernels' partial-sum order. */
-enum { RP_ATTN_NO_SPLIT = 0x200 };
 
 /* Multi-head self attention, flash-style (no T x T materialisation).
  * qkv: [B*T, 3*H*dk] rows = (q heads | k heads | v heads), dk == 64.
@@ -306,7 +300,7 @@ enum { RP_ATTN_NO_SPLIT = 0x200 };
  * times per 64-key tile, tiles in order, each step giving the word x ^ c; in tile t word j (1..8th of the tile)
  * holds the keys 64t + 16*(j>>1) + 4g + 2*(j&1) + {0: low 16 bits, 1: high 16 bits}; a key is kept iff its 16 bits
  * read as int16 are >= round(p*65536) - 32768 (rp_hash: repurpose_amd/csrc/rp_common.h).
- * The forward writes the keep bits to `dropmask` (uint16 [B*H][ceil(T/64)][4][roundup(T,256)],
+ * The forward writes the keep bits to `dropmask` (uint16 [B*H][ceil(T/64)][4][roundup(T,128)],
  * bit (kt*4 + r) of word (bh, tile, g, q) = keep(q, 64*tile + 16*kt + 4*g + r);
  * rp_attn_dropmask_elems() words), the backward reads them back.  dropmask may be NULL when
  * p == 0. */
@@ -319,7 +313,7 @@ int64_t rp_attn_dropmask_elems(int B, int T, int H);
  * a sequence has no valid key at all).  out [B*Tq, ldo]; lse [B, H, Tq] fp32.  Backward: dout
  * [B*Tq, lddo]; dq [B*Tq, lddq], dk / dv [B*Tk, lddk / lddv] are fully overwritten; delta_ws
  * [3, B, H, Tq] fp32 (plane 0 = delta; see rp_attn_bwd).  Dropout keep bits (forward -> backward) as for rp_attn_fwd with T -> (Tq, Tk):
- * rp_mha_dropmask_elems(B, Tq, Tk, H) uint16 words [B*H][ceil(Tk/64)][4][roundup(Tq,256)].
+ * rp_mha_dropmask_elems(B, Tq, Tk, H) uint16 words [B*H][ceil(Tk/64)][4][roundup(Tq,128)].
  * Replaces models/transformer.py:37-81 MultiHeadAttention's score/softmax/PV core (self attention
  * of EncoderLayer :84-102, cross attention of CrossAttentionEncoderLayer :105-130 and
  * CrossSelfEncoderLayer :133-176). */
@@ -406,9 +400,13 @@ int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int
  * 128-key block, reading delta).  The phases are also exported separately (per-kernel timing);
  * rp_attn_bwd_delta + rp_attn_bwd_dq is the unfused equivalent of rp_attn_bwd_dq_delta.
  * Where each of the two grids alone would fill the CUs once but not twice (B*H*ceil(T/128) in
- * [256, 384), e.g. B = 1, T = 4096, H = 8; bf16 with RP_ATTN_Q_PRESCALED), rp_attn_bwd and
+ * [256, 384) on 256 CUs, e.g. B = 1, T = 4096, H = 8; bf16 with RP_ATTN_Q_PRESCALED), rp_attn_bwd and
  * rp_mha_bwd with phases 7 instead run rp_attn_bwd_delta's pass and ONE launch whose workgroups take
- * either role (dK/dV blocks, then dQ blocks): same results up to the rounding of delta's sum. */
+ * either role (dK/dV blocks, then dQ blocks): same results up to the rounding of delta's sum.
+ * (The bound is in compute units: [CUs, 1.5 CUs).)  rp_attn_bwd_uses_roles tells whether rp_attn_bwd
+ * takes that form for a shape (1) or the two kernels (0), so a caller timing the phases separately
+ * (bench.py's roofline) can time the launch the step really runs. */
+int rp_attn_bwd_uses_roles(int dtype, int B, int T, int H, int dk);
 int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,
                 const float* lse, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
                 float dropout_p, const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream);

@@ -53,8 +53,8 @@ struct AttnCfg {
 // both 16x16x32 access patterns conflict-free: ds_read_b128 row fragments (16 lanes = 16 rows x 2
 // adjacent chunks cover all 16 bank quads) and ds_read_b64_tr_b16 column fragments (8 consecutive
 // rows x one 32-byte pair cover all 8 bank octets).  (Adding the chunk-parity bit (row >> 3) & 1,
-// which spreads the 32x32x16 row fragment of the optional kv32 kernel over all 16 quads, made the
-// shipping 16x16 kernels 6-9 % slower, +0.27 ms per step: measured and reverted, round 3.)
+// which spreads a 32x32x16 row fragment over all 16 quads, made these 16x16 kernels 6-9 % slower,
+// +0.27 ms per step: measured and reverted, round 3.)
 __device__ __forceinline__ int lds_swz(int row) { return ((row >> 1) & 3) << 1; }
 template <typename T>
 __device__ __forceinline__ int lds_off(int row, int byte) {
@@ -65,11 +65,11 @@ __device__ __forceinline__ int lds_off(int row, int byte) {
 }
 
 // keep-bit mask layout (the forward's register layout, so the forward and dQ kernels move one
-// 16-bit word per lane and key tile): [B*H][KT = ceil(T/64)][4 lane groups g][ldm = roundup(T,256)]
-// (a row covers every query of the last 256-query block of the ping-pong forward, so block-wide
-// stores and DMA pieces of a row never reach the next one)
+// 16-bit word per lane and key tile): [B*H][KT = ceil(T/64)][4 lane groups g][ldm = roundup(T,128)]
+// (a row covers every query of the last 128-query block, so block-wide stores and DMA pieces of a
+// row never reach the next one)
 // uint16; bit (kt*4 + r) of word (bh, tile, g, q) = keep(q, key = 64*tile + 16*kt + 4*g + r)
-__host__ __device__ inline int64_t mask_ld(int T) { return ((int64_t)T + 255) / 256 * 256; }
+__host__ __device__ inline int64_t mask_ld(int T) { return ((int64_t)T + 127) / 128 * 128; }
 __host__ __device__ inline int mask_kt(int T) { return (T + 63) / 64; }
 
 // ----- problem description (device side of rp_mha_args) ------------------------------------------
@@ -94,7 +94,6 @@ struct MhaDev {
   int qpre;  // RP_ATTN_Q_PRESCALED: q holds Q * scale * log2(e) (see include/rp_api.h)
   int empty_uniform;  // a sequence with no valid key attends uniformly to all keys (masked_fill(-1e9))
   uint64_t mwc_jump;  // split forward: A^(8 n) * 2^64 mod M, n = the key tiles of one part (mwc_jump)
-  int nosplit;  // RP_ATTN_NO_SPLIT: the backward keeps four-wave workgroups (dQ runs beside dK/dV)
 };
 
 // MWC64X skip-ahead.  The state S = c * 2^32 + x steps as S' = A * S mod M, M = A * 2^32 - 1, so n
@@ -1459,290 +1458,6 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_kv_dma_kernel(MhaD
 }
 
 // =================================================================================================
-// backward: dK, dV on 32x32x16 MFMAs (bf16, LDS-DMA) — same data flow, ring and DMA pieces as
-// attn_bwd_kv_dma_kernel<DROP, 2, true>, with each wave's 32 keys as ONE 32-wide MFMA column block:
-// a v_mfma_f32_32x32x16_bf16 holds the SIMD's vector issue for 8 of its 32 cycles where two
-// 16x16x32 ones (the same FLOPs) hold it for 16 of 32 — the kernel is issue-bound (SQ counters,
-// profiles/r03_attn_sq_counters.txt), so that is 256 issue cycles per wave and 64-query tile back.
-//   S  [32 q][32 keys] = Q' K^T   : A = Q rows (32x32x16 row fragments from the LDS image),
-//                                   B = K rows in registers (lane = key), 4 k-steps over dk = 64
-//   lane l (key kw0 + (l & 31), h = l >> 5) holds S rows (reg & 3) + 8 (reg >> 2) + 4h, reg 0..15:
-//   the row constants (-lse, -delta/ds) start the accumulators as four f32x4 LDS reads, and P / dS
-//   packed pairwise to bf16 (registers 8s .. 8s+7 -> k-step s) are the A operands of
-//   dV[key][d] += P^T dO, dK[key][d] += dS^T Q' with dO / Q' as transposed (tr16) column fragments
-//   whose k order matches: element j of lane half h = query 16s + 8 (j >> 2) + 4h + (j & 3).
-// =================================================================================================
-// 32x32x16 operand fragments: lane l (r = l & 31, h = l >> 5) holds X[r0 + r][k0 + 8h .. + 7]
-__device__ __forceinline__ bf16x8 row_frag32_lds(const char* lds, int r0, int k0, int lane) {
-  return *reinterpret_cast<const bf16x8*>(lds + lds_off<bf16>(r0 + (lane & 31), (k0 + 8 * (lane >> 5)) * 2));
-}
-__device__ __forceinline__ bf16x8 row_frag32_gmem(const bf16* base, int64_t ld, int r0, int nrows, int k0, int lane) {
-  const int r = r0 + (lane & 31);
-  if (r >= nrows) {
-    bf16x8 z;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
-    return z;
-  }
-  return *reinterpret_cast<const bf16x8*>(base + (int64_t)r * ld + k0 + 8 * (lane >> 5));
-}
-// column fragment (B operand over a row index): lane l (c = l & 31, h = l >> 5) receives
-// X[R + 4h + {0..3}][c0 + c] and X[R + 8 + 4h + {0..3}][c0 + c] through two ds_read_b64_tr_b16:
-// 16-lane group G reads the 4-row block R + 4 (G >> 1) (+ 8), columns c0 + 16 (G & 1) .. + 15
-__device__ __forceinline__ bf16x8 col_frag32_lds(const char* lds, int R, int c0, int lane) {
-  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int row = R + 4 * (G >> 1) + q, col = c0 + 16 * (G & 1) + 4 * p;
-  const char* p0 = lds + lds_off<bf16>(row, col * 2);
-  const char* p1 = lds + lds_off<bf16>(row + 8, col * 2);
-  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
-  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p1);
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
-}
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-template <bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_kv32_kernel(MhaDev a) {
-  constexpr int KB = NW * 32;  // keys per workgroup (one 32-key MFMA block per wave)
-  using C = AttnCfg<bf16>;
-  constexpr int TILE = KV_QT * C::ROWB;
-  constexpr int XR = 1024;
-  constexpr int BUF = 2 * TILE + 4 * XR;  // Q, dO images, lse row, delta row, keep bits, scratch
-  constexpr int NBUF = 3;
-  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5;
-  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
-  const uint8_t* __restrict__ kvalid = a.kvalid;
-  const uint16_t* __restrict__ dmask = a.dmask;
-  const int nkb = (Tk + KB - 1) / KB;
-  const int L = rp_xcd_remap(blockIdx.x, nkb * B * H);
-  const int bh = L / nkb, kb = L % nkb;
-  const int b = bh / H, hh = bh % H;
-  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
-  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + hh * HD;
-  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + hh * HD;
-  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + hh * HD;
-  const bf16* dOg = (const bf16*)a.dout + (int64_t)b * Tq * lddo + hh * HD;
-  const int64_t plane = (int64_t)B * H * Tq;
-  const float* nls_bh = a.delta + 2 * plane + (int64_t)bh * Tq;
-  const float* ndl_bh = a.delta + plane + (int64_t)bh * Tq;
-  const int kw0 = kb * KB + w * 32;
-  const int KT = mask_kt(Tk);
-  const int64_t ldm = mask_ld(Tq);
-
-  // K, V as B operands of S and dP: lane holds X[kw0 + (l & 31)][16 ks + 8h .. + 7]
-  bf16x8 kf[4], vf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    kf[ks] = row_frag32_gmem(Kg, ldk, kw0, Tk, ks * 16, lane);
-    vf[ks] = row_frag32_gmem(Vg, ldv, kw0, Tk, ks * 16, lane);
-  }
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) asm volatile("" ::"v"(kf[ks]), "v"(vf[ks]));
-
-  f32x16 dk[2], dv[2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dk[dt][r] = dv[dt][r] = 0.f;
-
-  auto ring = [&](auto bi) -> char* {
-    constexpr int BI = decltype(bi)::value;
-    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
-  };
-  // LDS-DMA of query tile it: exactly attn_bwd_kv_dma_kernel's five pieces per wave
-  Rows64 rq, rdo;
-  rq.init(Qg, ldq, Tq, w, lane);
-  rdo.init(dOg, lddo, Tq, w, lane);
-  const bool xmask = DROP && w == 3;
-  const uint16_t* mslab = DROP ? dmask + (int64_t)bh * KT * 4 * ldm : dmask;
-  const rp_srd srd_x = make_srd(xmask ? (const void*)mslab : (const void*)(w == 1 ? nls_bh : ndl_bh));
-  uint32_t vo_x = (uint32_t)(lane & 15) * 16u;
-  const uint32_t bpr_x = xmask ? 2u : 4u;
-  const uint32_t xo = (uint32_t)(2 * TILE + XR * (w == 1 ? 0 : (w == 2 ? 1 : (xmask ? 2 : 3))));
-  if (xmask) {
-    const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
-    int tile = kb * (KB / 64) + (r >> 2);
-    tile = tile < KT ? tile : KT - 1;
-    vo_x = (uint32_t)((((int64_t)tile * 4 + (r & 3)) * ldm + cch * 8) * 2);
-  }
-  const bool xfast = (int64_t)KT * 4 * ldm * 2 < ((int64_t)1 << 31) && rq.fast && rdo.fast;
-  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
-  auto issue = [&](int it, auto bi) {
-    constexpr int BI = decltype(bi)::value;
-    char* buf = ring(bi);
-    const int qs0 = it * KV_QT;
-    if (xfast && qs0 + KV_QT <= Tq) {
-      const uint32_t t = slot_lds[BI];
-      const uint32_t pq = t + (uint32_t)(w * 2) * 1024u;
-      static_assert(TILE == 8192, "dma16b_x4 places the second operand 8 KB on");
-      dma16b_x4(rq.srd, rq.vo0, rq.vo1, (uint32_t)qs0 * rq.rowbytes, rdo.srd, rdo.vo0, rdo.vo1,
-                (uint32_t)qs0 * rdo.rowbytes, pq);
-      dma16b(srd_x, vo_x, (uint32_t)qs0 * bpr_x, t + xo);
-    } else {
-      dma_rows64(Qg, ldq, qs0, Tq, buf, w, lane);
-      dma_rows64(dOg, lddo, qs0, Tq, buf + TILE, w, lane);
-      const int q = qs0 + lane;
-      if (xmask) {
-        const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = lane & 7;
-        int tile = kb * (KB / 64) + (r >> 2);
-        tile = tile < KT ? tile : KT - 1;
-        dma16(dmask + (((int64_t)bh * KT + tile) * 4 + (r & 3)) * ldm + qs0 + cch * 8, lds_addr(buf + xo));
-      } else if (w == 1) {
-        dma4(q < Tq ? nls_bh + q : kPadStart, lds_addr(buf + xo));
-      } else {
-        dma4(ndl_bh + (q < Tq ? q : Tq - 1), lds_addr(buf + xo));
-      }
-    }
-  };
-  auto wait_tile = [&](bool next) {
-    if (!next)
-      wait_vm<0>();
-    else
-      wait_vm<5>();
-  };
-  // this lane's key: keep-bit word row and bit (layout of include/rp_api.h / mask_ld)
-  const int kwl = w * 32 + (lane & 31);
-  const int ko = kwl & 63;
-  const int mrow_l = (kwl >> 6) * 4 + ((ko & 15) >> 2);
-  const int kbit = (ko >> 4) * 4 + (ko & 3);
-
-  const int nqt = (Tq + KV_QT - 1) / KV_QT;
-  issue(0, std::integral_constant<int, 0>());
-  if (nqt > 1) issue(1, std::integral_constant<int, 1>());
-  auto step = [&](auto bi, int it) {
-    constexpr int BI = decltype(bi)::value;
-    wait_tile(it + 1 < nqt);
-    raw_barrier();
-    if (it + 2 < nqt) issue(it + 2, std::integral_constant<int, (BI + 2) % NBUF>());
-    const char* cur = ring(bi);
-    const char* Ql = cur;
-    const char* dOl = cur + TILE;
-    const float* lrow = reinterpret_cast<const float*>(cur + 2 * TILE);
-    const float* drow = reinterpret_cast<const float*>(cur + 2 * TILE + XR);
-    const uint16_t* mw = reinterpret_cast<const uint16_t*>(cur + 2 * TILE + 2 * XR);
-
-    // one query block qb = 32 queries: S / dP (8 MFMAs), the probability / dS VALU, then the dV / dK
-    // products (8 MFMAs) over its two 16-query k-steps
-    // a query block's 16 row constants of this lane: four f32x4 reads, concatenated in register order
-    // (reg 4m + r <-> row r + 8m + 4h)
-    auto rows16 = [&](const float* src, int qb) -> f32x16 {
-      const int r0 = qb * 32 + 4 * h;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(src + r0);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + r0 + 8);
-      const f32x4 x2 = *reinterpret_cast<const f32x4*>(src + r0 + 16);
-      const f32x4 x3 = *reinterpret_cast<const f32x4*>(src + r0 + 24);
-      const f32x8 lo = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
-      const f32x8 hi = __builtin_shufflevector(x2, x3, 0, 1, 2, 3, 4, 5, 6, 7);
-      return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-    };
-    auto sdp = [&](int qb, f32x16& s, f32x16& dp) {
-      // the row constants enter as the first products' C operands (the dropout re-reads -delta/ds:
-      // a 32x32 MFMA's D overwrites its C, so keeping them live would cost 16 register copies)
-      const f32x16 nl = rows16(lrow, qb);
-      const f32x16 nd = rows16(drow, qb);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 qa = row_frag32_lds(Ql, qb * 32, ks * 16, lane);
-        const bf16x8 da = row_frag32_lds(dOl, qb * 32, ks * 16, lane);
-        s = mfma32(qa, kf[ks], ks == 0 ? nl : s);
-        dp = mfma32(da, vf[ks], ks == 0 ? nd : dp);
-      }
-    };
-    auto prob = [&](int qb, f32x16& s, f32x16& dp, bf16x8 (&pa)[2], bf16x8 (&sa)[2]) {
-      f32x16 nd;
-      if constexpr (DROP) {  // re-read, not kept live: the opaque zero keeps the compiler from reusing sdp's load
-        int z = 0;
-        asm volatile("" : "+v"(z));
-        nd = rows16(drow + z, qb);
-      }
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        uint2 bits = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-        if constexpr (DROP) bits = *reinterpret_cast<const uint2*>(mw + mrow_l * KV_QT + qb * 32 + 8 * m + 4 * h);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = 4 * m + r;
-          const float pr = rp_exp2(s[j]);  // with dropout: p * ds
-          if constexpr (DROP) {
-            const uint32_t km = keep_mask(r < 2 ? bits.x : bits.y, kbit + 16 * (r & 1));
-            s[j] = bfi_select(km, pr, 0.f);
-            dp[j] = pr * bfi_select(km, dp[j], nd[j]);
-          } else {
-            s[j] = pr;
-            dp[j] = pr * dp[j];
-          }
-        }
-      }
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        f32x4 a0, a1, b0, b1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          a0[r] = s[8 * ss + r];
-          a1[r] = s[8 * ss + 4 + r];
-          b0[r] = dp[8 * ss + r];
-          b1[r] = dp[8 * ss + 4 + r];
-        }
-        pa[ss] = pack8(a0, a1);
-        sa[ss] = pack8(b0, b1);
-      }
-    };
-    auto dvdk = [&](int qb, const bf16x8 (&pa)[2], const bf16x8 (&sa)[2]) {
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const bf16x8 dob = col_frag32_lds(dOl, qb * 32 + ss * 16, dt * 32, lane);
-          const bf16x8 qcb = col_frag32_lds(Ql, qb * 32 + ss * 16, dt * 32, lane);
-          dv[dt] = mfma32(pa[ss], dob, dv[dt]);
-          dk[dt] = mfma32(sa[ss], qcb, dk[dt]);
-        }
-    };
-    // both blocks' S / dP products first, so block 0's VALU runs beside block 1's MFMAs and block 1's
-    // VALU beside block 0's dV / dK products (attn_bwd_kv_dma_kernel's PIPE order)
-    f32x16 s0, dp0, s1, dp1;
-    bf16x8 pa0[2], sa0[2], pa1[2], sa1[2];
-    sdp(0, s0, dp0);
-    sdp(1, s1, dp1);
-    prob(0, s0, dp0, pa0, sa0);
-    dvdk(0, pa0, sa0);
-    prob(1, s1, dp1, pa1, sa1);
-    dvdk(1, pa1, sa1);
-  };
-  for (int it = 0; it < nqt; it += NBUF) {
-    step(std::integral_constant<int, 0>(), it);
-    if (it + 1 < nqt) step(std::integral_constant<int, 1>(), it + 1);
-    if (it + 2 < nqt) step(std::integral_constant<int, 2>(), it + 2);
-  }
-  // store: dk[dt][reg] = dK[key = kw0 + (reg & 3) + 8 (reg >> 2) + 4h][dk = 32 dt + (l & 31)];
-  // masked keys -> 0; dK = dS^T Q' / log2(e)
-  bf16* dK = (bf16*)a.dk + (int64_t)b * Tk * a.lddk + hh * HD;
-  bf16* dV = (bf16*)a.dv + (int64_t)b * Tk * a.lddv + hh * HD;
-#pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int key = kw0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-    if (key >= Tk) continue;
-    const bool ok = kvalid[(int64_t)b * Tk + key] != 0;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      rp_st(dK + (int64_t)key * a.lddk + dt * 32 + (lane & 31), ok ? dk[dt][reg] * (1.f / LOG2E) : 0.f);
-      rp_st(dV + (int64_t)key * a.lddv + dt * 32 + (lane & 31), ok ? dv[dt][reg] : 0.f);
-    }
-  }
-}
-
-// =================================================================================================
 // backward: dQ per 128-query block (4 waves x 32 queries), sweep over 64-key tiles
 // =================================================================================================
 // DELTA: the kernel also forms delta = rowsum(dO * O) of its queries (the lane's 16 dims of dO are
@@ -2794,1112 +2509,52 @@ __global__ __launch_bounds__(NT * SPL, SPL == 1 ? 3 : 1) void attn_fwd_dma_kerne
   }
 }
 
-// =================================================================================================
-// 32x32x16 forward and dQ kernels (bf16, 128-query workgroups, LDS-DMA three-slot ring).
-//
-// The 16x16x32 kernels above spend half of every MFMA's 16 cycles holding the SIMD's vector issue
-// port (MI355X_MICROARCH.md: an MFMA holds vector issue for 8 of its cycles), and their tile loops are
-// vector-issue bound: forward p = 0.1 ~1,460 issue cycles per wave and 64-key tile against 576 MFMA
-// cycles.  v_mfma_f32_32x32x16_bf16 does the same work as two 16x16x32 MFMAs for one 8-cycle issue
-// slot, and with the QUERY on the MFMA column (S^T = K Q^T: lane (h = l / 32, c = l % 32) holds query c
-// and keys 4h + 8j + r, j, r = 0..3, of a 32-key tile) every per-query quantity is one value per lane:
-//  * the running maximum / lse / delta enter the S^T and dP^T products as the first MFMA's C operand, a
-//    16-register tile holding the lane's value (the forward rebuilds it only on a rescale; the dQ kernel
-//    builds its two once);
-//  * the row maximum is lane-local over the lane's 32 scores plus one permlane32 swap with its partner
-//    lane (only inside the rare rescale branch);
-//  * the accumulator rows ARE the next product's k slots: packed to bf16, registers 8s'..8s'+7 of a
-//    32-key tile are the B operand of k-step s' of O^T += V^T P^T (forward) / dQ^T += K^T dS^T (dQ), with
-//    the k order k = 8h + 4jj + r <-> key 16s' + 8jj + 4h + r; the A operand's transposed fragments
-//    (ds_read_b64_tr_b16, keys 4h..4h+3 and 8+4h..8+4h+3) follow the same order.
-// LDS image of a [64 rows][64] bf16 tile: 128-byte rows, 16-byte chunk c of row r stored at chunk
-// c ^ swz32(r), swz32(r) = ((r & 2) << 1) | ((r >> 3) & 3): conflict-free for both 32x32x16 operand
-// reads — ds_read_b128 row fragments (16 rows x one chunk per lane group) and ds_read_b64_tr_b16
-// column fragments (4 rows x 64 bytes per 32-lane half) — found by exhaustive search over XOR maps of
-// the row bits (the 16x16 swizzle lds_swz leaves the 32-row fragment 4-way conflicted).
-// Dropout: lane (h, c) runs the MWC streams of (query c, lane groups g = h and h + 2) — exactly the
-// streams and keep bits of the 16x16 forward (attn_fwd_kernel), so the stored mask layout and every
-// reader are unchanged; one stream word covers one packed bf16 P pair.
-// =================================================================================================
-__device__ __forceinline__ int swz32(int row) { return ((row & 2) << 1) | ((row >> 3) & 3); }
-__device__ __forceinline__ int off32(int row, int chunk) { return row * 128 + ((chunk ^ swz32(row)) << 4); }
-
-__device__ __forceinline__ f32x16 splat16(float v) {
-  f32x16 r;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) r[j] = v;
-  return r;
-}
-
-// 32x32x16 row fragment (A or B operand): lane (h, m) holds X[r0 + m][16 s + 8 h + 0..7]
-__device__ __forceinline__ bf16x8 row32_lds(const char* lds, int r0, int s, int lane) {
-  const int m = lane & 31, h = lane >> 5;
-  return *reinterpret_cast<const bf16x8*>(lds + off32(r0 + m, 2 * s + h));
-}
-// 32x32x16 transposed fragment of a [key][col] tile (A operand of O^T += V^T P^T, dQ^T += K^T dS^T):
-// lane (h, m) holds X[R + 4h + {0..3}][c0 + m] and X[R + 8 + 4h + {0..3}][c0 + m] (k = 8h + 4jj + r <->
-// row R + 8jj + 4h + r, the accumulator k order above).  Per 16-lane group one 4-row x 16-column
-// block: lane 4q + p supplies row q, columns 4p..4p+3.
-__device__ __forceinline__ bf16x8 col32_lds(const char* lds, int R, int c0, int lane) {
-  const int h = lane >> 5, gg = (lane >> 4) & 1, i = lane & 15, q = i >> 2, p = i & 3;
-  const int row = R + 4 * h + q;
-  const int byte = 2 * (c0 + 16 * gg + 4 * p);
-  const char* p0 = lds + off32(row, byte >> 4) + (byte & 15);
-  const char* p1 = lds + off32(row + 8, byte >> 4) + (byte & 15);
-  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
-  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p1);
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
-}
-// registers 8k..8k+7 of a 32x32 accumulator -> bf16x8 (the B operand of k-step k of the next product)
-__device__ __forceinline__ bf16x8 pack8_32(const f32x16& a, int k) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * k + j];
-  return r;
-}
-
-// lane-local maximum of two 32x32 accumulators as a v_max3 tree (depth 4 instead of a 16-long chain)
-__device__ __forceinline__ float max32x2(const f32x16& x, const f32x16& y) {
-  float l1[11];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) l1[i] = fmaxf(fmaxf(x[3 * i], x[3 * i + 1]), x[3 * i + 2]);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) l1[5 + i] = fmaxf(fmaxf(y[3 * i], y[3 * i + 1]), y[3 * i + 2]);
-  l1[10] = fmaxf(x[15], y[15]);
-  const float a0 = fmaxf(fmaxf(l1[0], l1[1]), l1[2]), a1 = fmaxf(fmaxf(l1[3], l1[4]), l1[5]);
-  const float a2 = fmaxf(fmaxf(l1[6], l1[7]), l1[8]), a3 = fmaxf(l1[9], l1[10]);
-  return fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
-}
-// rows [row0, row0 + 64) of a [rows][64] bf16 operand -> the swz32 image (LDS-DMA, two 1 KB pieces
-// per wave, clamped source rows); descriptor form as Rows64
-__device__ __forceinline__ void dma_rows64_s32(const bf16* __restrict__ base, int64_t ld, int row0, int nrows,
-                                               char* tile, int w, int lane) {
-  const uint32_t t = lds_addr(tile);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int I = w * 2 + j;
-    const int r = I * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ swz32(r);
-    int rr = row0 + r;
-    rr = rr < nrows ? rr : nrows - 1;
-    dma16(base + (int64_t)rr * ld + c * 8, t + I * 1024);
-  }
-}
-struct Rows64S32 {
-  rp_srd srd;
-  uint32_t vo0, vo1, rowbytes;
-  bool fast;
-  __device__ __forceinline__ void init(const bf16* b, int64_t ld_, int nrows, int w, int lane) {
-    srd = make_srd(b);
-    const int r0 = (w * 2) * 8 + (lane >> 3), r1 = r0 + 8;
-    const int c0 = (lane & 7) ^ swz32(r0), c1 = (lane & 7) ^ swz32(r1);
-    vo0 = (uint32_t)((r0 * ld_ + c0 * 8) * 2);
-    vo1 = (uint32_t)((r1 * ld_ + c1 * 8) * 2);
-    rowbytes = (uint32_t)(ld_ * 2);
-    fast = ((int64_t)nrows + 64) * ld_ * 2 < ((int64_t)1 << 31);
-  }
-};
-
-// ---- forward ----
-template <bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_fwd32_kernel(MhaDev a) {
-  constexpr int QB = NW * 32;  // 128 queries per workgroup, 32 per wave
-  constexpr int TILE = FW_KT * 128;
-  constexpr int BUF = 2 * TILE;
-  constexpr int NBUF = 3;
-  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
-  __shared__ __attribute__((aligned(16))) uint8_t kvl[FD_TKMAX];
-  __shared__ int kfull[FD_TKMAX / FW_KT];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, c = lane & 31;
-  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
-  const uint32_t drop_thresh = a.drop_thresh;
-  const float drop_scale = a.drop_scale;
-  const float scale = a.scale;
-  const int nqb = (Tq + QB - 1) / QB;
-  const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
-  const int bh = L / nqb, qb = L % nqb;
-  const int b = bh / H, hh = bh % H;
-  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv;
-  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + hh * HD;
-  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + hh * HD;
-  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + hh * HD;
-  const int q0 = qb * QB + w * 32;
-  const int q = q0 + c;
-  const uint32_t seed_bh = rp_hash(rp_seed_eff(a.seed_base, a.seed), (uint32_t)bh);
-  const float cq = scale * LOG2E;
-  const int KT = mask_kt(Tk);
-  const int64_t ldm = mask_ld(Tq);
-  uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
-  const bool novalid = seq_has_no_key(a, b, tid);
-
-  // Q'^T as the B operand of S^T = K Q'^T: k-step s holds Q'[q][16 s + 8 h + 0..7]
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    if (q < Tq && !novalid) {
-      qf[s] = *reinterpret_cast<const bf16x8*>(Qg + (int64_t)q * ldq + 16 * s + 8 * h);
-      if (!a.qpre) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * cq);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)0.f;
-    }
-  }
-  const int nkt = (Tk + FW_KT - 1) / FW_KT;
-  for (int k = tid; k < nkt * FW_KT; k += NT)
-    kvl[k] = k < Tk ? (novalid || a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
-  __syncthreads();
-  for (int t = tid; t < nkt; t += NT) {
-    int ok = 1;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t v = reinterpret_cast<const uint32_t*>(kvl)[t * 16 + j];
-      ok &= ((v - 0x01010101u) & ~v & 0x80808080u) == 0u;
-    }
-    kfull[t] = ok;
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]));
-  __syncthreads();
-
-  // O^T[d = 32 dt + 8 j + 4 h + r][q]; ls: every row = the running sum of P (before dropout) of query c
-  f32x16 o[2], ls;
-  o[0] = o[1] = ls = splat16(0.f);
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-  float m = 0.f;          // reference max (log2 units) subtracted through the S^T start
-  bool mset = false;
-  float gthr = -INFINITY;  // the lane-local grow bound: -inf until the reference is set, then RESCALE_LOG2
-  f32x16 negm = splat16(0.f);
-  uint64_t st0 = 0, st1 = 0;  // MWC streams of (query, lane group h) and (query, lane group h + 2)
-  if constexpr (DROP) {
-    st0 = mwc_seed(rp_hash(seed_bh, (uint32_t)q * 4u + (uint32_t)h));
-    st1 = mwc_seed(rp_hash(seed_bh, (uint32_t)q * 4u + (uint32_t)(h + 2)));
-  }
-  const short ts = (short)((int)drop_thresh - 32768);
-  const i16x2 t2 = {ts, ts};
-
-  auto ring = [&](auto bi) -> char* {
-    constexpr int BI = decltype(bi)::value;
-    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
-  };
-  Rows64S32 rk, rv;
-  rk.init(Kg, ldk, Tk, w, lane);
-  rv.init(Vg, ldv, Tk, w, lane);
-  const bool xfast = rk.fast && rv.fast;
-  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
-  auto issue = [&](int it, auto bi) {
-    constexpr int BI = decltype(bi)::value;
-    const int k0 = it * FW_KT;
-    if (xfast && k0 + FW_KT <= Tk) {
-      const uint32_t pk = slot_lds[BI] + (uint32_t)(w * 2) * 1024u;
-      dma16b_x4(rk.srd, rk.vo0, rk.vo1, (uint32_t)k0 * rk.rowbytes, rv.srd, rv.vo0, rv.vo1,
-                (uint32_t)k0 * rv.rowbytes, pk);
-    } else {
-      char* buf = ring(bi);
-      dma_rows64_s32(Kg, ldk, k0, Tk, buf, w, lane);
-      dma_rows64_s32(Vg, ldv, k0, Tk, buf + TILE, w, lane);
-    }
-  };
-  // step it waits for DMA(it); issued after it: (it >= 2) the 2 keep-bit stores of step it - 2,
-  // DMA(it + 1) (4), the 2 stores of step it - 1 (it >= 1)
-  auto wait_tile = [&](int it) {
-    if (it + 1 >= nkt)
-      wait_vm<0>();
-    else if (!DROP || it == 0)
-      wait_vm<4>();
-    else if (it == 1)
-      wait_vm<6>();
-    else
-      wait_vm<8>();
-  };
-  issue(0, std::integral_constant<int, 0>());
-  if (nkt > 1) issue(1, std::integral_constant<int, 1>());
-
-  auto step = [&](auto bi, int kt_i) {
-    constexpr int BI = decltype(bi)::value;
-    wait_tile(kt_i);
-    raw_barrier();
-    if (kt_i + 2 < nkt) issue(kt_i + 2, std::integral_constant<int, (BI + 2) % NBUF>());
-    const char* Kl = ring(bi);
-    const char* Vl = Kl + TILE;
-    const bool full = kfull[kt_i] != 0;
-    // ---- S^T[key][q] = K Q'^T - m, two 32-key tiles ----
-    f32x16 s[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) s[t] = mfma32(row32_lds(Kl, 32 * t, ks, lane), qf[ks], ks == 0 ? negm : s[t]);
-    if (!full) {  // key bias 0 / -inf: register 4 j + r of tile t is key 32 t + 8 j + 4 h + r
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t vb = *reinterpret_cast<const uint32_t*>(kvl + kt_i * FW_KT + 32 * t + 8 * j + 4 * h);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (((vb >> (8 * r)) & 0xFFu) == 0u) s[t][4 * j + r] = -INFINITY;
-        }
-    }
-    // ---- lane-local max against the reference; deferred rescale (attn_fwd_kernel) ----
-    const float mx = max32x2(s[0], s[1]);
-    if (__ballot(mx > gthr) != 0) {
-      // the query's row max: this lane's 32 keys and its partner lane's (l ^ 32)
-      auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      const float rel = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-      const bool gq = mset ? rel > RESCALE_LOG2 : rel > -INFINITY;
-      const float alpha = gq ? (mset ? rp_exp2(-rel) : 0.f) : 1.f;
-      const float sub = gq ? rel : 0.f;
-      ls *= alpha;
-      o[0] *= alpha;
-      o[1] *= alpha;
-      m += sub;
-      mset = mset || gq;
-      gthr = mset ? RESCALE_LOG2 : -INFINITY;
-      negm = splat16(-m);
-      s[0] -= sub;
-      s[1] -= sub;
-    }
-    // ---- P = exp2(acc), packed: pf[2 t + s'] = registers 8 s'..8 s' + 7 of tile t ----
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) s[t][v] = rp_exp2(s[t][v]);
-    bf16x8 pf[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) pf[k] = pack8_32(s[k >> 1], k & 1);
-    // row sums of P (before dropout) on the matrix core
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ls = mfma32(ones, pf[k], ls);
-    if constexpr (DROP) {
-      // stream words in order jw = 2 k + e (k = 2 t + s', e = 0, 1): stream 0 masks pair words e of
-      // pf[k] (register row j = 2 s'), stream 1 pair words 2 + e (j = 2 s' + 1); keep bit of the low /
-      // high half -> bit 4 k + 2 e / + 1 of the stream's 16-bit word (drop_masks)
-      uint32_t acc0 = 0u, acc1 = 0u;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint4 u = __builtin_bit_cast(uint4, pf[k]);
-        uint32_t mk[4];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const uint32_t w0 = rp_mwc_next(st0), w1 = rp_mwc_next(st1);
-          const i16x2 d0 = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w0), t2);
-          const i16x2 d1 = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w1), t2);
-          mk[e] = __builtin_bit_cast(uint32_t, (i16x2)(d0 >> (short)15));
-          mk[2 + e] = __builtin_bit_cast(uint32_t, (i16x2)(d1 >> (short)15));
-          const int bb = 4 * k + 2 * e;
-          acc0 |= ~mk[e] & ((1u << bb) | (1u << (16 + bb + 1)));
-          acc1 |= ~mk[2 + e] & ((1u << bb) | (1u << (16 + bb + 1)));
-        }
-        u.x &= ~mk[0];
-        u.y &= ~mk[1];
-        u.z &= ~mk[2];
-        u.w &= ~mk[3];
-        pf[k] = __builtin_bit_cast(bf16x8, u);
-      }
-      uint16_t* mr = mrow + ((int64_t)kt_i * 4 + h) * ldm + q;
-      mr[0] = (uint16_t)((acc0 & 0xFFFFu) | (acc0 >> 16));
-      mr[2 * ldm] = (uint16_t)((acc1 & 0xFFFFu) | (acc1 >> 16));
-    }
-    // ---- O^T[d][q] += V^T P^T ----
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(col32_lds(Vl, 16 * k, 32 * dt, lane), pf[k], o[dt]);
-  };
-  for (int it = 0; it < nkt; it += NBUF) {
-    step(std::integral_constant<int, 0>(), it);
-    if (it + 1 < nkt) step(std::integral_constant<int, 1>(), it + 1);
-    if (it + 2 < nkt) step(std::integral_constant<int, 2>(), it + 2);
-  }
-
-  // ---- epilogue: O[q][d] = O^T / l (16-byte stores after a permlane32 swap of register rows), lse ----
-  const float l = ls[0];
-  const float inv = drop_scale / l;
-  const int64_t ldo = a.ldo;
-  const bool qok = q < Tq;  // the same for both partner lanes of a query (the swaps below pair them)
-  bf16* orow = (bf16*)a.out + ((int64_t)b * Tq + q) * ldo + hh * HD;
-  bf16* lorow = a.out_lo ? (bf16*)a.out_lo + ((int64_t)b * Tq + q) * ldo + hh * HD : nullptr;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      // rows j = 2u (d 16u + 4h + r) and j = 2u + 1 (d 16u + 8 + 4h + r) of d tile dt
-      uint32_t A[2], Bv[2], Al[2], Bl[2];
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const float x0 = o[dt][8 * u + 2 * pr] * inv, x1 = o[dt][8 * u + 2 * pr + 1] * inv;
-        const float y0 = o[dt][8 * u + 4 + 2 * pr] * inv, y1 = o[dt][8 * u + 4 + 2 * pr + 1] * inv;
-        const bf16 bx0 = (bf16)x0, bx1 = (bf16)x1, by0 = (bf16)y0, by1 = (bf16)y1;
-        A[pr] = (uint32_t)__builtin_bit_cast(uint16_t, bx0) | ((uint32_t)__builtin_bit_cast(uint16_t, bx1) << 16);
-        Bv[pr] = (uint32_t)__builtin_bit_cast(uint16_t, by0) | ((uint32_t)__builtin_bit_cast(uint16_t, by1) << 16);
-        const bf16 lx0 = (bf16)(x0 - (float)bx0), lx1 = (bf16)(x1 - (float)bx1);
-        const bf16 ly0 = (bf16)(y0 - (float)by0), ly1 = (bf16)(y1 - (float)by1);
-        Al[pr] = (uint32_t)__builtin_bit_cast(uint16_t, lx0) | ((uint32_t)__builtin_bit_cast(uint16_t, lx1) << 16);
-        Bl[pr] = (uint32_t)__builtin_bit_cast(uint16_t, ly0) | ((uint32_t)__builtin_bit_cast(uint16_t, ly1) << 16);
-      }
-      // lanes 32..63 of A <-> lanes 0..31 of Bv: lane h = 0 then holds d 16u + 0..7, h = 1 d 16u + 8..15
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        auto r = __builtin_amdgcn_permlane32_swap(A[pr], Bv[pr], false, false);
-        A[pr] = r[0];
-        Bv[pr] = r[1];
-        auto rl = __builtin_amdgcn_permlane32_swap(Al[pr], Bl[pr], false, false);
-        Al[pr] = rl[0];
-        Bl[pr] = rl[1];
-      }
-      const int d0 = 32 * dt + 16 * u + 8 * h;
-      if (qok) {
-        *reinterpret_cast<uint4*>(orow + d0) = make_uint4(A[0], A[1], Bv[0], Bv[1]);
-        if (lorow) *reinterpret_cast<uint4*>(lorow + d0) = make_uint4(Al[0], Al[1], Bl[0], Bl[1]);
-      }
-    }
-  if (qok && h == 0) a.lse[(int64_t)bh * Tq + q] = m * 0.6931471805599453f + logf(l);
-}
-
-// ---- backward dQ (+ delta), 32x32x16 (bf16, 128-query workgroups, LDS-DMA ring) ----
-// The data flow of attn_bwd_q_dma_kernel on 32x32x16 MFMAs with the query on the MFMA column (see the
-// forward above): S^T = K Q'^T - lse and dP^T = V dO^T - delta/ds start from two 16-register C tiles
-// built once per kernel (every register of a lane holds its query's constant); dS^T = P^T * ds *
-// (keep ? dP^T : -delta/ds); dQ^T += K^T dS^T with the packed dS^T as the B operand and the K^T
-// fragments through ds_read_b64_tr_b16 (the k order of the accumulator rows).  The keep bits of lane
-// (h, c) are the words (g = h, query c) and (g = h + 2, query c) of the tile: register 4 j + r of
-// 32-key tile t reads bit (2 t + (j >> 1)) * 4 + r of word g = h + 2 (j & 1) — compile-time positions.
-template <bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_q32_kernel(MhaDev a) {
-  constexpr int QB = NW * 32;            // 128 queries per workgroup
-  constexpr int TILE = FW_KT * 128;      // one 64-key K or V image (8 KB)
-  constexpr int MASKB = 1024;            // keep bits of the tile: 4 lane groups x 128 queries x u16
-  constexpr int BUF = 2 * TILE + MASKB;
-  constexpr int NBUF = 3;
-  __shared__ __attribute__((aligned(1024))) char ring0[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring1[BUF];
-  __shared__ __attribute__((aligned(1024))) char ring2[BUF];
-  __shared__ __attribute__((aligned(16))) uint8_t kvl[QD_TKMAX];
-  __shared__ int kfull[QD_TKMAX / FW_KT];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, c = lane & 31;
-  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
-  const float scale = a.scale, drop_scale = a.drop_scale;
-  const float* __restrict__ lse = a.lse;
-  const int nqb = (Tq + QB - 1) / QB;
-  const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
-  const int bh = L / nqb, qb = L % nqb;
-  const int b = bh / H, hh = bh % H;
-  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv, lddo = a.lddo;
-  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + hh * HD;
-  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + hh * HD;
-  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + hh * HD;
-  const bf16* dOg = (const bf16*)a.dout + (int64_t)b * Tq * lddo + hh * HD;
-  const int q = qb * QB + w * 32 + c;
-  const bool qok = q < Tq;
-  const float cq = scale * LOG2E;
-  const int KT = mask_kt(Tk);
-  const int64_t ldm = mask_ld(Tq);
-  const uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
-
-  // ---- prologue: Q', dO as B operands (k-step s: columns 16 s + 8 h + 0..7), lse, delta ----
-  bf16x8 qf[4], df[4];
-  float part = 0.f;
-  {
-    const bf16* orow = (const bf16*)a.out + ((int64_t)b * Tq + q) * a.ldo + hh * HD;
-    const bf16* lrow = a.out_lo ? (const bf16*)a.out_lo + ((int64_t)b * Tq + q) * a.ldo + hh * HD : nullptr;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int col = 16 * s + 8 * h;
-      if (qok) {
-        qf[s] = *reinterpret_cast<const bf16x8*>(Qg + (int64_t)q * ldq + col);
-        df[s] = *reinterpret_cast<const bf16x8*>(dOg + (int64_t)q * lddo + col);
-        const bf16x8 of = *reinterpret_cast<const bf16x8*>(orow + col);
-        if (lrow) {  // O = hi + lo: delta from the unrounded output
-          const bf16x8 ol = *reinterpret_cast<const bf16x8*>(lrow + col);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) part += (float)df[s][j] * ((float)of[j] + (float)ol[j]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) part += (float)df[s][j] * (float)of[j];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[s][j] = df[s][j] = (bf16)0.f;
-      }
-    }
-  }
-  // the query's other 32 dims live in the partner lane l ^ 32
-  auto psw = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
-  const float dl = __uint_as_float(psw[0]) + __uint_as_float(psw[1]);
-  const float lq = qok ? lse[(int64_t)bh * Tq + q] * LOG2E - (DROP ? log2f(drop_scale) : 0.f) : INFINITY;
-  const float dq = qok ? -dl * (DROP ? 1.f / drop_scale : 1.f) : 0.f;
-  if (h == 0 && qok) {  // delta and the dK/dV kernel's row constants (planes 1, 2)
-    const int64_t plane = (int64_t)B * H * Tq;
-    a.delta[(int64_t)bh * Tq + q] = dl;
-    a.delta[plane + (int64_t)bh * Tq + q] = dq;
-    a.delta[2 * plane + (int64_t)bh * Tq + q] = -lq;
-  }
-  if (seq_has_no_key(a, b, tid)) {  // empty_uniform: dQ = 0 (delta above is still written)
-    bf16* dQz = (bf16*)a.dq + ((int64_t)b * Tq + q) * a.lddq + hh * HD;
-    if (qok)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(dQz + 16 * u + 8 * h) = make_uint4(0u, 0u, 0u, 0u);
-    return;
-  }
-  if (!a.qpre) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * cq);
-  }
-  const int nkt = (Tk + FW_KT - 1) / FW_KT;
-  for (int k = tid; k < nkt * FW_KT; k += NT) kvl[k] = k < Tk ? (a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
-  __syncthreads();
-  for (int t = tid; t < nkt; t += NT) {
-    int ok = 1;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t v = reinterpret_cast<const uint32_t*>(kvl)[t * 16 + j];
-      ok &= ((v - 0x01010101u) & ~v & 0x80808080u) == 0u;
-    }
-    kfull[t] = ok;
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]), "v"(df[s]));
-  __syncthreads();
-
-  const f32x16 nls = splat16(-lq), ndq = splat16(dq);
-  f32x16 dqa[2];
-  dqa[0] = dqa[1] = splat16(0.f);
-
-  auto ring = [&](auto bi) -> char* {
-    constexpr int BI = decltype(bi)::value;
-    return BI == 0 ? ring0 : (BI == 1 ? ring1 : ring2);
-  };
-  Rows64S32 rk, rv;
-  rk.init(Kg, ldk, Tk, w, lane);
-  rv.init(Vg, ldv, Tk, w, lane);
-  // keep bits (wave 1): lane (g, cc) reads words [tile][g][this block's 128 queries], column chunk cc
-  const rp_srd srd_m = make_srd(mrow);
-  int64_t mcol = (int64_t)qb * QB + (lane & 15) * 8;
-  mcol = mcol < ldm - 8 ? mcol : ldm - 8;
-  const uint32_t vo_m = (uint32_t)((((int64_t)(lane >> 4)) * ldm + mcol) * 2);
-  const bool xfast = (int64_t)KT * 4 * ldm * 2 < ((int64_t)1 << 31) && rk.fast && rv.fast;
-  const uint32_t slot_lds[3] = {lds_addr(ring0), lds_addr(ring1), lds_addr(ring2)};
-  auto issue = [&](int it, auto bi) {
-    constexpr int BI = decltype(bi)::value;
-    char* buf = ring(bi);
-    const int k0 = it * FW_KT;
-    if (xfast && k0 + FW_KT <= Tk) {
-      const uint32_t t = slot_lds[BI];
-      const uint32_t pk = t + (uint32_t)(w * 2) * 1024u;
-      dma16b_x4(rk.srd, rk.vo0, rk.vo1, (uint32_t)k0 * rk.rowbytes, rv.srd, rv.vo0, rv.vo1,
-                (uint32_t)k0 * rv.rowbytes, pk);
-      if (DROP && w == 1) dma16b(srd_m, vo_m, (uint32_t)it * 8u * (uint32_t)ldm, t + 2 * TILE);
-    } else {
-      dma_rows64_s32(Kg, ldk, k0, Tk, buf, w, lane);
-      dma_rows64_s32(Vg, ldv, k0, Tk, buf + TILE, w, lane);
-      if (DROP && w == 1) dma16(mrow + ((int64_t)it * 4 + (lane >> 4)) * ldm + mcol, lds_addr(buf + 2 * TILE));
-    }
-  };
-  auto wait_tile = [&](bool next) {
-    if (!next)
-      wait_vm<0>();
-    else if (DROP && w == 1)
-      wait_vm<5>();
-    else
-      wait_vm<4>();
-  };
-  issue(0, std::integral_constant<int, 0>());
-  if (nkt > 1) issue(1, std::integral_constant<int, 1>());
-
-  auto step = [&](auto bi, int it) {
-    constexpr int BI = decltype(bi)::value;
-    wait_tile(it + 1 < nkt);
-    raw_barrier();
-    if (it + 2 < nkt) issue(it + 2, std::integral_constant<int, (BI + 2) % NBUF>());
-    const char* Kl = ring(bi);
-    const char* Vl = Kl + TILE;
-    uint32_t kw0 = 0u, kw1 = 0u;
-    if constexpr (DROP) {
-      const uint16_t* mw = reinterpret_cast<const uint16_t*>(Kl + 2 * TILE);
-      kw0 = mw[h * QB + w * 32 + c];
-      kw1 = mw[(h + 2) * QB + w * 32 + c];
-    }
-    const bool full = kfull[it] != 0;
-    // one 32-key half at a time (halves the live S / dP accumulators)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f32x16 s, dp;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s = mfma32(row32_lds(Kl, 32 * t, ks, lane), qf[ks], ks == 0 ? nls : s);
-        dp = mfma32(row32_lds(Vl, 32 * t, ks, lane), df[ks], ks == 0 ? ndq : dp);
-      }
-      if (!full) {  // masked keys: P = 0
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t vb = *reinterpret_cast<const uint32_t*>(kvl + it * FW_KT + 32 * t + 8 * j + 4 * h);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (((vb >> (8 * r)) & 0xFFu) == 0u) s[4 * j + r] = -INFINITY;
-        }
-      }
-      // dS^T = P^T * ds * (keep ? acc : -delta/ds)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const float p = rp_exp2(s[v]);
-        if constexpr (DROP) {
-          const int j = v >> 2, r = v & 3;
-          const uint32_t km = keep_mask((j & 1) ? kw1 : kw0, (2 * t + (j >> 1)) * 4 + r);
-          s[v] = p * bfi_select(km, dp[v], dq);
-        } else {
-          s[v] = p * dp[v];
-        }
-      }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const bf16x8 sf = pack8_32(s, kk);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) dqa[dt] = mfma32(col32_lds(Kl, 32 * t + 16 * kk, 32 * dt, lane), sf, dqa[dt]);
-      }
-    }
-  };
-  for (int it = 0; it < nkt; it += NBUF) {
-    step(std::integral_constant<int, 0>(), it);
-    if (it + 1 < nkt) step(std::integral_constant<int, 1>(), it + 1);
-    if (it + 2 < nkt) step(std::integral_constant<int, 2>(), it + 2);
-  }
-  // store dQ[q][d] = scale * dQ^T (16-byte stores after a permlane32 swap, as the forward's O)
-  bf16* dQ = (bf16*)a.dq + ((int64_t)b * Tq + q) * a.lddq + hh * HD;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      uint32_t A[2], Bv[2];
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const bf16 x0 = (bf16)(dqa[dt][8 * u + 2 * pr] * scale), x1 = (bf16)(dqa[dt][8 * u + 2 * pr + 1] * scale);
-        const bf16 y0 = (bf16)(dqa[dt][8 * u + 4 + 2 * pr] * scale), y1 = (bf16)(dqa[dt][8 * u + 4 + 2 * pr + 1] * scale);
-        A[pr] = (uint32_t)__builtin_bit_cast(uint16_t, x0) | ((uint32_t)__builtin_bit_cast(uint16_t, x1) << 16);
-        Bv[pr] = (uint32_t)__builtin_bit_cast(uint16_t, y0) | ((uint32_t)__builtin_bit_cast(uint16_t, y1) << 16);
-      }
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        auto r = __builtin_amdgcn_permlane32_swap(A[pr], Bv[pr], false, false);
-        A[pr] = r[0];
-        Bv[pr] = r[1];
-      }
-      if (qok) *reinterpret_cast<uint4*>(dQ + 32 * dt + 16 * u + 8 * h) = make_uint4(A[0], A[1], Bv[0], Bv[1]);
-    }
-}
-
-// =================================================================================================
-// forward, 8-wave ping-pong (bf16, 256 queries per workgroup, one workgroup per CU): the 32x32x16 data
-// flow of attn_fwd32_kernel with the two waves that share a SIMD (waves w and w + 4) offset by half a
-// key tile, so that on every SIMD one wave's MFMA segment runs beside its partner's softmax / dropout
-// VALU segment (MI355X_MICROARCH.md "Two waves per SIMD", cdna_hip_programming.md T15/T16):
-//   MFMA step t:    issue the LDS-DMA of key tile t + 2; O^T += V^T P^T of tile t - 1 (8 MFMAs);
-//                   S^T(t) = K Q'^T - m (8 MFMAs); wait for this wave's pieces of tile t + 1; barrier
-//   softmax step t: key mask, lane-local max / deferred rescale, P = exp2, pack to bf16, row sums on
-//                   the matrix core (4 MFMAs), dropout keep bits (mask + store); barrier
-// Waves 0..3 run MFMA step t while waves 4..7 run softmax step t - 1 and the reverse in the next
-// segment: waves 4..7 enter one barrier late (their first segment is idle) and waves 0..3 leave with
-// one barrier more, so every wave executes the same number of s_barrier.  Tile t is read by S(t)
-// (segments 2t / 2t + 1 for the two halves) and by P V(t) (segments 2t + 2 / 2t + 3): a four-slot ring,
-// the DMA of tile t + 2 issued at the start of MFMA step t (its slot's last reader, P V(t - 2) of waves
-// 4..7, ended with segment 2t - 1), landing before segment 2t + 4.  Each wave moves one 1 KB piece of K
-// and one of V per tile (16 KB per tile for 256 queries: half the LDS-DMA traffic per query of the
-// 128-query kernels).  Static priority for the younger half (waves 4..7: s_setprio 1 once, T5 static
-// form).  Keep bits, outputs and lse as attn_fwd32_kernel.
-// =================================================================================================
-constexpr int PP_NW = 8, PP_NT = PP_NW * 64, PP_QB = PP_NW * 32, PP_SLOT = 2 * FW_KT * 128;
-
-// two LDS-DMA pieces (one per descriptor) with m0 saved once
-__device__ __forceinline__ void dma16b_x2(const rp_srd& s0, uint32_t v0, uint32_t o0, uint32_t l0, const rp_srd& s1,
-                                          uint32_t v1, uint32_t o1, uint32_t l1) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %3, %5, %7 offen lds\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %4, %6, %8 offen lds\n\t"
-      "s_nop 0\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(l0), "s"(l1), "v"(v0), "v"(v1), "s"(s0), "s"(s1), "s"(o0), "s"(o1)
-      : "memory");
-}
-
-template <bool DROP, bool LOCK, int PRIO = 1>
-__global__ __launch_bounds__(PP_NT, 2) void attn_fwd_pp_kernel(MhaDev a) {
-  __shared__ __attribute__((aligned(1024))) char ring[4 * PP_SLOT];
-  __shared__ __attribute__((aligned(16))) uint8_t kvl[FD_TKMAX];
-  __shared__ int kfull[FD_TKMAX / FW_KT];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // the younger wave of each SIMD pair runs half a tile behind its partner: pair by the SIMD each wave
-  // actually runs on (hardware register HW_ID, SIMD_ID bits) — dispatch order is not an architectural
-  // guarantee; any assignment stays correct (both roles execute the same barriers), only the overlap
-  // depends on it
-  __shared__ int simd_of[PP_NW];
-  {
-    uint32_t sid;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID, 4, 2)" : "=s"(sid));
-    if (lane == 0) simd_of[w] = (int)sid;
-  }
-  __syncthreads();
-  bool young = false;
-  {
-    const int mine = __builtin_amdgcn_readfirstlane(simd_of[w]);
-#pragma unroll
-    for (int v = 0; v < PP_NW; ++v)
-      if (v < w && __builtin_amdgcn_readfirstlane(simd_of[v]) == mine) young = true;
-  }
-  const int h = lane >> 5, c = lane & 31;
-  const int B = a.B, H = a.H, Tq = a.Tq, Tk = a.Tk;
-  const uint32_t drop_thresh = a.drop_thresh;
-  const float drop_scale = a.drop_scale;
-  const float scale = a.scale;
-  const int nqb = (Tq + PP_QB - 1) / PP_QB;
-  const int L = rp_xcd_remap(blockIdx.x, nqb * B * H);
-  const int bh = L / nqb, qb = L % nqb;
-  const int b = bh / H, hh = bh % H;
-  const int64_t ldq = a.ldq, ldk = a.ldk, ldv = a.ldv;
-  const bf16* Qg = (const bf16*)a.q + (int64_t)b * Tq * ldq + hh * HD;
-  const bf16* Kg = (const bf16*)a.k + (int64_t)b * Tk * ldk + hh * HD;
-  const bf16* Vg = (const bf16*)a.v + (int64_t)b * Tk * ldv + hh * HD;
-  const int q = qb * PP_QB + w * 32 + c;
-  const uint32_t seed_bh = rp_hash(rp_seed_eff(a.seed_base, a.seed), (uint32_t)bh);
-  const float cq = scale * LOG2E;
-  const int KT = mask_kt(Tk);
-  const int64_t ldm = mask_ld(Tq);
-  uint16_t* mrow = a.dmask ? a.dmask + (int64_t)bh * KT * 4 * ldm : nullptr;
-  bool novalid;
-  {  // empty_uniform: does the sequence have no valid key?  (512 threads)
-    int any = 0;
-    if (a.empty_uniform)
-      for (int k = tid; k < Tk; k += PP_NT) any |= a.kvalid[(int64_t)b * Tk + k];
-    novalid = a.empty_uniform && __syncthreads_or(any) == 0;
-  }
-
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    if (q < Tq && !novalid) {
-      qf[s] = *reinterpret_cast<const bf16x8*>(Qg + (int64_t)q * ldq + 16 * s + 8 * h);
-      if (!a.qpre) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * cq);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)0.f;
-    }
-  }
-  const int nkt = (Tk + FW_KT - 1) / FW_KT;
-  for (int k = tid; k < nkt * FW_KT; k += PP_NT)
-    kvl[k] = k < Tk ? (novalid || a.kvalid[(int64_t)b * Tk + k] != 0) : 0;
-  __syncthreads();
-  // per-tile "no masked key" flags as one 64-bit scalar mask (nkt <= FD_TKMAX / 64 = 64): wave 0's lane t
-  // tests tile t, a ballot makes the mask, LDS hands it to the other waves
-  if (w == 0) {
-    int ok = 0;
-    if (lane < nkt) {
-      ok = 1;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t v = reinterpret_cast<const uint32_t*>(kvl)[lane * 16 + j];
-        ok &= ((v - 0x01010101u) & ~v & 0x80808080u) == 0u;
-      }
-    }
-    const uint64_t bal = __ballot(ok);
-    if (lane == 0) {
-      kfull[0] = (int)(uint32_t)bal;
-      kfull[1] = (int)(uint32_t)(bal >> 32);
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[s]));
-  __syncthreads();
-  const uint64_t fullmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(kfull[1]) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane(kfull[0]);
-
-  // row sums of P (before dropout) on the VALU, per lane over its 32 keys of each tile (the partner lane
-  // l ^ 32 holds the query's other 32): an MFMA in the softmax segment would queue behind the partner
-  // wave's MFMA segment on the shared matrix pipe (measured: the softmax segment stretched to ~1,600
-  // cycles with four row-sum MFMAs in it)
-  f32x16 o[2];
-  o[0] = o[1] = splat16(0.f);
-  float lsum = 0.f;
-  float m = 0.f;
-  bool mset = false;
-  float gthr = -INFINITY;
-  f32x16 negm = splat16(0.f);
-  uint64_t st0 = 0, st1 = 0;
-  if constexpr (DROP) {
-    st0 = mwc_seed(rp_hash(seed_bh, (uint32_t)q * 4u + (uint32_t)h));
-    st1 = mwc_seed(rp_hash(seed_bh, (uint32_t)q * 4u + (uint32_t)(h + 2)));
-  }
-  const short ts = (short)((int)drop_thresh - 32768);
-  const i16x2 t2 = {ts, ts};
-
-  // LDS-DMA: wave w moves rows 8w..8w+7 of the K tile and of the V tile (one 1 KB piece each)
-  const rp_srd srd_k = make_srd(Kg), srd_v = make_srd(Vg);
-  const int prow = 8 * w + (lane >> 3), pch = (lane & 7) ^ swz32(prow);
-  const uint32_t vo_k = (uint32_t)((prow * ldk + pch * 8) * 2), vo_v = (uint32_t)((prow * ldv + pch * 8) * 2);
-  const bool xfast = ((int64_t)Tk + 64) * ldk * 2 < ((int64_t)1 << 31) && ((int64_t)Tk + 64) * ldv * 2 < ((int64_t)1 << 31);
-  const uint32_t ring_lds = lds_addr(ring);
-  auto issue = [&](int it) {
-    const int k0 = it * FW_KT;
-    const uint32_t dst = ring_lds + (uint32_t)(it & 3) * PP_SLOT + (uint32_t)w * 1024u;
-    if (xfast && k0 + FW_KT <= Tk) {
-      dma16b_x2(srd_k, vo_k, (uint32_t)k0 * (uint32_t)(ldk * 2), dst, srd_v, vo_v, (uint32_t)k0 * (uint32_t)(ldv * 2),
-                dst + 8192u);
-    } else {  // partial tile: clamped source rows (their keys are masked through kvl)
-      int rr = k0 + prow;
-      rr = rr < Tk ? rr : Tk - 1;
-      dma16(Kg + (int64_t)rr * ldk + pch * 8, dst);
-      dma16(Vg + (int64_t)rr * ldv + pch * 8, dst + 8192u);
-    }
-  };
-  issue(0);
-  if (nkt > 1) issue(1);
-  if (nkt > 1) wait_vm<2>(); else wait_vm<0>();
-  raw_barrier();
-  // static priority (T5 static form): PRIO 1 the younger half (default), 2 the older half, 0 none
-  if ((PRIO == 1 && young) || (PRIO == 2 && !young)) __builtin_amdgcn_s_setprio(1);
-  if (young && !LOCK) raw_barrier();  // the younger half starts one segment late (LOCK: diagnostic, in step)
-
-  // -DRP_PP_STAMPS diagnostic build only (never the shipped library): s_memtime after every barrier of
-  // workgroup 0, written over the lse output ([wave][64 stamps] uint64)
-#ifdef RP_PP_STAMPS
-  int nst = 0;
-  uint64_t* stamps = reinterpret_cast<uint64_t*>(a.lse) + (int64_t)w * 64;
-  auto stamp = [&]() {
-    const uint64_t tt = __builtin_amdgcn_s_memtime();
-    if (blockIdx.x == 0 && lane == 0 && nst < 64) stamps[nst] = tt;
-    ++nst;
-  };
-#else
-  auto stamp = [&]() {};
-#endif
-  stamp();
-  f32x16 s[2];
-  bf16x8 pf[4];
-  // operands in registers: vA = the V^T fragments of the next P V (read at the start of the softmax
-  // step, landing during its VALU), kA = the K fragments of S (read at the start of the MFMA step,
-  // landing under its P V MFMAs)
-  bf16x8 vA[8], kA[8];
-  auto mfma_step = [&](auto bi, int t) {
-    constexpr int SL = decltype(bi)::value;   // slot of tile t
-    if (t + 2 < nkt) issue(t + 2);
-    {
-      const char* Kl = ring + SL * PP_SLOT;
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) kA[4 * tt + ks] = row32_lds(Kl, 32 * tt, ks, lane);
-    }
-    if (t > 0) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(vA[2 * k + dt], pf[k], o[dt]);
-    }
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) s[tt] = mfma32(kA[4 * tt + ks], qf[ks], ks == 0 ? negm : s[tt]);
-    stamp();
-    // this wave's pieces of tile t + 1 have landed (issued at MFMA step t - 1, or before the loop);
-    // issued after them: the keep-bit stores of softmax step t - 1 and the pieces of tile t + 2
-    if (t + 1 < nkt) {
-      const int n = (DROP && t > 0 ? 2 : 0) + (t + 2 < nkt ? 2 : 0);
-      if (n == 4)
-        wait_vm<4>();
-      else if (n == 2)
-        wait_vm<2>();
-      else
-        wait_vm<0>();
-    }
-    raw_barrier();
-    stamp();
-  };
-  auto softmax_step = [&](auto bi, int t) {
-    constexpr int SL = decltype(bi)::value;
-    {  // V^T fragments of tile t for the P V of the next MFMA step
-      const char* Vl = ring + SL * PP_SLOT + 8192;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) vA[2 * k + dt] = col32_lds(Vl, 16 * k, 32 * dt, lane);
-    }
-    if (((fullmask >> t) & 1u) == 0) {
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t vb = *reinterpret_cast<const uint32_t*>(kvl + t * FW_KT + 32 * tt + 8 * j + 4 * h);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (((vb >> (8 * r)) & 0xFFu) == 0u) s[tt][4 * j + r] = -INFINITY;
-        }
-    }
-    const float mx = max32x2(s[0], s[1]);
-    if (__ballot(mx > gthr) != 0) {
-      auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      const float rel = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-      const bool gq = mset ? rel > RESCALE_LOG2 : rel > -INFINITY;
-      const float alpha = gq ? (mset ? rp_exp2(-rel) : 0.f) : 1.f;
-      const float sub = gq ? rel : 0.f;
-      lsum *= alpha;
-      o[0] *= alpha;
-      o[1] *= alpha;
-      m += sub;
-      mset = mset || gq;
-      gthr = mset ? RESCALE_LOG2 : -INFINITY;
-      negm = splat16(-m);
-      s[0] -= sub;
-      s[1] -= sub;
-    }
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) s[tt][v] = rp_exp2(s[tt][v]);
-    {
-      float t8[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) t8[u] = (s[0][2 * u] + s[0][2 * u + 1]) + (s[1][2 * u] + s[1][2 * u + 1]);
-      lsum += ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) pf[k] = pack8_32(s[k >> 1], k & 1);
-    if constexpr (DROP) {
-      uint32_t acc0 = 0u, acc1 = 0u;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint4 u = __builtin_bit_cast(uint4, pf[k]);
-        uint32_t mk[4];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const uint32_t w0 = rp_mwc_next(st0), w1 = rp_mwc_next(st1);
-          const i16x2 d0 = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w0), t2);
-          const i16x2 d1 = __builtin_elementwise_sub_sat(__builtin_bit_cast(i16x2, w1), t2);
-          mk[e] = __builtin_bit_cast(uint32_t, (i16x2)(d0 >> (short)15));
-          mk[2 + e] = __builtin_bit_cast(uint32_t, (i16x2)(d1 >> (short)15));
-          const int bb = 4 * k + 2 * e;
-          acc0 |= ~mk[e] & ((1u << bb) | (1u << (16 + bb + 1)));
-          acc1 |= ~mk[2 + e] & ((1u << bb) | (1u << (16 + bb + 1)));
-        }
-        u.x &= ~mk[0];
-        u.y &= ~mk[1];
-        u.z &= ~mk[2];
-        u.w &= ~mk[3];
-        pf[k] = __builtin_bit_cast(bf16x8, u);
-      }
-      uint16_t* mr = mrow + ((int64_t)t * 4 + h) * ldm + q;
-      mr[0] = (uint16_t)((acc0 & 0xFFFFu) | (acc0 >> 16));
-      mr[2 * ldm] = (uint16_t)((acc1 & 0xFFFFu) | (acc1 >> 16));
-    }
-    stamp();
-    raw_barrier();
-    stamp();
-  };
-  for (int t = 0; t < nkt; t += 4) {
-    mfma_step(std::integral_constant<int, 0>(), t);
-    softmax_step(std::integral_constant<int, 0>(), t);
-    if (t + 1 < nkt) {
-      mfma_step(std::integral_constant<int, 1>(), t + 1);
-      softmax_step(std::integral_constant<int, 1>(), t + 1);
-    }
-    if (t + 2 < nkt) {
-      mfma_step(std::integral_constant<int, 2>(), t + 2);
-      softmax_step(std::integral_constant<int, 2>(), t + 2);
-    }
-    if (t + 3 < nkt) {
-      mfma_step(std::integral_constant<int, 3>(), t + 3);
-      softmax_step(std::integral_constant<int, 3>(), t + 3);
-    }
-  }
-  // the last P V (its V^T fragments were read by the last softmax step)
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(vA[2 * k + dt], pf[k], o[dt]);
-  if (!young && !LOCK) raw_barrier();  // the older half's extra barrier (matches the younger half's late start)
-
-  auto lsw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
-  const float l = __uint_as_float(lsw[0]) + __uint_as_float(lsw[1]);
-  const float inv = drop_scale / l;
-  const int64_t ldo = a.ldo;
-  const bool qok = q < Tq;
-  bf16* orow = (bf16*)a.out + ((int64_t)b * Tq + q) * ldo + hh * HD;
-  bf16* lorow = a.out_lo ? (bf16*)a.out_lo + ((int64_t)b * Tq + q) * ldo + hh * HD : nullptr;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      uint32_t A[2], Bv[2], Al[2], Bl[2];
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const float x0 = o[dt][8 * u + 2 * pr] * inv, x1 = o[dt][8 * u + 2 * pr + 1] * inv;
-        const float y0 = o[dt][8 * u + 4 + 2 * pr] * inv, y1 = o[dt][8 * u + 4 + 2 * pr + 1] * inv;
-        const bf16 bx0 = (bf16)x0, bx1 = (bf16)x1, by0 = (bf16)y0, by1 = (bf16)y1;
-        A[pr] = (uint32_t)__builtin_bit_cast(uint16_t, bx0) | ((uint32_t)__builtin_bit_cast(uint16_t, bx1) << 16);
-        Bv[pr] = (uint32_t)__builtin_bit_cast(uint16_t, by0) | ((uint32_t)__builtin_bit_cast(uint16_t, by1) << 16);
-        const bf16 lx0 = (bf16)(x0 - (float)bx0), lx1 = (bf16)(x1 - (float)bx1);
-        const bf16 ly0 = (bf16)(y0 - (float)by0), ly1 = (bf16)(y1 - (float)by1);
-        Al[pr] = (uint32_t)__builtin_bit_cast(uint16_t, lx0) | ((uint32_t)__builtin_bit_cast(uint16_t, lx1) << 16);
-        Bl[pr] = (uint32_t)__builtin_bit_cast(uint16_t, ly0) | ((uint32_t)__builtin_bit_cast(uint16_t, ly1) << 16);
-      }
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        auto r = __builtin_amdgcn_permlane32_swap(A[pr], Bv[pr], false, false);
-        A[pr] = r[0];
-        Bv[pr] = r[1];
-        auto rl = __builtin_amdgcn_permlane32_swap(Al[pr], Bl[pr], false, false);
-        Al[pr] = rl[0];
-        Bl[pr] = rl[1];
-      }
-      const int d0 = 32 * dt + 16 * u + 8 * h;
-      if (qok) {
-        *reinterpret_cast<uint4*>(orow + d0) = make_uint4(A[0], A[1], Bv[0], Bv[1]);
-        if (lorow) *reinterpret_cast<uint4*>(lorow + d0) = make_uint4(Al[0], Al[1], Bl[0], Bl[1]);
-      }
-    }
-#ifndef RP_PP_STAMPS
-  if (qok && h == 0) a.lse[(int64_t)bh * Tq + q] = m * 0.6931471805599453f + logf(l);
-#endif
-}
-
-// 128-row blocks (the LDS-DMA kernels) from this many workgroups up; 64-row blocks below
-constexpr int64_t ATTN_SMALL_GRID = 256;
-
-// RP_ATTN_BLOCK=64 | 128 forces the workgroup block (queries for fwd / dQ, keys for dK/dV), for tuning
-static int attn_block_override() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_ATTN_BLOCK");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
-// RP_ATTN_DMA=0 selects the register-staged backward kernels (A/B tuning)
-static bool attn_dma_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_ATTN_DMA");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v != 0;
-}
-
-// RP_ATTN_DMA_Q=0 selects the register-staged dQ kernel only (A/B tuning)
-static bool attn_dma_q_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_ATTN_DMA_Q");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v != 0 && attn_dma_enabled();
-}
-
-// RP_ATTN_KV32=1: the 32x32x16 dK/dV kernel instead of the 16x16x32 one — measured slower at the
-// metric shape, kept as a tested option.  Read at every launch (tests flip it).
-static bool attn_kv32_enabled() {
-  const char* e = getenv("RP_ATTN_KV32");
-  return e && e[0] == '1';
-}
-
-// RP_ATTN_PIPE=0: the dK/dV kernel processes its two 32-query halves one after the other instead of
-// issuing both halves' S / dP products ahead of the VALU (A/B tuning)
-static bool attn_pipe_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_ATTN_PIPE");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v != 0;
-}
-
-static size_t attn_fwd_pad() {
-  static long v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_ATTN_FWD_LDS_PAD");
-    v = e ? atol(e) : 0;
-    if (v < 0 || v > 65536) v = 0;
-  }
-  return (size_t)v;
-}
-
-// RP_ATTN_DMA_F=0 selects the register-staged forward kernel (A/B tuning)
-static bool attn_dma_f_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_ATTN_DMA_F");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v != 0 && attn_dma_enabled();
-}
-
-// RP_ATTN_FWD_PP=1 selects the 8-wave ping-pong forward (A/B; read per launch; off by default until it
-// beats the 16x16x32 kernel)
-static bool attn_fwd_pp_enabled() {
-  const char* e = getenv("RP_ATTN_FWD_PP");
-  return e && e[0] == '1';
-}
-// RP_ATTN_FWD32=1 selects the 4-wave 32x32x16 forward (A/B; read per launch; off by default)
-static bool attn_fwd32_enabled() {
-  const char* e = getenv("RP_ATTN_FWD32");
-  return e && e[0] == '1';
-}
-
-// compute units of the current device (cached per device)
+// compute units of the current device (cached per device); every "fills the CUs once / twice" rule
+// below is in units of this count (256 on a whole MI355X)
 static int64_t attn_cu_count() {
   static int cus[64] = {0};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return ATTN_SMALL_GRID;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
   if (cus[dev] == 0) {
     int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = (int)ATTN_SMALL_GRID;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
     cus[dev] = n;
   }
   return cus[dev];
 }
 
+// 128-row blocks (the LDS-DMA kernels) from one workgroup per CU up; 64-row blocks below.  At one per
+// CU the 128-row LDS-DMA kernel still beats the 64-row register-staged one at twice the workgroups
+// (config 4, B = 1, T = 4096: fwd 85 vs 96 us; dQ 78 vs 101; step 9.59 -> 9.06 ms).  RP_ATTN_BLOCK=64 |
+// 128 forces one (tuning; read once)
+static bool attn_small(int64_t big_grid) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RP_ATTN_BLOCK");
+    v = e ? atoi(e) : 0;
+  }
+  if (v == 64) return true;
+  if (v == 128) return false;
+  return big_grid < attn_cu_count();
+}
+
 // Split workgroups (SPL = 2: eight waves, the reduced sequence range in two halves, partials merged in
 // LDS) for grids of 128-row blocks that fill the CUs once but not twice (config 4: B = 1, T = 4096 is
 // 256 blocks): two waves per SIMD instead of one.  RP_ATTN_SPLIT=0 never, =1 whenever the range has
-// two tiles (tests), unset: 256 <= grid < 384.  Read per launch.
+// two tiles (tests), unset: CUs <= grid < 1.5 CUs.  Read per launch (tests flip it).
 static bool attn_split(int64_t grid, int tiles) {
   if (tiles < 2) return false;
   const char* e = getenv("RP_ATTN_SPLIT");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return grid >= ATTN_SMALL_GRID && grid < ATTN_SMALL_GRID + ATTN_SMALL_GRID / 2;
+  const int64_t cus = attn_cu_count();
+  return grid >= cus && grid < cus + cus / 2;
 }
 
 template <typename T>
 int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
-  // 128-query blocks unless that leaves fewer than one workgroup per CU (256 CUs): then 64.  At one
-  // per CU the 128-row LDS-DMA kernel still beats the 64-row register-staged one at twice the
-  // workgroups (config 4, B = 1, T = 4096: 85 vs 96 us; dQ 78 vs 101; step 9.59 -> 9.06 ms)
   const int64_t big = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H;
-  const bool small = attn_block_override() ? attn_block_override() == 64 : big < ATTN_SMALL_GRID;
+  const bool small = attn_small(big);
   const int qb = small ? NW * 16 : FW_QB;
   const int nqb = (a.Tq + qb - 1) / qb;
   const dim3 grid((unsigned)(nqb * a.B * a.H));
@@ -3908,44 +2563,7 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
       hipLaunchKernelGGL((attn_fwd_kernel<T, true, 1>), grid, dim3(NT), 0, s, a);
     else
       hipLaunchKernelGGL((attn_fwd_kernel<T, false, 1>), grid, dim3(NT), 0, s, a);
-  } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX && attn_dma_f_enabled() && attn_fwd_pp_enabled() &&
-             (int64_t)((a.Tq + PP_QB - 1) / PP_QB) * a.B * a.H >= ATTN_SMALL_GRID) {
-    // the 8-wave ping-pong forward (256-query blocks) while its grid still fills every CU
-    const dim3 gpp((unsigned)((a.Tq + PP_QB - 1) / PP_QB * a.B * a.H));
-    const char* lk = getenv("RP_ATTN_PP_LOCK");  // diagnostic: both wave halves in step
-    const char* pr = getenv("RP_ATTN_PP_PRIO");  // diagnostic: 0 no priority, 2 the older half
-    if (pr && (pr[0] == '0' || pr[0] == '2')) {
-      if (pr[0] == '0') {
-        if (a.drop_thresh)
-          hipLaunchKernelGGL((attn_fwd_pp_kernel<true, false, 0>), gpp, dim3(PP_NT), 0, s, a);
-        else
-          hipLaunchKernelGGL((attn_fwd_pp_kernel<false, false, 0>), gpp, dim3(PP_NT), 0, s, a);
-      } else {
-        if (a.drop_thresh)
-          hipLaunchKernelGGL((attn_fwd_pp_kernel<true, false, 2>), gpp, dim3(PP_NT), 0, s, a);
-        else
-          hipLaunchKernelGGL((attn_fwd_pp_kernel<false, false, 2>), gpp, dim3(PP_NT), 0, s, a);
-      }
-    } else if (lk && lk[0] == '1') {
-      if (a.drop_thresh)
-        hipLaunchKernelGGL((attn_fwd_pp_kernel<true, true>), gpp, dim3(PP_NT), 0, s, a);
-      else
-        hipLaunchKernelGGL((attn_fwd_pp_kernel<false, true>), gpp, dim3(PP_NT), 0, s, a);
-    } else if (a.drop_thresh) {
-      hipLaunchKernelGGL((attn_fwd_pp_kernel<true, false>), gpp, dim3(PP_NT), 0, s, a);
-    } else {
-      hipLaunchKernelGGL((attn_fwd_pp_kernel<false, false>), gpp, dim3(PP_NT), 0, s, a);
-    }
-  } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX && attn_dma_f_enabled() && attn_fwd32_enabled()) {
-    // the 32x32x16 forward (query on the MFMA column)
-    if (a.drop_thresh)
-      hipLaunchKernelGGL((attn_fwd32_kernel<true>), grid, dim3(NT), 0, s, a);
-    else
-      hipLaunchKernelGGL((attn_fwd32_kernel<false>), grid, dim3(NT), 0, s, a);
-  } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX && attn_dma_f_enabled()) {
-    // RP_ATTN_FWD_LDS_PAD (bytes of unused dynamic LDS): tuning knob for the workgroups per CU
-    // (53.8 KB static -> three per CU, a fourth of the metric grid then runs as a one-per-CU tail)
-    const size_t pad = attn_fwd_pad();
+  } else if (std::is_same<T, bf16>::value && a.Tk <= FD_TKMAX) {
     const int nkt = (a.Tk + FW_KT - 1) / FW_KT;
     // grids of at most one block per CU (config 4: 256) on the three-part split kernel (three waves
     // per SIMD, the unsplit kernel's residency); RP_ATTN_SPLIT=3 forces it.  Measured and dropped: the
@@ -3970,9 +2588,9 @@ int launch_mha_fwd(const MhaDev& a, hipStream_t s) {
       else
         hipLaunchKernelGGL((attn_fwd_dma_kernel<false, 2>), grid, dim3(2 * NT), 0, s, as);
     } else if (a.drop_thresh) {
-      hipLaunchKernelGGL((attn_fwd_dma_kernel<true>), grid, dim3(NT), pad, s, a);
+      hipLaunchKernelGGL((attn_fwd_dma_kernel<true>), grid, dim3(NT), 0, s, a);
     } else {
-      hipLaunchKernelGGL((attn_fwd_dma_kernel<false>), grid, dim3(NT), pad, s, a);
+      hipLaunchKernelGGL((attn_fwd_dma_kernel<false>), grid, dim3(NT), 0, s, a);
     }
   } else {
     if (a.drop_thresh)
@@ -4001,23 +2619,16 @@ void launch_bwd_q(bool delta, const MhaDev& a, hipStream_t s) {
   }
 }
 
-// RP_ATTN_DQ32=1 selects the 32x32x16 dQ kernel (A/B; read per launch)
-static bool attn_dq32_enabled() {
-  const char* e = getenv("RP_ATTN_DQ32");
-  return e && e[0] == '1';
-}
-
 // the two-role backward (attn_bwd_roles_kernel): bf16 with the producer's Q prescale on the LDS-DMA
 // kernels, 128-row blocks on both sides, and both grids in the split range (attn_split); RP_ATTN_ROLES=0
 // keeps the two kernels (read per launch)
 static bool attn_roles(const MhaDev& a) {
   const char* e = getenv("RP_ATTN_ROLES");
   if (e && e[0] == '0') return false;
-  if (!a.qpre || a.empty_uniform || a.nosplit || a.Tk > QD_TKMAX || attn_block_override()) return false;
-  if (!attn_dma_enabled() || !attn_dma_q_enabled() || attn_kv32_enabled() || attn_dq32_enabled()) return false;
+  if (!a.qpre || a.empty_uniform || a.Tk > QD_TKMAX) return false;
   const int64_t gkv = (int64_t)((a.Tk + KV_KB - 1) / KV_KB) * a.B * a.H;
   const int64_t gq = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H;
-  if (gkv < ATTN_SMALL_GRID || gq < ATTN_SMALL_GRID) return false;
+  if (attn_small(gkv) || attn_small(gq)) return false;
   return attn_split(gkv, (a.Tq + KV_QT - 1) / KV_QT) && attn_split(gq, (a.Tk + FW_KT - 1) / FW_KT);
 }
 
@@ -4037,32 +2648,25 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     return rp_check_launch("rp_mha_bwd");
   }
   // dQ: 128-query blocks unless that leaves fewer than one workgroup per CU (then 64, as the forward)
-  const bool small = attn_block_override() ? attn_block_override() == 64
-                                           : (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H < ATTN_SMALL_GRID;
+  const dim3 gq((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
+  const bool small = attn_small((int64_t)gq.x);
+  const bool dma_q = !small && std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX;
   const bool fused = (phases & 5) == 5;
   if (fused) {
-    if (small) {
-      launch_bwd_q<T, 1>(true, a, s);
-    } else if (std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX && attn_dma_q_enabled() && attn_dq32_enabled()) {
-      // bf16, 128-query blocks: the 32x32x16 dQ kernel
-      const dim3 grid((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
-      if (a.drop_thresh)
-        hipLaunchKernelGGL((attn_bwd_q32_kernel<true>), grid, dim3(NT), 0, s, a);
-      else
-        hipLaunchKernelGGL((attn_bwd_q32_kernel<false>), grid, dim3(NT), 0, s, a);
-    } else if (std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX && attn_dma_q_enabled()) {
-      // bf16, 128-query blocks: the LDS-DMA staged dQ kernel (RP_ATTN_DMA=0: register staged)
-      const dim3 grid((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
-      if (attn_split((int64_t)grid.x, (a.Tk + FW_KT - 1) / FW_KT)) {
+    if (dma_q) {
+      // bf16, 128-query blocks: the LDS-DMA staged dQ kernel with the delta pre-pass fused in
+      if (attn_split((int64_t)gq.x, (a.Tk + FW_KT - 1) / FW_KT)) {
         if (a.drop_thresh)
-          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 2>), grid, dim3(2 * NT), 0, s, a);
+          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 2>), gq, dim3(2 * NT), 0, s, a);
         else
-          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false, 2>), grid, dim3(2 * NT), 0, s, a);
+          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false, 2>), gq, dim3(2 * NT), 0, s, a);
       } else if (a.drop_thresh) {
-        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true>), grid, dim3(NT), 0, s, a);
+        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true>), gq, dim3(NT), 0, s, a);
       } else {
-        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false>), grid, dim3(NT), 0, s, a);
+        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false>), gq, dim3(NT), 0, s, a);
       }
+    } else if (small) {
+      launch_bwd_q<T, 1>(true, a, s);
     } else {
       launch_bwd_q<T, 2>(true, a, s);
     }
@@ -4071,35 +2675,25 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   }
   if (phases & 2) {
     // 128-key blocks unless that leaves fewer than one workgroup per CU: then 64
-    const bool small_kv =
-        attn_block_override() ? attn_block_override() == 64 : (int64_t)nkb * a.B * a.H < ATTN_SMALL_GRID;
+    const bool small_kv = attn_small((int64_t)nkb * a.B * a.H);
     const dim3 grid(small_kv ? (unsigned)((a.Tk + NW * 16 - 1) / (NW * 16) * a.B * a.H) : (unsigned)(nkb * a.B * a.H));
-    // bf16 with the producer's Q prescale: the LDS-DMA staged kernel (RP_ATTN_DMA=0: register staged)
-    if (std::is_same<T, bf16>::value && a.qpre && !a.empty_uniform && attn_dma_enabled()) {
-      const bool pipe = attn_pipe_enabled();
-#define RP_KVD(DROPV, KTWV)                                                                        \
-  do {                                                                                             \
-    if (pipe)                                                                                      \
-      hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<DROPV, KTWV, true>), grid, dim3(NT), 0, s, a);  \
-    else                                                                                           \
-      hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<DROPV, KTWV, false>), grid, dim3(NT), 0, s, a); \
-  } while (0)
+    // bf16 with the producer's Q prescale: the LDS-DMA staged kernel
+    if (std::is_same<T, bf16>::value && a.qpre && !a.empty_uniform) {
       if (small_kv) {
-        if (a.drop_thresh) RP_KVD(true, 1); else RP_KVD(false, 1);
-      } else if (attn_kv32_enabled()) {
         if (a.drop_thresh)
-          hipLaunchKernelGGL((attn_bwd_kv32_kernel<true>), grid, dim3(NT), 0, s, a);
+          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<true, 1, true>), grid, dim3(NT), 0, s, a);
         else
-          hipLaunchKernelGGL((attn_bwd_kv32_kernel<false>), grid, dim3(NT), 0, s, a);
-      } else if (!a.nosplit && attn_split((int64_t)nkb * a.B * a.H, (a.Tq + KV_QT - 1) / KV_QT)) {
+          hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<false, 1, true>), grid, dim3(NT), 0, s, a);
+      } else if (attn_split((int64_t)nkb * a.B * a.H, (a.Tq + KV_QT - 1) / KV_QT)) {
         if (a.drop_thresh)
           hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<true, 2, false, 2>), grid, dim3(2 * NT), 0, s, a);
         else
           hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<false, 2, false, 2>), grid, dim3(2 * NT), 0, s, a);
+      } else if (a.drop_thresh) {
+        hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<true, 2, true>), grid, dim3(NT), 0, s, a);
       } else {
-        if (a.drop_thresh) RP_KVD(true, 2); else RP_KVD(false, 2);
+        hipLaunchKernelGGL((attn_bwd_kv_dma_kernel<false, 2, true>), grid, dim3(NT), 0, s, a);
       }
-#undef RP_KVD
     } else if (small_kv) {
       if (a.drop_thresh)
         hipLaunchKernelGGL((attn_bwd_kv_kernel<T, true, 1>), grid, dim3(NT), 0, s, a);
@@ -4113,18 +2707,17 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     }
   }
   if ((phases & 4) && !fused) {
-    const dim3 grid((unsigned)((a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
-    if (!small && std::is_same<T, bf16>::value && a.Tk <= QD_TKMAX && attn_dma_q_enabled() && !attn_dq32_enabled()) {
+    if (dma_q) {
       // bf16, 128-query blocks, delta formed beforehand: the LDS-DMA dQ kernel reading it
-      if (!a.nosplit && attn_split((int64_t)grid.x, (a.Tk + FW_KT - 1) / FW_KT)) {
+      if (attn_split((int64_t)gq.x, (a.Tk + FW_KT - 1) / FW_KT)) {
         if (a.drop_thresh)
-          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 2, false>), grid, dim3(2 * NT), 0, s, a);
+          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 2, false>), gq, dim3(2 * NT), 0, s, a);
         else
-          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false, 2, false>), grid, dim3(2 * NT), 0, s, a);
+          hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false, 2, false>), gq, dim3(2 * NT), 0, s, a);
       } else if (a.drop_thresh) {
-        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 1, false>), grid, dim3(NT), 0, s, a);
+        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<true, 1, false>), gq, dim3(NT), 0, s, a);
       } else {
-        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false, 1, false>), grid, dim3(NT), 0, s, a);
+        hipLaunchKernelGGL((attn_bwd_q_dma_kernel<false, 1, false>), gq, dim3(NT), 0, s, a);
       }
     } else if (small)
       launch_bwd_q<T, 1>(false, a, s);
@@ -4133,7 +2726,6 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   }
   return rp_check_launch("rp_mha_bwd");
 }
-
 int launch_mha_bwd_dtype(int dtype, int phases, const MhaDev& a, hipStream_t s) {
   return dtype == RP_BF16 ? launch_mha_bwd<bf16>(phases, a, s) : launch_mha_bwd<float>(phases, a, s);
 }
@@ -4183,7 +2775,7 @@ int make_dev(const char* fn, int dtype, int qpre, const rp_mha_args* p, int phas
 
 // the attention entry points take RP_ATTN_Q_PRESCALED or-ed into their dtype argument
 inline int attn_qpre(int dtype) { return (dtype & RP_ATTN_Q_PRESCALED) ? 1 : 0; }
-inline int attn_dtype(int dtype) { return dtype & ~(RP_ATTN_Q_PRESCALED | RP_ATTN_NO_SPLIT); }
+inline int attn_dtype(int dtype) { return dtype & ~RP_ATTN_Q_PRESCALED; }
 
 int mha_fwd_entry(int flagged, const rp_mha_args* p, void* stream) {
   const int dtype = attn_dtype(flagged);
@@ -4202,7 +2794,6 @@ int mha_bwd_entry(int flagged, const rp_mha_args* p, int phases, void* stream) {
   MhaDev a;
   const int rc = make_dev("rp_mha_bwd", dtype, attn_qpre(flagged), p, phases, a);
   if (rc) return rc;
-  a.nosplit = (flagged & RP_ATTN_NO_SPLIT) ? 1 : 0;
   if (a.B == 0 || a.Tq == 0 || a.Tk == 0) return RP_OK;
   hipStream_t s = (hipStream_t)stream;
   return dtype == RP_BF16 ? launch_mha_bwd<bf16>(phases, a, s) : launch_mha_bwd<float>(phases, a, s);
@@ -4270,6 +2861,13 @@ static int attn_bwd_packed(int phases, int dtype, const void* qkv, const void* o
                          dropmask, dout, dqkv, delta_ws);
   packed_offsets(a, attn_dtype(dtype));
   return mha_bwd_entry(dtype, &a, phases, stream);
+}
+
+extern "C" int rp_attn_bwd_uses_roles(int dtype, int B, int T, int H, int dk) {
+  if (attn_dtype(dtype) != RP_BF16 || dk != HD || B <= 0 || T <= 0 || H <= 0) return 0;
+  MhaDev a{};
+  a.B = B; a.Tq = T; a.Tk = T; a.H = H; a.qpre = attn_qpre(dtype);
+  return attn_roles(a) ? 1 : 0;
 }
 
 extern "C" int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,

@@ -5,7 +5,6 @@ current torch stream through ``_native.call``.  Outputs are allocated with the t
 allocator; the library itself never allocates.  There is no CPU path: CPU tensors raise.
 """
 import ctypes
-import os
 
 import torch
 
@@ -13,7 +12,6 @@ from . import _native as N
 
 _DT = {torch.float32: N.RP_F32, torch.bfloat16: N.RP_BF16}
 RP_ATTN_Q_PRESCALED = 0x100  # include/rp_api.h: q holds Q * scale * log2(e)
-RP_ATTN_NO_SPLIT = 0x200  # include/rp_api.h: four-wave backward workgroups (dQ runs beside dK/dV)
 LOG2E = 1.4426950408889634
 
 
@@ -409,22 +407,10 @@ def attn_fwd(qkv, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, q_prescaled=
     return out, lse, mask
 
 
-_FUSED_DELTA = os.environ.get("RP_ATTN_FUSED_DELTA", "1") != "0"
-# dQ beside dK/dV: delta first (its own small pass), then the dQ kernel on a side stream concurrently
-# with the dK/dV kernel on the launch stream, so each kernel's last partial round of workgroups
-# is filled by the other's (both grids are 4/3 of the CUs' three-per-CU residency at the metric shape)
-_BWD_OVERLAP = os.environ.get("RP_ATTN_BWD_OVERLAP", "0") == "1"
-# overlapped form on grids that fill the CUs once (config 4): the two four-wave grids side by side
-# instead of the eight-wave split workgroups (RP_ATTN_OVL_SPLIT=1 keeps those)
-_OVL_NOSPLIT = os.environ.get("RP_ATTN_OVL_SPLIT", "0") != "1"
-_SIDE = {}
-
-
-def _side_stream(dev):
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
-    if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=dev)
-    return _SIDE[key]
+def attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=False):
+    """True where attn_bwd runs the delta pass + ONE two-role launch (dK/dV and dQ workgroups side by
+    side: grids that fill the CUs once, e.g. config 4) instead of the fused-delta dQ kernel + dK/dV."""
+    return bool(N.load().rp_attn_bwd_uses_roles(_adt(qkv, q_prescaled), B, T, H, qkv.shape[1] // (3 * H)))
 
 
 def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, dropmask=None,
@@ -438,50 +424,28 @@ def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed
     delta = torch.empty(3, B, H, T, device=qkv.device, dtype=torch.float32)  # delta + 2 row-constant planes
     st, dt = _stream(qkv), _adt(qkv, q_prescaled)
     e0 = _tick("attn_bwd")
-    if _BWD_OVERLAP:
-        if _OVL_NOSPLIT:
-            dt |= RP_ATTN_NO_SPLIT
-        N.call("rp_attn_bwd_delta", dt, _p(out), _p(out_lo), _p(dout), _p(lse), B, T, H, dk, float(dropout_p),
-               _p(delta), st)
-        main = torch.cuda.current_stream(qkv.device)
-        side = _side_stream(qkv.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            e2 = _tick("attn_bwd_dq")
-            N.call("rp_attn_bwd_dq", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
-                   float(scale), float(dropout_p), _p(dropmask), _p(dqkv), ctypes.c_void_p(side.cuda_stream))
-            _tock(e2)
-        e1 = _tick("attn_bwd_dkdv")
-        N.call("rp_attn_bwd_dkdv", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
-               float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
-        _tock(e1)
-        main.wait_stream(side)  # before any tensor used on the side stream is released or reused
-        _tock(e0)
-        return dqkv
-    if _FUSED_DELTA and not ({"attn_bwd_dq", "attn_bwd_dkdv"} & set(_timer["names"])):
+    timed = {"attn_bwd_dq", "attn_bwd_dkdv", "attn_bwd_roles"} & set(_timer["names"])
+    roles = bool(timed) and attn_bwd_uses_roles(qkv, B, T, H, q_prescaled)
+    if not timed or roles:
         # one entry: the library launches the fused-delta dQ kernel then dK/dV, or, where each grid
-        # fills the CUs once but not twice (config 4), the delta pass and ONE two-role launch
+        # fills the CUs once but not twice (config 4), the delta pass and ONE two-role launch (timed
+        # whole as "attn_bwd_roles": the per-kernel timers must time what the step runs)
+        e3 = _tick("attn_bwd_roles") if roles else None
         N.call("rp_attn_bwd", dt, _p(qkv), _p(out), _p(out_lo), _p(dout), _p(lse), _p(key_valid), B, T, H, dk,
                float(scale), float(dropout_p), _p(dropmask), _p(dqkv), _p(delta), st)
+        _tock(e3)
         _tock(e0)
         return dqkv
-    if _FUSED_DELTA:  # per-kernel timing (bench.py roofline): the two kernels as separate calls  # dQ first, with the delta = rowsum(dO * O) pre-pass fused in; dK/dV reads it
-        e2 = _tick("attn_bwd_dq")
-        N.call("rp_attn_bwd_dq_delta", dt, _p(qkv), _p(out), _p(out_lo), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T,
-               H, dk, float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
-        _tock(e2)
-    else:
-        N.call("rp_attn_bwd_delta", dt, _p(out), _p(out_lo), _p(dout), _p(lse), B, T, H, dk, float(dropout_p),
-               _p(delta), st)
+    # per-kernel timing (bench.py roofline): the two kernels of rp_attn_bwd as separate calls — dQ
+    # first, with the delta = rowsum(dO * O) pre-pass fused in; dK/dV reads it
+    e2 = _tick("attn_bwd_dq")
+    N.call("rp_attn_bwd_dq_delta", dt, _p(qkv), _p(out), _p(out_lo), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T,
+           H, dk, float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
+    _tock(e2)
     e1 = _tick("attn_bwd_dkdv")
     N.call("rp_attn_bwd_dkdv", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
            float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
     _tock(e1)
-    if not _FUSED_DELTA:
-        e2 = _tick("attn_bwd_dq")
-        N.call("rp_attn_bwd_dq", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
-               float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
-        _tock(e2)
     _tock(e0)
     return dqkv
 

@@ -1,7 +1,7 @@
 """A/B of attention kernel variants selected by per-launch environment switches, in ONE process (tuning
 aid, not product): the same inputs through variant A and variant B — keep bits compared bit for bit,
 outputs / gradients compared against each other, and each kernel timed with HIP events (interleaved
-repetitions).  usage: python scripts/attn_ab.py --a RP_ATTN_FWD32=0 --b RP_ATTN_FWD32=1 [--B 8 --T 2048
+repetitions).  usage: python scripts/attn_ab.py --a RP_ATTN_SPLIT=0 --b RP_ATTN_SPLIT=1 [--B 8 --T 2048
 --p 0.1 --ragged --reps 10]"""
 import argparse
 import os

@@ -126,7 +126,7 @@ int main() {
   BAD(rp_attn_bwd_dq_delta(RP_F32, P, nullptr, nullptr, P, F, F, (const uint8_t*)P, 2, 64, 8, 64, 0.125f, 0.f,
                            nullptr, P, nullptr), nullptr);
   BAD(rp_attn_bwd_delta(RP_BF16, nullptr, nullptr, P, F, 2, 64, 8, 64, 0.f, F, nullptr), nullptr);
-  if (rp_attn_dropmask_elems(2, 100, 8) != 2ll * 8 * 2 * 4 * 256) { ++g_fail; fprintf(stderr, "FAIL dm elems\n"); }
+  if (rp_attn_dropmask_elems(2, 100, 8) != 2ll * 8 * 2 * 4 * 128 || rp_attn_dropmask_elems(1, 129, 1) != 3ll * 4 * 256) { ++g_fail; fprintf(stderr, "FAIL dm elems\n"); }
   if (rp_mha_dropmask_elems(0, 100, 100, 8) != 0) { ++g_fail; fprintf(stderr, "FAIL dm elems 0\n"); }
   rp_mha_args ma;
   memset(&ma, 0, sizeof ma);

@@ -255,7 +255,7 @@ def test_attention_fwd_bwd(dev, dtype, T, p):
     ftol = 2e-5 if dtype == torch.float32 else 2e-2
     close(o, ref.detach(), atol=ftol, rtol=ftol, what="attn fwd")
     if p > 0:  # the stored keep bits are exactly the restated ones
-        KT, ldm = (T + 63) // 64, (T + 255) // 256 * 256
+        KT, ldm = (T + 63) // 64, (T + 127) // 128 * 128
         words = mask.view(B * H, KT, 4, ldm)[..., :T].to(torch.int64) & 0xFFFF  # [bh, tile, g, q]
         bits = (words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1       # [bh, tile, g, q, kt*4+r]
         bits = bits.view(B * H, KT, 4, T, 4, 4)                                  # [bh, tile, g, q, kt, r]
@@ -349,7 +349,7 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled, p=0.1):
     # hi + lo carries the output to ~2^-17
     close(o.double() + olo.double(), ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd hi+lo")
     if p > 0:
-        KT, ldm = (T + 63) // 64, (T + 255) // 256 * 256
+        KT, ldm = (T + 63) // 64, (T + 127) // 128 * 128
         words = mask.view(B * H, KT, 4, ldm)[..., :T].to(torch.int64) & 0xFFFF
         bits = ((words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1).view(B * H, KT, 4, T, 4, 4)
         got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, T, KT * 64)[:, :, :T].bool()
@@ -366,18 +366,6 @@ def test_attention_128_blocks_ragged_dropout(dev, q_prescaled, p=0.1):
     dv1, rv1 = dqkv[rows, 2 * H * 64:].double().cpu(), gref[rows, 2 * H * 64:].cpu()
     assert ((dv1 - rv1).abs().max() / rv1.abs().max()).item() < 1e-2
     assert dqkv[rows, H * 64:2 * H * 64].abs().max().item() < 1e-2
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("switch", ["RP_ATTN_FWD32", "RP_ATTN_FWD_PP", "RP_ATTN_DQ32"])
-def test_attention_32x32_options(dev, monkeypatch, switch):
-    """The opt-in 32x32x16 kernels (measured slower than the 16x16x32 defaults at the bench shape,
-    DESIGN.md §8 round 4, kept as options): 4-wave forward, 8-wave ping-pong forward, dQ.  Same checks
-    as test_attention_128_blocks_ragged_dropout (ragged down to one valid key, dropout keep bits bit for
-    bit against the restatement — the 32x32 forwards run the same per-(query, lane group) streams — fwd
-    and every gradient vs fp64)."""
-    monkeypatch.setenv(switch, "1")
-    test_attention_128_blocks_ragged_dropout(dev, True)
 
 
 @pytest.mark.gpu
@@ -411,38 +399,11 @@ def test_attention_split3_short_ranges(dev, monkeypatch, T):
         monkeypatch.setenv("RP_ATTN_SPLIT", flag)
         res[flag] = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed)
     (o3, l3, m3), (o0, l0, m0) = res["3"], res["0"]
-    KT, ldm = (T + 63) // 64, (T + 255) // 256 * 256
+    KT, ldm = (T + 63) // 64, (T + 127) // 128 * 128
     valid = lambda m: m.view(B * H, KT, 4, ldm)[..., :T]  # noqa: E731 (rows past T are never written)
     assert torch.equal(valid(m3), valid(m0))
     close(o3, o0.double(), atol=1e-2, rtol=1e-2, what=f"split3 vs unsplit T={T}")
     assert (l3 - l0).abs().max().item() < 5e-3
-
-
-@pytest.mark.gpu
-def test_attention_kv32_option(dev, monkeypatch):
-    """RP_ATTN_KV32=1 (the 32x32x16 dK/dV kernel): ragged lengths down to one valid key, dropout, the
-    128-key-block path; dQ bitwise the default path's (same dQ kernel), dK / dV within bf16 rounding of
-    it and against fp64 at the tolerances above."""
-    B, H, T, p = 8, 8, 1030, 0.1
-    qkv0 = rnd(B * T, 3 * H * 64, dev=dev, seed=T).to(torch.bfloat16)
-    qkv, eff = prescale_q(qkv0, H, 0.125)
-    lens = torch.tensor([T, T - 1, 1000, 777, 640, 129, 2, 1], device=dev)
-    kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
-    olo = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
-    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 99, q_prescaled=True, out_lo=olo)
-    do = rnd(B * T, H * 64, dev=dev, seed=T + 1).to(torch.bfloat16)
-    outs = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("RP_ATTN_KV32", v)
-        outs[v] = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True, out_lo=olo)
-    torch.cuda.synchronize()
-    D = H * 64
-    assert torch.equal(outs["0"][:, :D], outs["1"][:, :D])
-    close_per_seq(outs["1"][:, D:], outs["0"][:, D:], B, atol=1e-2, rtol=1e-2, what="kv32 vs kv16 dk/dv")
-    ref_in = eff.requires_grad_(True)
-    ref = attn_ref(ref_in, kv, B, T, H, p, 99)
-    gref = torch.autograd.grad(ref, ref_in, do.double())[0]
-    close_per_seq(outs["1"][:, D:], gref[:, D:], B, atol=6e-2, rtol=6e-2, what="kv32 dk/dv vs fp64")
 
 
 @pytest.mark.gpu
@@ -483,7 +444,7 @@ def test_mha_cross_dropout_prescaled(dev, monkeypatch, split):
     lens = torch.tensor([Tk, 999, 900, 513, 500, 128, 64, 700], device=dev)
     kv = (torch.arange(Tk, device=dev)[None] < lens[:, None]).to(torch.uint8)
     o, lse, mask = K.mha_fwd(qp, k, v, kv, B, Tq, Tk, H, 0.125, dropout_p=p, seed=seed, q_prescaled=True)
-    KT, ldm = (Tk + 63) // 64, (Tq + 255) // 256 * 256
+    KT, ldm = (Tk + 63) // 64, (Tq + 127) // 128 * 128
     words = mask.view(B * H, KT, 4, ldm)[..., :Tq].to(torch.int64) & 0xFFFF
     bits = ((words.unsqueeze(-1) >> torch.arange(16, device=dev)) & 1).view(B * H, KT, 4, Tq, 4, 4)
     got = bits.permute(0, 3, 1, 4, 2, 5).reshape(B * H, Tq, KT * 64)[:, :, :Tk].bool()
@@ -753,24 +714,35 @@ def test_gemm_64_row_tiles_bitwise(dev, monkeypatch, M):
         assert torch.equal(a, c) and torch.equal(c, d) and torch.equal(a, e)
 
 
-def test_attention_metric_shape_bf16_dropout(dev):
-    """Attention at the bench shape (B = 8, T = 2048, H = 8, dk = 64) with dropout 0.1 and ragged key
-    padding: forward output and all three gradients against an fp64 torch restatement (same bf16
-    inputs, the restated keep bits) on a sample of 2 (batch, head) pairs."""
-    B, T, H = 8, 2048, 8
-    qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=21).to(torch.bfloat16)
-    lens = torch.tensor([T, T - 1, 1900, 1537, T, 1024, 2047, 64], device=dev)
+@pytest.mark.parametrize("B,T,qpre", [(8, 2048, False), (8, 2048, True), (1, 4096, True)])
+def test_attention_metric_shape_bf16_dropout(dev, B, T, qpre):
+    """Attention at the bench shape (B = 8, T = 2048, H = 8, dk = 64) and at config 4's (B = 1, T = 4096)
+    with dropout 0.1 and ragged key padding: forward output and all three gradients against an fp64
+    torch restatement (same bf16 inputs, the restated keep bits) on a sample of (batch, head) pairs.
+    With the producer's Q prescale (qpre, what the model runs) the shipping LDS-DMA kernels run: at the
+    bench shape the fused-delta dQ kernel and the 128-key dK/dV kernel, at config 4 the delta pass and
+    the two-role launch (attn_bwd_roles_kernel) — asserted, so this is its fp64 check at T = 4096."""
+    H = 8
+    qkv0 = rnd(B * T, 3 * H * 64, dev=dev, seed=21).to(torch.bfloat16)
+    if qpre:
+        qkv, eff = prescale_q(qkv0, H, 0.125)
+    else:
+        qkv, eff = qkv0, qkv0.double()
+    lens = torch.tensor([T, T - 1, 1900, 1537, T, 1024, 2047, 64][:B] if B > 1 else [T - 301], device=dev)
     kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
     p, seed = 0.1, 777
-    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed)
+    olo = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=qpre, out_lo=olo)
     do = rnd(B * T, H * 64, dev=dev, seed=22).to(torch.bfloat16)
-    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask)
+    if B == 1:
+        assert K.attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=qpre)
+    dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=qpre, out_lo=olo)
     keep_all = attn_keep(B, H, T, p, seed, dev)                       # [B, H, T, T]
-    q, k, v = qkv.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)        # [B, H, T, 64]
+    q, k, v = eff.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)        # [B, H, T, 64]
     dq, dk, dv = dqkv.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
     og = o.view(B, T, H, 64).permute(0, 2, 1, 3)
     dog = do.view(B, T, H, 64).permute(0, 2, 1, 3)
-    for (bb, hh) in [(3, 5), (6, 0)]:
+    for (bb, hh) in ([(3, 5), (6, 0)] if B > 1 else [(0, 2), (0, 7)]):
         qd, kd, vd = (t[bb, hh].double().requires_grad_(True) for t in (q, k, v))
         s = (qd @ kd.T) * 0.125
         s = s.masked_fill(~kv[bb].bool()[None, :], float("-inf"))
@@ -784,33 +756,6 @@ def test_attention_metric_shape_bf16_dropout(dev):
         close(dk[bb, hh][valid], gk[valid], atol=6e-2, rtol=6e-2, what=f"dk b{bb} h{hh}")
         close(dv[bb, hh][valid], gv[valid], atol=6e-2, rtol=6e-2, what=f"dv b{bb} h{hh}")
         assert torch.count_nonzero(dk[bb, hh][~valid]) == 0 and torch.count_nonzero(dv[bb, hh][~valid]) == 0
-
-
-@pytest.mark.parametrize("B,T", [(8, 2048), (1, 4096)])
-def test_attention_bwd_overlap_matches_sequential(dev, monkeypatch, B, T):
-    """The overlapped backward (delta pass, then the dQ kernel on a side stream beside dK/dV; the dQ
-    kernel reads the precomputed row constants, 128-query and split workgroups) against the sequential
-    one (dQ with the fused delta, then dK/dV) at the bench shape and config 4's, Q prescaled, dropout
-    0.1, ragged keys: the gradients differ only through the rounding of delta (its two producers sum in
-    different orders), and the overlapped form repeats bitwise (no race between the two streams)."""
-    H, p = 8, 0.1
-    qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=31).to(torch.bfloat16)
-    qkv[:, :H * 64] = (qkv[:, :H * 64].float() * (0.125 * K.LOG2E)).to(torch.bfloat16)
-    lens = torch.tensor([T, T - 1, 1900, 1537, T, 1024, 2047, 64][:B], device=dev)
-    kv = (torch.arange(T, device=dev)[None] < lens[:, None]).to(torch.uint8)
-    olo = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
-    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 91, q_prescaled=True, out_lo=olo)
-    do = rnd(B * T, H * 64, dev=dev, seed=32).to(torch.bfloat16)
-    outs = {}
-    for mode in (False, True, True):
-        monkeypatch.setattr(K, "_BWD_OVERLAP", mode)
-        r = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True, out_lo=olo)
-        torch.cuda.synchronize()
-        if mode in outs:
-            assert torch.equal(r, outs[mode]), "overlapped backward not repeatable"
-        outs[mode] = r
-    assert torch.isfinite(outs[True]).all()
-    close(outs[True].float(), outs[False].double(), atol=2e-2, rtol=2e-2, what="overlapped vs sequential dqkv")
 
 
 @pytest.mark.parametrize("B,T,p", [(1, 4096, 0.1), (1, 4096, 0.0), (2, 2048, 0.1), (1, 4000, 0.1)])
