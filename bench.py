@@ -29,6 +29,7 @@ the reference's precision, as a graph replay) and `fresh_batch` (the trainer-sha
 pinned ragged batch per step through the device collate and CapturedTrainStep.load()).
 """
 import argparse
+import datetime
 import json
 import math
 import os
@@ -227,10 +228,13 @@ def main():
     if dp:
         torch.cuda.set_device(gpu)
         backend = os.environ.get("RP_DIST_BACKEND", "nccl")
+        # bounded: a rank that never arrives, or a collective that never completes, ends the run with an
+        # error and a stack after 5 minutes instead of the default 30
+        tmo = datetime.timedelta(seconds=300)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     dev = torch.device("cuda", gpu if dp else 0)
 
     from repurpose_amd import kernels as K

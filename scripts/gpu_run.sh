@@ -19,7 +19,7 @@ for s in $STEPS; do
     kernels) step kernels 400 $PYT tests/test_kernels_gpu.py ;;
     model)   step model 400 $PYT tests/test_model_gpu.py ;;
     infer)   step infer 300 $PYT tests/test_infer_gpu.py ;;
-    gputests) step gputests 600 $PYT -m gpu tests ;;
+    gputests) step gputests 1000 $PYT -m gpu tests ;;
     smoke)   step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 400 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     benchfull) step benchfull 500 python -u bench.py ;;

@@ -45,7 +45,7 @@ def _worker(rank, world, port, q, dtype="fp32"):
         from repurpose_amd.MMCTransformer import MMCTransformer
         from repurpose_amd.optim import FusedAdam
 
-        s = MultiGPUStrategy(strategy="auto", backend="gloo", timeout=120)
+        s = MultiGPUStrategy(strategy="auto", backend="gloo", timeout=60)
         assert s.strategy == "ddp" and s.world_size == world and s.rank == rank, (s.strategy, s.world_size)
         assert s.setup() is True
         dev = s.device

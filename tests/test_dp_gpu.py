@@ -9,8 +9,16 @@
   tile ``[0, trainable_numel)`` exactly once, in reverse layout order;
 * the captured DP step (``CapturedTrainStep(capture_collectives=True)``: RCCL all-reduces captured into
   the HIP graph, tile cut active, backward writing the gradients) on a one-rank RCCL group gives bitwise
-  the parameters and Adam moments of eager DP steps.
+  the parameters and Adam moments of eager DP steps;
+* the DP update pinned to the oracle: two ranks through ``MultiGPUStrategy.setup`` / ``wrap_model`` /
+  the HIP backward / ``FusedAdam`` against the CPU oracle's gradients of each rank's batch, averaged,
+  then ``torch.optim.Adam`` (``/root/reference/main.py:331-369``, ``utils/distributed.py:415-428``).
+
+Every process group here is created with a bounded timeout (60 s), so a stuck rendezvous or collective
+raises with a stack instead of stalling the suite, and the parent notices a worker that died without
+answering within two seconds (``_wait``).
 """
+import datetime
 import json
 import os
 import socket
@@ -37,24 +45,36 @@ def _heartbeat(request, msg):
 
 
 def _wait(q, p, request, name, limit, trace=None):
-    """The worker's (status, result), polling every 20 s with a progress line; ("timeout", log tail)
-    when it has not answered within ``limit`` seconds or died without answering."""
+    """The worker's (status, result): polled every 2 s, a progress line every 20 s; ("timeout", log tail)
+    when it has not answered within ``limit`` seconds, ("died", exit code + log tail) as soon as it
+    has exited without answering (a crashed worker must not look like a hang)."""
     import queue
     import time
-    t0 = time.time()
+    t0 = last_beat = time.time()
+
+    def log_tail():
+        if trace and os.path.exists(trace):
+            with open(trace) as f:
+                return f.read()[-6000:]
+        return ""
+
     try:
         while True:
             try:
-                return q.get(timeout=20)
+                return q.get(timeout=2)
             except queue.Empty:
-                log = ""
-                if trace and os.path.exists(trace):
-                    with open(trace) as f:
-                        log = f.read()
-                if time.time() - t0 > limit or not p.is_alive():
-                    return "timeout", log[-6000:] or f"{name}: no answer after {time.time() - t0:.0f}s"
-                last = log.strip().splitlines()[-1] if log.strip() else "running"
-                _heartbeat(request, f"{name} {time.time() - t0:.0f}s: {last}")
+                now = time.time()
+                if not p.is_alive():
+                    try:  # an answer put just before exiting
+                        return q.get(timeout=1)
+                    except queue.Empty:
+                        return "died", f"{name}: exited with code {p.exitcode} without answering\n{log_tail()}"
+                if now - t0 > limit:
+                    return "timeout", log_tail() or f"{name}: no answer after {now - t0:.0f}s"
+                if now - last_beat >= 20:
+                    last_beat = now
+                    tail = log_tail().strip().splitlines()
+                    _heartbeat(request, f"{name} {now - t0:.0f}s: {tail[-1] if tail else 'running'}")
     finally:
         p.join(timeout=30)
         if p.is_alive():
@@ -111,7 +131,7 @@ def _tiling_worker(port, q, cases):
         from repurpose_amd.distributed import GradAllReducer
         from repurpose_amd.MMCTransformer import MMCTransformer
         from tests.test_model_gpu import TRI, make_batch, to_dev
-        dist.init_process_group("gloo", rank=0, world_size=1)
+        dist.init_process_group("gloo", rank=0, world_size=1, timeout=datetime.timedelta(seconds=60))
         dev = torch.device("cuda", 0)
         b = to_dev(make_batch(TRI, 2, 128, [128, 90], seed=3), dev)
         out = []
@@ -192,7 +212,7 @@ def _captured_worker(q, trace):
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         mark("init_process_group")
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, timeout=datetime.timedelta(seconds=60))
         mark("process group up")
         cfg = dict(TRI, self_num_layers=16)
         batches = [{k: v for k, v in to_dev(make_batch(cfg, 2, 128, [128, 100], seed=40 + i), dev).items()
@@ -226,6 +246,11 @@ def _captured_worker(q, trace):
         ok = (run._graph is not None, len(rg.launched) > 0,
               torch.equal(mg.flat_params()[:n], me.flat_params()[:n]),
               torch.equal(og._m, oe._m), torch.equal(og._v, oe._v))
+        # the graph (and the RCCL plan resources it holds) goes before the communicator it was
+        # captured on is destroyed
+        del run
+        torch.cuda.synchronize()
+        mark("graph released")
         q.put(("ok", ok))
     except Exception:
         import traceback
@@ -251,3 +276,150 @@ def test_captured_rccl_dp_step_equals_eager_dp(dev, tmp_path, request):
     assert captured, "the DP step was not captured"
     assert hooked, "the captured backward issued no all-reduce"
     assert params and m1 and m2, res
+
+
+# ------------------------------------------------------------------- DP update pinned to the oracle
+DP_CFG = dict(vis_dim=512, aud_dim=2048, text_dim=384, d_model=512, self_num_layers=2, text_num_layers=3,
+              cross_num_layers=3, num_heads=8)
+DP_STEPS, DP_B, DP_T = 2, 2, 128
+DP_LR, DP_WD = 1e-3, 1e-4
+
+
+def _dp_batch(rank, step):
+    """Rank ``rank``'s batch of step ``step``: B = 2 ragged sequences (its own data, as a
+    DistributedSampler hands each rank)."""
+    from tests.test_model_gpu import make_batch
+    lens = [[DP_T, 77], [101, DP_T]][rank]
+    b = make_batch(DP_CFG, DP_B, DP_T, lens, seed=1000 + 10 * rank + step)
+    return {k: v for k, v in b.items() if torch.is_tensor(v)}
+
+
+def _dp_oracle_worker(rank, world, port, q, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        from repurpose_amd.distributed import DistributedModel, MultiGPUStrategy
+        from repurpose_amd.MMCTransformer import MMCTransformer
+        from repurpose_amd.optim import FusedAdam
+        s = MultiGPUStrategy(strategy="auto", backend="gloo", timeout=60)
+        assert s.strategy == "ddp" and s.world_size == world and s.setup() is True
+        torch.manual_seed(100 + rank)  # a different init per rank: wrap_model broadcasts rank 0's
+        m = MMCTransformer(**DP_CFG, compute_dtype="fp32")
+        m.DROPOUT = 0.0  # dropout off: the oracle runs in eval mode
+        w = s.wrap_model(m)
+        assert isinstance(w, DistributedModel)
+        opt = FusedAdam(w.parameters(), lr=DP_LR, weight_decay=DP_WD)
+        w.train()
+        rec = {}
+        for step in range(DP_STEPS):
+            b = {k: v.to(s.device) for k, v in _dp_batch(rank, step).items()}
+            opt.zero_grad()
+            out = w(b)
+            loss = w.module.losses(*out)["cls_loss"] / DP_B  # main.py:331: cls_loss / batch_size
+            loss.backward()  # DDP: the HIP backward's hooks all-reduce the flat gradient (AVG)
+            opt.step()
+            torch.cuda.synchronize()
+            rec[f"grad{step}"] = m.flat_grads()[:m.trainable_numel()].cpu().clone()
+            rec[f"params{step}"] = m.flat_params().cpu().clone()
+        torch.save(rec, os.path.join(outdir, f"rank{rank}.pt"))
+        s.barrier()
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_update_matches_oracle_adam(dev, tmp_path):
+    """The data-parallel update against the reference computation done by the CPU oracle: two gloo ranks
+    (sharing the box's GPU) each run their own ragged batch through ``MultiGPUStrategy.setup`` ->
+    ``wrap_model`` (rank 0's parameters broadcast) -> the HIP fp32 forward / backward with the bucketed
+    all-reduce -> ``FusedAdam``, two steps; the oracle (``oracle/mmct_oracle.py``, rank 0's init, eval
+    mode = dropout off) computes each rank's ``cls_loss / B`` gradient, averages the two (DDP) and applies
+    ``torch.optim.Adam(lr=1e-3, weight_decay=1e-4)``.  Checks: the averaged gradient per tensor within
+    the fp32 gradient gate of ``test_model_gpu.py::test_backward_fp32_parity`` (2e-3 of the tensor's
+    largest element); the parameters after each step within 1e-5 of each tensor's largest parameter,
+    except where the oracle's gradient is within that gate of zero (Adam's first steps move every
+    element by ~lr whatever its gradient's size, so a gradient inside the fp32 noise can take either
+    sign: there at most 2 lr per step); reg_head untouched; both ranks bitwise equal."""
+    from oracle.mmct_oracle import MMCTransformer as Oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_dp_oracle_worker, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = []
+        for _ in procs:
+            try:
+                res.append(q.get(timeout=240))
+            except Exception:
+                res.append((-1, "no answer within 240 s: " + ", ".join(f"rank {i} exit {p.exitcode}"
+                                                                       for i, p in enumerate(procs))))
+                break
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    bad = [f"rank {rank}: {msg}" for rank, msg in sorted(res) if msg != "ok"]
+    assert not bad, "\n".join(bad)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), f"ranks differ in {k}"
+
+    torch.manual_seed(100)
+    ref = Oracle(**DP_CFG).eval()
+    opt = torch.optim.Adam(ref.parameters(), lr=DP_LR, weight_decay=DP_WD)
+    names = [n for n, _ in ref.named_parameters()]
+    params = dict(ref.named_parameters())
+    sizes = [p.numel() for p in ref.parameters()]
+    from repurpose_amd.MMCTransformer import MMCTransformer
+    torch.manual_seed(100)
+    layout = MMCTransformer(**DP_CFG, compute_dtype="fp32")
+    base = layout.flat_params().data_ptr()
+    offs = [(p.data_ptr() - base) // 4 for p in layout.parameters()]
+    assert [n for n, _ in layout.named_parameters()] == names
+    init = {n: p.detach().clone() for n, p in ref.named_parameters()}
+    worst_g, worst_p, flips = 0.0, 0.0, 0
+    for step in range(DP_STEPS):
+        acc = None
+        for rank in range(2):
+            ref.zero_grad(set_to_none=True)
+            b = _dp_batch(rank, step)
+            (ref.losses(*ref(b))["cls_loss"] / DP_B).backward()
+            g = {n: (p.grad.detach().clone() if p.grad is not None else None) for n, p in ref.named_parameters()}
+            acc = g if acc is None else {n: (None if v is None else v + g[n]) for n, v in acc.items()}
+        for n, p in ref.named_parameters():
+            p.grad = None if acc[n] is None else acc[n] / 2  # DDP: the mean over ranks
+        geff = {n: (None if p.grad is None else p.grad + DP_WD * p.detach()) for n, p in ref.named_parameters()}
+        opt.step()
+        g_hip, p_hip = r0[f"grad{step}"], r0[f"params{step}"]
+        for n, off, size in zip(names, offs, sizes):
+            p_ref = params[n].detach()
+            got_p = p_hip[off:off + size].view_as(p_ref)
+            if n.startswith("reg_head."):
+                assert torch.equal(got_p, init[n]), f"{n} moved (no loss reaches it: torch skips grad None)"
+                continue
+            gr = params[n].grad
+            got_g = g_hip[off:off + size].view_as(gr)
+            gscale = gr.abs().max().item() + 1e-12
+            rel_g = (got_g - gr).abs().max().item() / gscale
+            worst_g = max(worst_g, rel_g)
+            assert rel_g < 2e-3, f"step {step} {n}: averaged gradient rel err {rel_g:.2e}"
+            pscale = p_ref.abs().max().item() + 1e-12
+            d = (got_p - p_ref).abs()
+            noise = geff[n].abs() <= 2e-3 * geff[n].abs().max()
+            flips += int(((d > 1e-5 * pscale) & noise).sum())
+            rel_p = (d[~noise].max().item() if (~noise).any() else 0.0) / pscale
+            worst_p = max(worst_p, rel_p)
+            assert rel_p < 1e-5, f"step {step} {n}: parameters after Adam rel err {rel_p:.2e}"
+            assert (d[noise] <= 2 * DP_LR * (step + 1) * 1.001).all(), f"step {step} {n}: noise-level move"
+    print(f"worst averaged-gradient rel err {worst_g:.2e}, worst parameter rel err {worst_p:.2e}, "
+          f"noise-level sign flips {flips}")
