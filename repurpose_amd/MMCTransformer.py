@@ -625,17 +625,19 @@ class _Schedule:
         deferred = [] if (dt == torch.bfloat16 and side is None and M % 64 == 0
                           and os.environ.get("RP_WGRAD_GROUPED", "1") != "0") else None
         held = []  # layer prefixes whose gradients wait for their group launch
-        # one launch for the whole encoder on one GPU.  With gradient hooks (DP all-reduce) the first
-        # launch is cut so its exchange overlaps the rest of the backward: by default where its 256x256
-        # tiles first fill a whole number of rounds of the CUs (768 tiles at the metric shape: layers
-        # 15..11 plus layer 10's linear2 = 256 tiles = one round, the rest 512 = two; eight-layer
-        # groups were 384 + 384, a half-idle round each: 0.25 ms per step more); RP_WGRAD_GROUP_LAYERS=n
-        # cuts it every n whole layers instead
+        # one launch for the whole encoder on one GPU.  With gradient hooks (DP all-reduce) the launch is
+        # cut so that each part's exchange overlaps the backward after it: every time the tiles gathered
+        # since the last cut fill a whole round of the CUs (768 tiles at the metric shape: layers 15..11
+        # plus layer 10's linear2 = 256 tiles = one round, then layer 10's rest .. layer 5's linear1 =
+        # 256, then the last 256 — three launches; a 256-tile launch runs at the per-tile rate of the
+        # 768-tile one, 455 vs 450 us per 256 tiles, so the cuts cost no GEMM time; eight-layer groups
+        # were 384 + 384, a half-idle round each: 0.25 ms per step more).  Only the last part's exchange
+        # is exposed after the backward.  RP_WGRAD_GROUP_LAYERS=n cuts every n whole layers instead
         env_layers = os.environ.get("RP_WGRAD_GROUP_LAYERS")
         per_launch = 4 * int(env_layers or "16")
         tile_cut = deferred is not None and bool(m._grad_ready_hooks) and env_layers is None
         ncu = torch.cuda.get_device_properties(dlogits.device).multi_processor_count if tile_cut else 0
-        cut = {"tiles": 0, "done": False}
+        cut = {"tiles": 0}  # 256 x 256 tiles gathered since the last cut
 
         # LayerNorm gamma / beta partials: reduced together by one rp_colsum_batched launch per flush
         # (before the gradients they finish are announced, and at the end) instead of one per LayerNorm
@@ -647,8 +649,9 @@ class _Schedule:
                 cs.clear()
 
         def flush_group():
-            K.linear_wgrad_grouped(deferred, accumulate=acc)
-            deferred.clear()
+            if deferred:
+                K.linear_wgrad_grouped(deferred, accumulate=acc)
+                deferred.clear()
             flush_cs()
             for pf in held:
                 m._grads_ready(pf)
@@ -657,10 +660,10 @@ class _Schedule:
         def wgrad(dy, x, wname, bname):
             if deferred is not None and wname.startswith("multimodal_encoder."):
                 deferred.append((dy, x, G(wname), G(bname)))
-                if tile_cut and not cut["done"]:
+                if tile_cut:
                     cut["tiles"] += -(-dy.shape[1] // 256) * -(-x.shape[1] // 256)
                     if cut["tiles"] >= ncu and (cut["tiles"] % ncu == 0 or cut["tiles"] >= 2 * ncu):
-                        cut["done"] = True
+                        cut["tiles"] = 0
                         flush_group()  # announces the layers already complete (held), not this one
                 return
             if side is None:
@@ -765,7 +768,9 @@ class _Schedule:
                                          lp_seed=0 if last else self.seed(103 + 4 * (l - 1)), seed_base=self.sb,
                                          dgamma=G(pre + "norm1.weight"), dbeta=G(pre + "norm1.bias"), ws=ws, defer=cs)
             ready([pre])
-        if deferred:
+        if deferred is not None and (deferred or held):
+            # the rest of the grouped launch, and the layers it completes (a tile cut can fall on the
+            # last layer's last GEMM: then nothing is left to launch, but layer 0 is still to announce)
             flush_group()
         # input LayerNorm (+PE, no grad) and input projection (weight/bias grads only)
         _, dproj = K.layernorm_bwd(dx, S["proj"], S["mu0"], S["rs0"], self.P("input_norm.weight"), want_f32=False,

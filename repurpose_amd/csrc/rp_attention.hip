@@ -1928,10 +1928,13 @@ __device__ __forceinline__ void attn_bwd_q_dma_body(const MhaDev& a, const int b
   Rows64 rk, rv;
   rk.init(Kg, ldk, Tk, w, lane);
   rv.init(Vg, ldv, Tk, w, lane);
-  // keep bits (wave 1): lane (g, c) reads words [tile][g][this block's 128 queries], column chunk c
+  // keep bits (wave 1): lane (g, c) reads words [tile][g][this block's 128 queries], column chunk
+  // c ^ 2g into LDS chunk c: row g's 32-byte chunks are XOR-swizzled by g, so the tile loop's 16-bit
+  // reads (lanes of groups g and g ^ 1 share an LDS lane group; rows are 256 B = 0 mod 32 banks apart)
+  // hit different bank octets — conflict-free (the unswizzled rows were 2-way conflicted at p > 0).
+  // ldm is a multiple of 128, so the block's 128 columns are always inside the row.
   const rp_srd srd_m = make_srd(mrow);
-  int64_t mcol = (int64_t)qb * QB + (lane & 15) * 8;
-  mcol = mcol < ldm - 8 ? mcol : ldm - 8;
+  const int64_t mcol = (int64_t)qb * QB + ((lane & 15) ^ (2 * (lane >> 4))) * 8;
   const uint32_t vo_m = (uint32_t)((((int64_t)(lane >> 4)) * ldm + mcol) * 2);
   const bool xfast = (int64_t)KT * 4 * ldm * 2 < ((int64_t)1 << 31) && rk.fast && rv.fast;
   const uint32_t slot_lds[3] = {lds_addr(ring0) + (uint32_t)hoff, lds_addr(ring1) + (uint32_t)hoff,
@@ -1978,8 +1981,8 @@ __device__ __forceinline__ void attn_bwd_q_dma_body(const MhaDev& a, const int b
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
       kwd[qt] = 0u;
-      if constexpr (DROP)
-        kwd[qt] = reinterpret_cast<const uint16_t*>(Kl + 2 * TILE)[g * QB + w * 16 * QT + qt * 16 + i];
+      if constexpr (DROP)  // this lane's query word, in its 32-byte chunk (w * QT + qt) ^ g of row g
+        kwd[qt] = reinterpret_cast<const uint16_t*>(Kl + 2 * TILE)[g * QB + (((w * QT + qt) ^ g) << 4) + i];
     }
     const bool full = kfull[it] != 0;
     f32x4 s[4][QT], dp[4][QT];

@@ -713,6 +713,7 @@ struct WgItem {
 };
 struct WgGroup {
   int n, accumulate, tiles_total;
+  int order;  // tile order (A/B): 0 XCD chunks, m-major; 1 XCD chunks, n-major; 2 no XCD remap
   int64_t K;
   int start[WG_MAX + 1];
   WgItem it[WG_MAX];
@@ -1336,14 +1337,14 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
 // the grouped launch is bound by; one workgroup of 8 waves per CU
 __global__ __launch_bounds__(NT8, 1) void wgrad8_grouped_kernel(const WgGroup g) {
   __shared__ __attribute__((aligned(16))) char lds[G8<256, 64, 2>::LDS];
-  const int t = rp_xcd_remap(blockIdx.x, g.tiles_total);
+  const int t = g.order == 2 ? (int)blockIdx.x : rp_xcd_remap(blockIdx.x, g.tiles_total);
   int k = 0;
   while (k + 1 < g.n && t >= g.start[k + 1]) ++k;
   const WgItem w = g.it[k];
   const int local = t - g.start[k];
-  const int tiles_n = (w.N + 255) / 256;
-  const int64_t m0 = (int64_t)(local / tiles_n) * 256;
-  const int64_t n0 = (int64_t)(local % tiles_n) * 256;
+  const int tiles_n = (w.N + 255) / 256, tiles_m = (w.M + 255) / 256;
+  const int64_t m0 = (int64_t)(g.order == 1 ? local % tiles_m : local / tiles_n) * 256;
+  const int64_t n0 = (int64_t)(g.order == 1 ? local / tiles_m : local % tiles_n) * 256;
   EpiDev ep{};
   ep.gate_scale = 1.f;
   ep.accumulate = g.accumulate;
@@ -2046,6 +2047,8 @@ extern "C" int rp_gemm_wgrad_grouped(int64_t K, const rp_wgrad_item* items, int 
   g.n = n_items;
   g.accumulate = accumulate;
   g.K = K;
+  const char* oe = getenv("RP_WGRAD_ORDER");  // A/B (read per call)
+  g.order = oe ? atoi(oe) : 0;
   int64_t tiles = 0;
   const bool big = rp_wgrad8_enabled();  // 256 x 256 tiles (wgrad8_grouped_kernel)
   for (int i = 0; i < n_items; ++i) {

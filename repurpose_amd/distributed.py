@@ -249,6 +249,7 @@ class DataParallelModel(nn.Module):
         self.module = module.to(self.device_ids[0])
         self._replicas = []  # replicas 1.. (plain list: not sub-modules, so state_dict / parameters are .module's)
         self._queued = False
+        self._done_events = []
 
     def _replica(self, i):
         import copy
@@ -261,6 +262,11 @@ class DataParallelModel(nn.Module):
         return self._replicas[i - 1]
 
     def _on_replica_done(self):
+        # the replica's backward was enqueued on its device's current stream (this hook runs at its
+        # end, on the engine's thread for that device): an event there orders the cross-device read
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self._done_events.append(ev)
         if not self._queued:  # once per backward: after the engine has run every replica's backward
             self._queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._reduce)
@@ -269,8 +275,13 @@ class DataParallelModel(nn.Module):
         self._queued = False
         g0 = self.module.flat_grads()
         n = self.module.trainable_numel()
-        for r in self._active:
-            g0[:n].add_(r.flat_grads()[:n].to(g0.device))
+        s0 = torch.cuda.current_stream(g0.device)
+        for ev in self._done_events:  # device 0 reads the replicas' gradients only once they are written
+            s0.wait_event(ev)
+        self._done_events = []
+        with torch.cuda.stream(s0):
+            for r in self._active:
+                g0[:n].add_(r.flat_grads()[:n].to(g0.device, non_blocking=True))
 
     def forward(self, batch):
         pieces = _split_batch(batch, len(self.device_ids))

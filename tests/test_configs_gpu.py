@@ -106,8 +106,10 @@ def test_config2_bf16_L16_T1024_B8(dev):
 @pytest.mark.timeout(600)
 def test_config4_bf16_L16_T4096_B1(dev):
     """Config 4 (T = 4096, B = 1) in bf16 through the kernels only that shape selects — the three-part
-    split attention forward, the two-part split dQ / dK/dV, 64 x 128 GEMM tiles — checked as config 2:
-    logits against the fp32 oracle, one step's gradients against the fp32 GPU gradients."""
+    split attention forward, the delta pass + two-role backward launch (attn_bwd_roles_kernel: dK/dV and
+    dQ workgroups side by side), 64- and 32-row GEMM tiles — checked as config 2: logits against the fp32
+    oracle, one step's gradients (dropout off) against the fp32 GPU gradients.  The roles kernel with
+    dropout is checked against fp64 in test_config4_bf16_attention_T4096_dropout."""
     bf16_whole_batch(dev, 1, 4096, [4000], seed=45, tag="config 4", sub=1)
 
 
@@ -164,11 +166,12 @@ def attn_ref64(qkv, kv, B, T, H, p, seed, dev):
 
 @pytest.mark.timeout(300)
 def test_config4_bf16_attention_T4096_dropout(dev, monkeypatch):
-    """rp_attn fwd/bwd at T = 4096, B = 1 (8 heads: 256 blocks of 128 rows -> the split 8-wave
-    workgroups, SPL = 2), dropout 0.1 with the stored keep bits, the Q columns prescaled as the model's
-    QKV GEMM writes them; fwd and gradients vs fp64, and against the unsplit 4-wave kernels
-    (RP_ATTN_SPLIT=0): keep bits bit for bit (the second key half's streams are advanced by the
-    skip-ahead multiplier), outputs and gradients within bf16 rounding."""
+    """rp_attn fwd/bwd at T = 4096, B = 1 (8 heads: 256 blocks of 128 rows -> the three-part split
+    forward and the two-role backward launch, asserted), dropout 0.1 with the stored keep bits, the Q
+    columns prescaled as the model's QKV GEMM writes them; fwd and every gradient (dQ, dK, dV of all 8
+    heads) vs fp64, and against the unsplit 4-wave kernels (RP_ATTN_SPLIT=0, which also turns the roles
+    form off): keep bits bit for bit (the later key parts' streams are advanced by the skip-ahead
+    multiplier), outputs and gradients within bf16 rounding."""
     from tests.test_kernels_gpu import close, close_per_seq, prescale_q, rnd
     B, H, T, p, seed = 1, 8, 4096, 0.1, 7
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=3).to(torch.bfloat16)
@@ -181,12 +184,14 @@ def test_config4_bf16_attention_T4096_dropout(dev, monkeypatch):
     ref = attn_ref64(ref_in, kv, B, T, H, p, seed, dev)
     close(o, ref.detach(), atol=2e-2, rtol=2e-2, what="attn fwd T=4096")
     do = rnd(B * T, H * 64, dev=dev, seed=4).to(torch.bfloat16)
+    assert K.attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=True)
     dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True, out_lo=olo)
     gref = torch.autograd.grad(ref, ref_in, do.double())[0]
     for part, name in enumerate("qkv"):
         cols = slice(part * H * 64, (part + 1) * H * 64)
         close_per_seq(dqkv[:, cols], gref[:, cols], B, atol=6e-2, rtol=6e-2, what=f"attn d{name} T=4096")
     monkeypatch.setenv("RP_ATTN_SPLIT", "0")
+    assert not K.attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=True)
     o0, lse0, mask0 = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=True, out_lo=olo.clone())
     assert torch.equal(mask0, mask)
     close(o, o0.double(), atol=1e-2, rtol=1e-2, what="split vs unsplit fwd")
