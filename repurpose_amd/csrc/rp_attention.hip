@@ -2632,6 +2632,7 @@ static bool attn_roles(const MhaDev& a) {
   const int64_t gkv = (int64_t)((a.Tk + KV_KB - 1) / KV_KB) * a.B * a.H;
   const int64_t gq = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H;
   if (attn_small(gkv) || attn_small(gq)) return false;
+  if (e && e[0] == '2') return true;  // A/B: wherever legal (e.g. the metric shape's 2 x 1,024 blocks)
   return attn_split(gkv, (a.Tq + KV_QT - 1) / KV_QT) && attn_split(gq, (a.Tk + FW_KT - 1) / FW_KT);
 }
 
