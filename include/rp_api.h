@@ -399,13 +399,13 @@ int rp_attn_fwd(int dtype, const void* qkv, const uint8_t* key_valid, int B, int
  * delta = rowsum(dout * out) to delta_ws), then rp_attn_bwd_dkdv (dK, dV columns, one workgroup per
  * 128-key block, reading delta).  The phases are also exported separately (per-kernel timing);
  * rp_attn_bwd_delta + rp_attn_bwd_dq is the unfused equivalent of rp_attn_bwd_dq_delta.
- * Where each of the two grids alone would fill the CUs once but not twice (B*H*ceil(T/128) in
- * [256, 384) on 256 CUs, e.g. B = 1, T = 4096, H = 8; bf16 with RP_ATTN_Q_PRESCALED), rp_attn_bwd and
- * rp_mha_bwd with phases 7 instead run rp_attn_bwd_delta's pass and ONE launch whose workgroups take
- * either role (dK/dV blocks, then dQ blocks): same results up to the rounding of delta's sum.
- * (The bound is in compute units: [CUs, 1.5 CUs).)  rp_attn_bwd_uses_roles tells whether rp_attn_bwd
- * takes that form for a shape (1) or the two kernels (0), so a caller timing the phases separately
- * (bench.py's roofline) can time the launch the step really runs. */
+ * bf16 with RP_ATTN_Q_PRESCALED where both grids have at least one 128-row block per compute unit
+ * (B*H*ceil(T/128) >= 256 on 256 CUs: the metric shape, configs 2 and 4): rp_attn_bwd and rp_mha_bwd
+ * with phases 7 instead run rp_attn_bwd_delta's pass and ONE launch whose workgroups take either role
+ * (dK/dV blocks, then dQ blocks): same results up to the rounding of delta's sum.
+ * rp_attn_bwd_uses_roles tells whether rp_attn_bwd takes that form for a shape (1) or the two kernels
+ * (0), so a caller timing the phases separately (bench.py's roofline) can time the launch the step
+ * really runs. */
 int rp_attn_bwd_uses_roles(int dtype, int B, int T, int H, int dk);
 int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,
                 const float* lse, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,

@@ -2623,17 +2623,19 @@ void launch_bwd_q(bool delta, const MhaDev& a, hipStream_t s) {
 }
 
 // the two-role backward (attn_bwd_roles_kernel): bf16 with the producer's Q prescale on the LDS-DMA
-// kernels, 128-row blocks on both sides, and both grids in the split range (attn_split); RP_ATTN_ROLES=0
-// keeps the two kernels (read per launch)
+// kernels and 128-row blocks on both sides (both grids at least one workgroup per CU).  Config 4 (each
+// grid fills the CUs once: 2 x 256 four-wave blocks side by side instead of two launches of eight-wave
+// split blocks): step 7.48 -> 7.31 ms; the metric shape (2 x 1,024 blocks, one launch instead of two:
+// no drain / fill between the kernels, the roles' different lengths interleaved): 15.39 / 15.42 / 15.44
+// -> 15.33 / 15.26 / 15.27 ms (three interleaved pairs, round 5).  RP_ATTN_ROLES=0 keeps the two
+// kernels (read per launch)
 static bool attn_roles(const MhaDev& a) {
   const char* e = getenv("RP_ATTN_ROLES");
   if (e && e[0] == '0') return false;
   if (!a.qpre || a.empty_uniform || a.Tk > QD_TKMAX) return false;
   const int64_t gkv = (int64_t)((a.Tk + KV_KB - 1) / KV_KB) * a.B * a.H;
   const int64_t gq = (int64_t)((a.Tq + FW_QB - 1) / FW_QB) * a.B * a.H;
-  if (attn_small(gkv) || attn_small(gq)) return false;
-  if (e && e[0] == '2') return true;  // A/B: wherever legal (e.g. the metric shape's 2 x 1,024 blocks)
-  return attn_split(gkv, (a.Tq + KV_QT - 1) / KV_QT) && attn_split(gq, (a.Tk + FW_KT - 1) / FW_KT);
+  return !attn_small(gkv) && !attn_small(gq);
 }
 
 template <typename T>

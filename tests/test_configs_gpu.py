@@ -169,8 +169,7 @@ def test_config4_bf16_attention_T4096_dropout(dev, monkeypatch):
     """rp_attn fwd/bwd at T = 4096, B = 1 (8 heads: 256 blocks of 128 rows -> the three-part split
     forward and the two-role backward launch, asserted), dropout 0.1 with the stored keep bits, the Q
     columns prescaled as the model's QKV GEMM writes them; fwd and every gradient (dQ, dK, dV of all 8
-    heads) vs fp64, and against the unsplit 4-wave kernels (RP_ATTN_SPLIT=0, which also turns the roles
-    form off): keep bits bit for bit (the later key parts' streams are advanced by the skip-ahead
+    heads) vs fp64, and against the unsplit 4-wave kernels (RP_ATTN_SPLIT=0 and RP_ATTN_ROLES=0): keep bits bit for bit (the later key parts' streams are advanced by the skip-ahead
     multiplier), outputs and gradients within bf16 rounding."""
     from tests.test_kernels_gpu import close, close_per_seq, prescale_q, rnd
     B, H, T, p, seed = 1, 8, 4096, 0.1, 7
@@ -191,6 +190,7 @@ def test_config4_bf16_attention_T4096_dropout(dev, monkeypatch):
         cols = slice(part * H * 64, (part + 1) * H * 64)
         close_per_seq(dqkv[:, cols], gref[:, cols], B, atol=6e-2, rtol=6e-2, what=f"attn d{name} T=4096")
     monkeypatch.setenv("RP_ATTN_SPLIT", "0")
+    monkeypatch.setenv("RP_ATTN_ROLES", "0")
     assert not K.attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=True)
     o0, lse0, mask0 = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=True, out_lo=olo.clone())
     assert torch.equal(mask0, mask)

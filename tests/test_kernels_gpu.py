@@ -380,6 +380,7 @@ def test_attention_split_workgroups(dev, monkeypatch, p, split):
     in the merge), the dropout keep bits bit for bit against the restatement (the later parts' MWC
     streams start from the skip-ahead multiplier), fwd and every gradient vs fp64."""
     monkeypatch.setenv("RP_ATTN_SPLIT", split)
+    monkeypatch.setenv("RP_ATTN_ROLES", "0")  # the backward's own split kernels, not the two-role launch
     test_attention_128_blocks_ragged_dropout(dev, True, p=p)
 
 
@@ -435,6 +436,7 @@ def test_mha_cross_dropout_prescaled(dev, monkeypatch, split):
     forward / dQ split 16 key tiles 8 + 8, dK/dV 18 query tiles 9 + 9) and unsplit.  Keep bits bit for bit
     against the restatement (Tq x Tk streams), forward and every gradient vs fp64."""
     monkeypatch.setenv("RP_ATTN_SPLIT", split)
+    monkeypatch.setenv("RP_ATTN_ROLES", "0")  # the per-phase kernels (the two-role launch: test above)
     B, H, Tq, Tk, p, seed = 8, 8, 1100, 1000, 0.1, 31
     c = 0.125 * K.LOG2E
     q = rnd(B * Tq, H * 64, dev=dev, seed=15).to(torch.bfloat16)
@@ -714,14 +716,16 @@ def test_gemm_64_row_tiles_bitwise(dev, monkeypatch, M):
         assert torch.equal(a, c) and torch.equal(c, d) and torch.equal(a, e)
 
 
-@pytest.mark.parametrize("B,T,qpre", [(8, 2048, False), (8, 2048, True), (1, 4096, True)])
-def test_attention_metric_shape_bf16_dropout(dev, B, T, qpre):
+@pytest.mark.parametrize("B,T,qpre,roles", [(8, 2048, False, "1"), (8, 2048, True, "1"), (8, 2048, True, "0"),
+                                            (1, 4096, True, "1")])
+def test_attention_metric_shape_bf16_dropout(dev, monkeypatch, B, T, qpre, roles):
     """Attention at the bench shape (B = 8, T = 2048, H = 8, dk = 64) and at config 4's (B = 1, T = 4096)
     with dropout 0.1 and ragged key padding: forward output and all three gradients against an fp64
     torch restatement (same bf16 inputs, the restated keep bits) on a sample of (batch, head) pairs.
-    With the producer's Q prescale (qpre, what the model runs) the shipping LDS-DMA kernels run: at the
-    bench shape the fused-delta dQ kernel and the 128-key dK/dV kernel, at config 4 the delta pass and
-    the two-role launch (attn_bwd_roles_kernel) — asserted, so this is its fp64 check at T = 4096."""
+    With the producer's Q prescale (qpre, what the model runs) the shipping LDS-DMA kernels run: the
+    delta pass and the two-role launch (attn_bwd_roles_kernel) at both shapes — asserted — and with
+    RP_ATTN_ROLES=0 the fused-delta dQ kernel then the 128-key dK/dV kernel (the per-phase form)."""
+    monkeypatch.setenv("RP_ATTN_ROLES", roles)
     H = 8
     qkv0 = rnd(B * T, 3 * H * 64, dev=dev, seed=21).to(torch.bfloat16)
     if qpre:
@@ -734,8 +738,7 @@ def test_attention_metric_shape_bf16_dropout(dev, B, T, qpre):
     olo = torch.empty(B * T, H * 64, device=dev, dtype=torch.bfloat16)
     o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, seed, q_prescaled=qpre, out_lo=olo)
     do = rnd(B * T, H * 64, dev=dev, seed=22).to(torch.bfloat16)
-    if B == 1:
-        assert K.attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=qpre)
+    assert K.attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=qpre) == (qpre and roles == "1")
     dqkv = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=qpre, out_lo=olo)
     keep_all = attn_keep(B, H, T, p, seed, dev)                       # [B, H, T, T]
     q, k, v = eff.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)        # [B, H, T, 64]
