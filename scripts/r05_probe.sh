@@ -28,6 +28,15 @@ for s in ${STEPS:-dp wgrad wpmc roles sq}; do
             done
           done ;;
     sq) run sq 400 bash scripts/sq_attn.sh ${TAG}_sq ;;
+    wpad) for pd in 0 64 128 0; do run wpad$pd 200 python -u scripts/wgrad_probe.py --reps 10 --pad $pd; done
+          for pd in 0 64; do
+            for c in "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+              d=gpurun_out/${TAG}_wpad${pd}_$(echo $c | cut -d' ' -f1)
+              timeout -s KILL 90 rocprofv3 --pmc $c -d $d -o run --output-format csv -- \
+                python3 scripts/wgrad_probe.py --reps 2 --pad $pd > $d.log 2>&1
+              rc=$?; echo "wpad pmc pad=$pd $c rc=$rc"; if [ $rc -ne 0 ]; then tail -5 $d.log; exit $rc; fi
+            done
+          done ;;
     roles) run roles 900 bash scripts/ab_env_bench.sh RP_ATTN_ROLES 3 "--steps 20 --warmup 3 --no-cpu-baseline --no-parity-mode --no-fresh-batch" 1 2 ;;
   esac
 done

@@ -13,11 +13,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from repurpose_amd import kernels as K  # noqa: E402
 
 
-def items(dev, L=16, T=16384, d=512, dff=2048, seed=0):
+def items(dev, L=16, T=16384, d=512, dff=2048, seed=0, pad=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
 
-    def r(n):
-        return (torch.randn(T, n, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    def r(n):  # [T, n] operand; pad > 0: rows `pad` elements longer than n (a non-power-of-two stride)
+        x = (torch.randn(T, n, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+        if pad == 0:
+            return x
+        buf = torch.zeros(T, n + pad, dtype=torch.bfloat16, device=dev)
+        buf[:, :n] = x
+        return buf[:, :n]
     out = []
     for l in reversed(range(L)):  # backward order: linear2, linear1, out_proj, in_proj per layer
         for n_out, n_in in ((d, dff), (dff, d), (d, d), (3 * d, d)):
@@ -30,9 +35,10 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--env", nargs="*", default=[])
     ap.add_argument("--cut", type=int, default=64, help="items per launch (64 = all 16 layers in one)")
+    ap.add_argument("--pad", type=int, default=0, help="operand row padding in elements")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    it = items(dev)
+    it = items(dev, pad=a.pad)
     variants = [("default", {})] + [(e, dict([e.split("=", 1)])) for e in a.env]
     ref = None
     for name, env in variants:
