@@ -636,13 +636,52 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 // =================================================================================================
 // backward pre-pass: delta[bh][q] = sum_d dO[q][d] * O[q][d]
 // =================================================================================================
+// one wave per DELTA_RPW query rows, 8 lanes per head; bf16 (D = 512): every load of the wave's rows
+// is issued before the first use, so a wave keeps 3 x DELTA_RPW x 1 KB in flight and the grid's
+// 4,096 waves (metric shape) are all resident at once — one HBM round trip instead of two rounds of
+// one-row waves (14.5 us -> see DESIGN.md §8 round 5)
+constexpr int DELTA_RPW = 4;
+__device__ __forceinline__ void delta_store(const MhaDev& a, int64_t row, int e, float s) {
+  const int b = (int)(row / a.Tq), t = (int)(row % a.Tq);
+  const int64_t at = ((int64_t)b * a.H + e / HD) * a.Tq + t, plane = (int64_t)a.B * a.H * a.Tq;
+  a.delta[at] = s;
+  // the dK/dV kernel's row constants (plane 1, 2): -delta/ds and -lse*log2(e) + log2(ds)
+  a.delta[plane + at] = -s / a.drop_scale;
+  if (a.lse) a.delta[2 * plane + at] = -(a.lse[at] * LOG2E - log2f(a.drop_scale));
+}
 template <typename T>
 __global__ void attn_delta_kernel(MhaDev a) {
-  // one wave per (b, t) query row; 8 lanes per head
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (int64_t)a.B * a.Tq) return;
+  const int64_t rows = (int64_t)a.B * a.Tq;
   const int D = a.H * HD;
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (D == 8 * 64) {  // the metric shape's d_model = 512: lane = 8 columns of one head, 4 rows per wave
+      const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * DELTA_RPW;
+      const int e = lane * 8;
+      bf16x8 ov[DELTA_RPW], dv[DELTA_RPW], lv[DELTA_RPW];
+#pragma unroll
+      for (int r = 0; r < DELTA_RPW; ++r) {
+        const int64_t row = row0 + r < rows ? row0 + r : rows - 1;
+        ov[r] = *reinterpret_cast<const bf16x8*>((const bf16*)a.out + row * a.ldo + e);
+        dv[r] = *reinterpret_cast<const bf16x8*>((const bf16*)a.dout + row * a.lddo + e);
+        if (a.out_lo) lv[r] = *reinterpret_cast<const bf16x8*>((const bf16*)a.out_lo + row * a.ldo + e);
+      }
+#pragma unroll
+      for (int r = 0; r < DELTA_RPW; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += ((float)ov[r][j] + (a.out_lo ? (float)lv[r][j] : 0.f)) * (float)dv[r][j];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        if ((lane & 7) == 0 && row0 + r < rows) delta_store(a, row0 + r, e, s);
+      }
+      return;
+    }
+  }
+  // general: one wave per (b, t) query row
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
   const T* o = (const T*)a.out + row * a.ldo;
   const T* ol = a.out_lo ? (const T*)a.out_lo + row * a.ldo : nullptr;
   const T* d = (const T*)a.dout + row * a.lddo;
@@ -662,15 +701,14 @@ __global__ void attn_delta_kernel(MhaDev a) {
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
-    if ((lane & 7) == 0) {
-      const int b = (int)(row / a.Tq), t = (int)(row % a.Tq);
-      const int64_t at = ((int64_t)b * a.H + e / HD) * a.Tq + t, plane = (int64_t)a.B * a.H * a.Tq;
-      a.delta[at] = s;
-      // the dK/dV kernel's row constants (plane 1, 2): -delta/ds and -lse*log2(e) + log2(ds)
-      a.delta[plane + at] = -s / a.drop_scale;
-      if (a.lse) a.delta[2 * plane + at] = -(a.lse[at] * LOG2E - log2f(a.drop_scale));
-    }
+    if ((lane & 7) == 0) delta_store(a, row, e, s);
   }
+}
+template <typename T>
+dim3 delta_grid(const MhaDev& a) {
+  const int64_t rows = (int64_t)a.B * a.Tq;
+  const int64_t rpb = (std::is_same<T, bf16>::value && a.H * HD == 512) ? 4 * DELTA_RPW : 4;
+  return dim3((unsigned)((rows + rpb - 1) / rpb));
 }
 
 // =================================================================================================
@@ -2644,7 +2682,7 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
   const int nkb = (a.Tk + KV_KB - 1) / KV_KB;
   if (std::is_same<T, bf16>::value && (phases & 6) == 6 && attn_roles(a)) {
     if (phases & 1)
-      hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
+      hipLaunchKernelGGL(attn_delta_kernel<T>, delta_grid<T>(a), dim3(256), 0, s, a);
     const int nkv = nkb * a.B * a.H;
     const dim3 grid((unsigned)(nkv + (a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
     if (a.drop_thresh)
@@ -2677,7 +2715,7 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
       launch_bwd_q<T, 2>(true, a, s);
     }
   } else if (phases & 1) {
-    hipLaunchKernelGGL(attn_delta_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_delta_kernel<T>, delta_grid<T>(a), dim3(256), 0, s, a);
   }
   if (phases & 2) {
     // 128-key blocks unless that leaves fewer than one workgroup per CU: then 64

