@@ -2139,22 +2139,10 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDe
 // as eight-wave split workgroups one per CU: here 512 four-wave workgroups two per CU, the dQ blocks
 // beside the dK/dV ones, with no partial merge and no cross-stream wait (RP_ATTN_BWD_OVERLAP: 42-68 us).
 constexpr int ROLES_LDS = 3 * KV_DMA_BUF > QD_DMA_LDS(1) ? 3 * KV_DMA_BUF : QD_DMA_LDS(1);
-// il (equal role counts, a multiple of 8): the roles alternate every 8 blocks (blocks 16g .. 16g+7 the
-// dK/dV blocks 8g .. 8g+7, the next 8 the dQ blocks 8g .. 8g+7), so each CU holds one block of each role
-// instead of all dK/dV blocks first; a role's block index stays = blockIdx mod 8, the XCD its bodies'
-// remap assumes
 template <bool DROP>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_roles_kernel(MhaDev a, int nkv, int il) {
+__global__ __launch_bounds__(NT, 2) void attn_bwd_roles_kernel(MhaDev a, int nkv) {
   __shared__ __attribute__((aligned(1024))) char lds[ROLES_LDS];
   const int blk = blockIdx.x;
-  if (il) {
-    const int idx = (blk >> 4) * 8 + (blk & 7);
-    if ((blk & 8) == 0)
-      attn_bwd_kv_dma_body<DROP, 2, true, 1>(a, idx, lds);
-    else
-      attn_bwd_q_dma_body<DROP, 1, false>(a, idx, lds);
-    return;
-  }
   if (blk < nkv)
     attn_bwd_kv_dma_body<DROP, 2, true, 1>(a, blk, lds);
   else
@@ -2696,14 +2684,11 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
     if (phases & 1)
       hipLaunchKernelGGL(attn_delta_kernel<T>, delta_grid<T>(a), dim3(256), 0, s, a);
     const int nkv = nkb * a.B * a.H;
-    const int nq = (a.Tq + FW_QB - 1) / FW_QB * a.B * a.H;
-    const dim3 grid((unsigned)(nkv + nq));
-    const char* ie = getenv("RP_ATTN_ROLES_IL");  // A/B (read per launch)
-    const int il = (ie && ie[0] == '1' && nkv == nq && nkv % 8 == 0) ? 1 : 0;
+    const dim3 grid((unsigned)(nkv + (a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
     if (a.drop_thresh)
-      hipLaunchKernelGGL(attn_bwd_roles_kernel<true>, grid, dim3(NT), 0, s, a, nkv, il);
+      hipLaunchKernelGGL(attn_bwd_roles_kernel<true>, grid, dim3(NT), 0, s, a, nkv);
     else
-      hipLaunchKernelGGL(attn_bwd_roles_kernel<false>, grid, dim3(NT), 0, s, a, nkv, il);
+      hipLaunchKernelGGL(attn_bwd_roles_kernel<false>, grid, dim3(NT), 0, s, a, nkv);
     return rp_check_launch("rp_mha_bwd");
   }
   // dQ: 128-query blocks unless that leaves fewer than one workgroup per CU (then 64, as the forward)
