@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from repurpose_amd import kernels as K  # noqa: E402
 
 
-def items(dev, L=16, T=16384, d=512, dff=2048, seed=0, pad=0):
+def items(dev, L=16, T=16384, d=512, dff=2048, seed=0, pad=0, only=None):
     g = torch.Generator(device="cpu").manual_seed(seed)
 
     def r(n):  # [T, n] operand; pad > 0: rows `pad` elements longer than n (a non-power-of-two stride)
@@ -25,7 +25,9 @@ def items(dev, L=16, T=16384, d=512, dff=2048, seed=0, pad=0):
         return buf[:, :n]
     out = []
     for l in reversed(range(L)):  # backward order: linear2, linear1, out_proj, in_proj per layer
-        for n_out, n_in in ((d, dff), (dff, d), (d, d), (3 * d, d)):
+        for name, (n_out, n_in) in zip(("linear2", "linear1", "out_proj", "in_proj"), ((d, dff), (dff, d), (d, d), (3 * d, d))):
+            if only and name != only:
+                continue
             out.append((r(n_out), r(n_in), torch.empty(n_out, n_in, device=dev), torch.empty(n_out, device=dev)))
     return out
 
@@ -36,9 +38,10 @@ def main():
     ap.add_argument("--env", nargs="*", default=[])
     ap.add_argument("--cut", type=int, default=64, help="items per launch (64 = all 16 layers in one)")
     ap.add_argument("--pad", type=int, default=0, help="operand row padding in elements")
+    ap.add_argument("--only", default=None, help="one GEMM kind of the 4 (linear2 | linear1 | out_proj | in_proj)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    it = items(dev, pad=a.pad)
+    it = items(dev, pad=a.pad, only=a.only)
     variants = [("default", {})] + [(e, dict([e.split("=", 1)])) for e in a.env]
     ref = None
     for name, env in variants:
