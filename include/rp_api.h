@@ -98,6 +98,17 @@ int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t l
             const void* B, int64_t ldb, int b_kmajor, void* C, int64_t ldc, int c_dtype, float alpha,
             const rp_gemm_epilogue* ep, void* stream);
 
+/* The attention output's gradient with the attention backward's delta pre-pass fused into its
+ * epilogue (bf16): dO = dY W (the self_attn.out_proj dgrad of models/MMCTransformer.py:41-55 under
+ * loss.backward(); dY [M, ldy] k-major, W [K, ldw] the out_proj weight, dO [M, ldo] bf16 written) and,
+ * per row m = b*T + t and head h, delta = sum_d dO[m][64h + d] * (out + out_lo)[m][64h + d] into
+ * delta_ws planes 0..2 exactly as rp_attn_bwd_delta writes them (bitwise: the stored bf16 dO, the
+ * same summation order), so rp_mha_bwd / rp_attn_bwd_given_delta can skip the pre-pass.
+ * M = B*T and H*64 multiples of 128, K a multiple of 64. */
+int rp_gemm_attn_dout_delta(const void* dY, int64_t ldy, const void* W, int64_t ldw, int64_t M, int64_t K, void* dO,
+                            int64_t ldo, const void* out, const void* out_lo, int64_t ld_out, const float* lse, int B,
+                            int T, int H, float dropout_p, float* delta_ws, void* stream);
+
 /* Weight gradient of a Linear layer: dW[m, n] (+)= sum_k dY[k, m] * X[k, n] and (if db)
  * db[m] (+)= sum_k dY[k, m] — the token dimension K is split over workgroups (deterministic
  * split-K: fp32 partial slabs in `workspace`, reduced in a fixed order); the bias gradient is
@@ -410,6 +421,11 @@ int rp_attn_bwd_uses_roles(int dtype, int B, int T, int H, int dk);
 int rp_attn_bwd(int dtype, const void* qkv, const void* out, const void* out_lo, const void* dout,
                 const float* lse, const uint8_t* key_valid, int B, int T, int H, int dk, float scale,
                 float dropout_p, const uint16_t* dropmask, void* dqkv, float* delta_ws, void* stream);
+/* rp_attn_bwd without the delta pre-pass: delta_ws already holds its three planes (rp_attn_bwd_delta or
+ * rp_gemm_attn_dout_delta); the two-role launch, or the dQ kernel reading the planes then dK/dV. */
+int rp_attn_bwd_given_delta(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,
+                            const uint8_t* key_valid, int B, int T, int H, int dk, float scale, float dropout_p,
+                            const uint16_t* dropmask, void* dqkv, void* stream);
 int rp_attn_bwd_delta(int dtype, const void* out, const void* out_lo, const void* dout, const float* lse, int B,
                       int T, int H, int dk, float dropout_p, float* delta_ws, void* stream);
 int rp_attn_bwd_dkdv(int dtype, const void* qkv, const void* dout, const float* lse, const float* delta_ws,

@@ -747,10 +747,14 @@ class _Schedule:
                                           dgamma=G(pre + "norm2.weight"), dbeta=G(pre + "norm2.bias"), ws=ws, defer=cs)
             # out_proj
             wgrad(g1, o, pre + "self_attn.out_proj.weight", pre + "self_attn.out_proj.bias")
-            do = K.linear_dgrad(g1, self.W(pre + "self_attn.out_proj.weight"), out_dtype=dt)
-            # attention
+            # attention (bf16: the delta = rowsum(dO * O) pre-pass rides in the out_proj dgrad's epilogue)
+            if K.attn_dout_delta_ok(M, H, d, dt):
+                do, delta = K.attn_dout_delta(g1, self.W(pre + "self_attn.out_proj.weight"), o, olo, lse, B, T, H, p)
+            else:
+                do = K.linear_dgrad(g1, self.W(pre + "self_attn.out_proj.weight"), out_dtype=dt)
+                delta = None
             dqkv = K.attn_bwd(qkv, o, do, lse, self.kv, B, T, H, self.scale, p, dropmask=dmask, q_prescaled=True,
-                              out_lo=olo)
+                              out_lo=olo, delta=delta)
             # in_proj
             wgrad(dqkv, h1, pre + "self_attn.in_proj_weight", pre + "self_attn.in_proj_bias")
             # norm1 + residual; masked lp gradient for the previous layer's dropout2

@@ -106,6 +106,10 @@ _SIGNATURES = {
     "rp_attn_dropmask_elems": (c_i64, [c_i, c_i, c_i]),
     "rp_attn_fwd": (c_i, [c_i, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rp_attn_bwd_uses_roles": (c_i, [c_i, c_i, c_i, c_i, c_i]),
+    "rp_attn_bwd_given_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp, c_vp,
+                                      c_vp]),
+    "rp_gemm_attn_dout_delta": (c_i, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                      c_i, c_i, c_i, c_f, c_vp, c_vp]),
     "rp_attn_bwd": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_f, c_vp,
                           c_vp, c_vp, c_vp]),
     "rp_attn_bwd_delta": (c_i, [c_i, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_f, c_vp, c_vp]),

@@ -2921,6 +2921,14 @@ extern "C" int rp_attn_bwd(int dtype, const void* qkv, const void* out, const vo
                          dqkv, delta_ws, stream);
 }
 
+extern "C" int rp_attn_bwd_given_delta(int dtype, const void* qkv, const void* dout, const float* lse,
+                                       const float* delta_ws, const uint8_t* key_valid, int B, int T, int H, int dk,
+                                       float scale, float dropout_p, const uint16_t* dropmask, void* dqkv,
+                                       void* stream) {
+  return attn_bwd_packed(6, dtype, qkv, nullptr, nullptr, dout, lse, key_valid, B, T, H, dk, scale, dropout_p, dropmask,
+                         dqkv, const_cast<float*>(delta_ws), stream);
+}
+
 extern "C" int rp_attn_bwd_delta(int dtype, const void* out, const void* out_lo, const void* dout, const float* lse,
                                  int B, int T, int H, int dk, float dropout_p, float* delta_ws, void* stream) {
   RP_REQUIRE(dk == HD, "rp_attn_bwd_delta: head dim %d unsupported (64)", dk);

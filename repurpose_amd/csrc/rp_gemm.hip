@@ -51,6 +51,16 @@ struct EpiDev {
   float col_scale;
   int split_major;  // split-K: deal the (split, tile) work items split-major over the XCDs (see tile_split)
   int prefetch_gate;  // 256-row kernel: touch the tile's bf16 gate lines one K-tile before the epilogue
+  // attention delta fused into the attention-output gradient GEMM (rp_gemm_attn_dout_delta; bf16 C,
+  // 128 x 128 tiles, M % 128 == N % 128 == 0): per (row, 64-column head) the row dot of the STORED bf16
+  // output with (dot_hi + dot_lo) -> the delta workspace planes, exactly as attn_delta_kernel forms them
+  const bf16* dot_hi;
+  const bf16* dot_lo;  // may be null
+  int64_t ld_dot;
+  float* delta;        // [3, B, H, T] fp32
+  const float* lse;    // [B, H, T]
+  int dT, dH;          // rows are b * dT + t; dH heads of 64 columns
+  float dscale;        // 1 / (1 - p)
 };
 
 // Work item of a workgroup: output tile t (XCD-aware: consecutive tiles share an XCD's L2) and, for
@@ -367,6 +377,27 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* l
 #pragma unroll
       for (int e = 0; e < 8; ++e) ob[e] = (bf16)v[e];
       *reinterpret_cast<uint4*>(dst) = o;
+      if (MODE == 0 && ep.delta) {
+        // the row dot of this chunk's 8 stored values with the output (hi + lo), then the 8 chunks of
+        // the head (consecutive lanes: 16 chunks per row, M and N whole tiles so every lane is here)
+        // by xor 1, 2, 4 — attn_delta_kernel's order, so the planes are bitwise its
+        const bf16x8 oh = *reinterpret_cast<const bf16x8*>(ep.dot_hi + m * ep.ld_dot + n);
+        bf16x8 ol;
+        if (ep.dot_lo) ol = *reinterpret_cast<const bf16x8*>(ep.dot_lo + m * ep.ld_dot + n);
+        float dsum = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dsum += ((float)oh[e] + (ep.dot_lo ? (float)ol[e] : 0.f)) * (float)ob[e];
+        dsum += __shfl_xor(dsum, 1, 64);
+        dsum += __shfl_xor(dsum, 2, 64);
+        dsum += __shfl_xor(dsum, 4, 64);
+        if ((n & 63) == 0) {
+          const int b = (int)(m / ep.dT), t = (int)(m % ep.dT);
+          const int64_t at = ((int64_t)b * ep.dH + n / 64) * ep.dT + t, plane = (M / ep.dT) * ep.dH * ep.dT;
+          ep.delta[at] = dsum;
+          ep.delta[plane + at] = -dsum / ep.dscale;
+          ep.delta[2 * plane + at] = -(ep.lse[at] * 1.4426950408889634f - log2f(ep.dscale));
+        }
+      }
     }
   }
   }
@@ -2073,6 +2104,40 @@ extern "C" int rp_gemm_wgrad_grouped(int64_t K, const rp_wgrad_item* items, int 
   else
     hipLaunchKernelGGL(wgrad_grouped_kernel, dim3((unsigned)tiles), dim3(NT), 0, (hipStream_t)stream, g);
   return rp_check_launch("rp_gemm_wgrad_grouped");
+}
+
+extern "C" int rp_gemm_attn_dout_delta(const void* dY, int64_t ldy, const void* W, int64_t ldw, int64_t M, int64_t K,
+                                       void* dO, int64_t ldo, const void* out, const void* out_lo, int64_t ld_out,
+                                       const float* lse, int B, int T, int H, float dropout_p, float* delta_ws,
+                                       void* stream) {
+  const int64_t N = (int64_t)H * 64;
+  RP_REQUIRE(B > 0 && T > 0 && H > 0 && M == (int64_t)B * T, "rp_gemm_attn_dout_delta: M must be B*T");
+  RP_REQUIRE(M % BM == 0 && N % BN == 0 && K % 64 == 0 && K > 0,
+             "rp_gemm_attn_dout_delta: M and H*64 multiples of 128, K a multiple of 64");
+  RP_REQUIRE(dY && W && dO && out && lse && delta_ws, "rp_gemm_attn_dout_delta: null pointer");
+  RP_REQUIRE(rp_aligned16(dY) && rp_aligned16(W) && rp_aligned16(dO) && rp_aligned16(out) &&
+                 (!out_lo || rp_aligned16(out_lo)),
+             "rp_gemm_attn_dout_delta: 16-byte alignment required");
+  RP_REQUIRE(ldy >= K && ldw >= N && ldo >= N && ld_out >= N && ldy % 8 == 0 && ldw % 8 == 0 && ldo % 8 == 0 &&
+                 ld_out % 8 == 0,
+             "rp_gemm_attn_dout_delta: leading dims");
+  RP_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "rp_gemm_attn_dout_delta: dropout_p out of range");
+  EpiDev e{};
+  e.gate_scale = 1.f;
+  e.dot_hi = (const bf16*)out;
+  e.dot_lo = (const bf16*)out_lo;
+  e.ld_dot = ld_out;
+  e.delta = delta_ws;
+  e.lse = lse;
+  e.dT = T;
+  e.dH = H;
+  e.dscale = dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f;
+  // dO = dY W: k-major A = dY [M, K], B = W [K, N] row-major (the nn.Linear weight's dgrad layout),
+  // 128 x 128 tiles, configuration 0 — the only path that carries the fused delta
+  const dim3 grid((unsigned)((M / BM) * (N / BN)));
+  hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, bf16, 0, 0>), grid, dim3(NT), 0, (hipStream_t)stream, M, N, K,
+                     (const bf16*)dY, ldy, (const bf16*)W, ldw, (bf16*)dO, ldo, 1.f, e, (int64_t)0, (float*)nullptr);
+  return rp_check_launch("rp_gemm_attn_dout_delta");
 }
 
 extern "C" int64_t rp_gemm_wgrad_workspace(int64_t M, int64_t N, int64_t K) {

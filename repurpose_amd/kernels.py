@@ -413,19 +413,79 @@ def attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=False):
     return bool(N.load().rp_attn_bwd_uses_roles(_adt(qkv, q_prescaled), B, T, H, qkv.shape[1] // (3 * H)))
 
 
+def attn_dout_delta(dy, W, out, out_lo, lse, B, T, H, dropout_p=0.0):
+    """dO = dy W (bf16, the attention output's gradient through out_proj) with the attention backward's
+    delta planes formed in the same launch (rp_gemm_attn_dout_delta).  -> (dO [M, H*64], delta
+    [3, B, H, T]); hand delta to attn_bwd(delta=...).  bf16 operands, M = B*T and H*64 multiples of 128."""
+    _gpu(dy, W, out, out_lo, lse)
+    M, K = dy.shape
+    D = H * 64
+    if dy.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
+        raise TypeError("attn_dout_delta: bf16 operands")
+    if W.shape != (K, D) or out.shape != (M, D) or M != B * T or dy.stride(1) != 1 or W.stride(1) != 1:
+        raise ValueError("attn_dout_delta: dy [B*T, K], W [K, H*64], out [B*T, H*64] with unit column strides")
+    if out_lo is not None and (out_lo.shape != out.shape or out_lo.stride(0) != out.stride(0)):
+        raise ValueError("attn_dout_delta: out_lo must be laid out as out")
+    _contig(lse)
+    dO = torch.empty(M, D, device=dy.device, dtype=torch.bfloat16)
+    delta = torch.empty(3, B, H, T, device=dy.device, dtype=torch.float32)
+    N.call("rp_gemm_attn_dout_delta", _p(dy), dy.stride(0), _p(W), W.stride(0), M, K, _p(dO), D, _p(out), _p(out_lo),
+           out.stride(0), _p(lse), B, T, H, float(dropout_p), _p(delta), _stream(dy))
+    return dO, delta
+
+
+def attn_delta(out, out_lo, dout, lse, B, T, H, dropout_p=0.0):
+    """The attention backward's delta pre-pass alone (rp_attn_bwd_delta): [3, B, H, T] planes
+    (delta, -delta / (1 / (1 - p)), -lse log2 e + log2 (1 / (1 - p)))."""
+    _gpu(out, out_lo, dout, lse)
+    _contig(out, dout, lse)
+    delta = torch.empty(3, B, H, T, device=out.device, dtype=torch.float32)
+    N.call("rp_attn_bwd_delta", _dt(out), _p(out), _p(out_lo), _p(dout), _p(lse), B, T, H, out.shape[1] // H,
+           float(dropout_p), _p(delta), _stream(out))
+    return delta
+
+
+def attn_dout_delta_ok(M, H, K, dtype):
+    """Whether the fused dO + delta launch serves a shape (else linear_dgrad + attn_bwd's own pass)."""
+    return dtype == torch.bfloat16 and M % 128 == 0 and (H * 64) % 128 == 0 and K % 64 == 0
+
+
 def attn_bwd(qkv, out, dout, lse, key_valid, B, T, H, scale, dropout_p=0.0, seed=0, dropmask=None,
-             q_prescaled=False, out_lo=None):
-    _gpu(qkv, out, dout, lse, key_valid, dropmask)
+             q_prescaled=False, out_lo=None, delta=None):
+    """-> dqkv.  delta (optional): the [3, B, H, T] planes already formed (attn_dout_delta); the
+    backward then skips its own delta pass."""
+    _gpu(qkv, out, dout, lse, key_valid, dropmask, delta)
     _contig(qkv, out, dout, lse, key_valid)
     if dropout_p > 0 and dropmask is None:
         raise ValueError("attn_bwd: dropout needs the forward's dropmask")
     dk = qkv.shape[1] // (3 * H)
     dqkv = torch.empty_like(qkv)
-    delta = torch.empty(3, B, H, T, device=qkv.device, dtype=torch.float32)  # delta + 2 row-constant planes
     st, dt = _stream(qkv), _adt(qkv, q_prescaled)
     e0 = _tick("attn_bwd")
     timed = {"attn_bwd_dq", "attn_bwd_dkdv", "attn_bwd_roles"} & set(_timer["names"])
     roles = bool(timed) and attn_bwd_uses_roles(qkv, B, T, H, q_prescaled)
+    if delta is not None:
+        _contig(delta)
+        if tuple(delta.shape) != (3, B, H, T) or delta.dtype != torch.float32:
+            raise ValueError("attn_bwd: delta must be fp32 [3, B, H, T]")
+        if not timed or roles:
+            e3 = _tick("attn_bwd_roles") if roles else None
+            N.call("rp_attn_bwd_given_delta", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
+                   float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
+            _tock(e3)
+            _tock(e0)
+            return dqkv
+        e2 = _tick("attn_bwd_dq")
+        N.call("rp_attn_bwd_dq", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
+               float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
+        _tock(e2)
+        e1 = _tick("attn_bwd_dkdv")
+        N.call("rp_attn_bwd_dkdv", dt, _p(qkv), _p(dout), _p(lse), _p(delta), _p(key_valid), B, T, H, dk,
+               float(scale), float(dropout_p), _p(dropmask), _p(dqkv), st)
+        _tock(e1)
+        _tock(e0)
+        return dqkv
+    delta = torch.empty(3, B, H, T, device=qkv.device, dtype=torch.float32)  # delta + 2 row-constant planes
     if not timed or roles:
         # one entry: the library launches the fused-delta dQ kernel then dK/dV, or, where each grid
         # fills the CUs once but not twice (config 4), the delta pass and ONE two-role launch (timed

@@ -838,3 +838,32 @@ def test_gemm8_dgrad_gate_prefetch_repeat_bitwise(dev, Kr):
             first = got.clone()
         else:
             assert torch.equal(first, got)
+
+
+@pytest.mark.parametrize("B,T,p", [(8, 2048, 0.1), (2, 384, 0.0)])
+def test_attn_dout_delta_fused_bitwise(dev, B, T, p):
+    """rp_gemm_attn_dout_delta (the out_proj dgrad with the attention delta pre-pass in its epilogue)
+    against the two launches it replaces: dO bitwise the plain dgrad GEMM's, the three delta planes
+    bitwise rp_attn_bwd_delta's on that dO, and the attention backward fed those planes bitwise the
+    backward that forms them itself (two-role launch at the metric shape)."""
+    H, d = 8, 512
+    M = B * T
+    g1 = rnd(M, d, dev=dev, seed=51).to(torch.bfloat16)
+    W = rnd(d, d, dev=dev, seed=52, scale=0.05).to(torch.bfloat16)
+    qkv = rnd(M, 3 * d, dev=dev, seed=53).to(torch.bfloat16)
+    qkv, _ = prescale_q(qkv, H, 0.125)
+    kv = torch.ones(B, T, dtype=torch.uint8, device=dev)
+    kv[-1, T // 3:] = 0
+    olo = torch.empty(M, d, device=dev, dtype=torch.bfloat16)
+    o, lse, mask = K.attn_fwd(qkv, kv, B, T, H, 0.125, p, 7, q_prescaled=True, out_lo=olo)
+    do_ref = K.linear_dgrad(g1, W, out_dtype=torch.bfloat16)
+    do, delta = K.attn_dout_delta(g1, W, o, olo, lse, B, T, H, p)
+    assert torch.equal(do, do_ref)
+    delta_ref = K.attn_delta(o, olo, do_ref, lse, B, T, H, p)
+    assert torch.equal(delta, delta_ref)
+    ref = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True, out_lo=olo)
+    got = K.attn_bwd(qkv, o, do, lse, kv, B, T, H, 0.125, p, dropmask=mask, q_prescaled=True, out_lo=olo, delta=delta)
+    if K.attn_bwd_uses_roles(qkv, B, T, H, q_prescaled=True):
+        assert torch.equal(got, ref)  # the same delta planes into the same launch
+    else:  # the small-grid dQ kernel forms delta itself when not given it: same value, another sum order
+        close(got, ref.double(), atol=2e-2, rtol=2e-2, what="given-delta vs fused-delta backward")
