@@ -5,6 +5,7 @@ current torch stream through ``_native.call``.  Outputs are allocated with the t
 allocator; the library itself never allocates.  There is no CPU path: CPU tensors raise.
 """
 import ctypes
+import os
 
 import torch
 
@@ -446,7 +447,10 @@ def attn_delta(out, out_lo, dout, lse, B, T, H, dropout_p=0.0):
 
 
 def attn_dout_delta_ok(M, H, K, dtype):
-    """Whether the fused dO + delta launch serves a shape (else linear_dgrad + attn_bwd's own pass)."""
+    """Whether the fused dO + delta launch serves a shape (else linear_dgrad + attn_bwd's own pass);
+    RP_DOUT_DELTA=0 turns it off (A/B)."""
+    if os.environ.get("RP_DOUT_DELTA", "1") == "0":
+        return False
     return dtype == torch.bfloat16 and M % 128 == 0 and (H * 64) % 128 == 0 and K % 64 == 0
 
 
