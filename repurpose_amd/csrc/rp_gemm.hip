@@ -1383,6 +1383,20 @@ __global__ __launch_bounds__(NT8, 1) void wgrad8_grouped_kernel(const WgGroup g)
                                           n0 == 0 ? w.db : nullptr, g.accumulate, lds);
 }
 
+// compute units of the current device (cached per device); the tile-shape rules below count workgroups
+// per CU in units of it (256 on a whole MI355X)
+static int64_t gemm_cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 // 256-row phased path selection.  RP_GEMM8=0 disables it, RP_GEMM8=1 forces it wherever legal
 // (read per call: scripts/gemm_ab.py switches it between launches).  Default: the wide short-K
 // shapes with at least one 256 x 256 tile per CU (MI355X, M = 16384: linear1 forward 54.6 ->
@@ -1404,7 +1418,7 @@ static int rp_gemm8_bn(int64_t M, int64_t N, int64_t kext) {
   if (mode == 0) return 0;
   if (mode == 1) return 256;
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  return (N >= 2048 && kext <= 1024 && tiles >= 256) ? 256 : 0;
+  return (N >= 2048 && kext <= 1024 && tiles >= gemm_cu_count()) ? 256 : 0;
 }
 
 // dst[i] (+)= sum_s slab[s][i] in fixed slab order (deterministic), for the weight slabs (n
@@ -1463,7 +1477,7 @@ static int rp_gemm_cfg(int64_t kext, int64_t n, int64_t m) {
   if (forced >= 0) return (forced == 2 || kext % 64 == 0) ? forced : 2;
   if (kext % 64 != 0) return 2;
   const int64_t tiles = ((m + BM - 1) / BM) * ((n + BN - 1) / BN);
-  return (kext <= 1024 && n >= 1536 && policy == 1 && tiles > 512) ? 1 : 0;
+  return (kext <= 1024 && n >= 1536 && policy == 1 && tiles > 2 * gemm_cu_count()) ? 1 : 0;
 }
 
 // RP_WGRAD8=0: the grouped weight gradients on 128 x 128 tiles instead of 256 x 256 (A/B tuning)
@@ -1548,7 +1562,7 @@ static bool rp_gemm_bm64(int64_t M, int64_t N) {
   const char* e = getenv("RP_GEMM_BM64");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return ((M + BM - 1) / BM) * ((N + BN - 1) / BN) < 512;
+  return ((M + BM - 1) / BM) * ((N + BN - 1) / BN) < 2 * gemm_cu_count();
 }
 
 // 32 x 128 tiles (each wave 16 x 64; the same K order per output element, so bitwise the 64- and
@@ -1559,7 +1573,7 @@ static bool rp_gemm_bm32(int64_t M, int64_t N) {
   const char* e = getenv("RP_GEMM_BM32");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return ((M + 63) / 64) * ((N + BN - 1) / BN) < 512;
+  return ((M + 63) / 64) * ((N + BN - 1) / BN) < 2 * gemm_cu_count();
 }
 
 template <typename T, typename TC>
