@@ -61,10 +61,6 @@ struct EpiDev {
   const float* lse;    // [B, H, T]
   int dT, dH;          // rows are b * dT + t; dH heads of 64 columns
   float dscale;        // 1 / (1 - p)
-  // A/B: workgroups from stagger_from on start stagger_cycles later (the second workgroup of each CU on
-  // a grid of exactly two per CU), so the two tiles' HBM-bound epilogues do not coincide
-  int stagger_from;
-  int stagger_cycles;
 };
 
 // Work item of a workgroup: output tile t (XCD-aware: consecutive tiles share an XCD's L2) and, for
@@ -698,10 +694,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
     kend = kbeg + kchunk < K ? kbeg + kchunk : K;
   }
   const bool want_bias = MODE == 1 && !AK && bslab != nullptr && n0 == 0;
-  if (ep.stagger_cycles > 0 && (int)(blockIdx.x + blockIdx.y * gridDim.x) >= ep.stagger_from) {
-    const uint64_t st0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - st0 < (uint64_t)ep.stagger_cycles) __builtin_amdgcn_s_sleep(16);
-  }
   f32x4 acc[MI][4];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -1592,18 +1584,6 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
   const T* a = (const T*)A;
   const T* b = (const T*)B;
   TC* c = (TC*)Cp;
-  EpiDev epx = ep;
-  {
-    const char* se = getenv("RP_GEMM_STAGGER");  // A/B (read per call): cycles
-    const int cyc = se ? atoi(se) : 0;
-    const int64_t cus = gemm_cu_count();
-    if (cyc > 0 && splits == 0 && tiles == 2 * cus) {
-      epx.stagger_from = (int)cus;
-      epx.stagger_cycles = cyc;
-    }
-  }
-  const EpiDev& ep2 = epx;
-#define ep ep2
   if constexpr (std::is_same<T, bf16>::value) {
     const int bn8 = splits == 0 ? rp_gemm8_bn(M, N, K) : 0;
     if (bn8 > 0 && rp_dma_enabled())
@@ -1710,7 +1690,6 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
     else if (!ak && !bk) RP_GEMM_LAUNCH(false, false, 1, grid);
     else RP_GEMM_LAUNCH(false, true, 1, grid);
   }
-#undef ep
   return rp_check_launch("rp_gemm");
 }
 
