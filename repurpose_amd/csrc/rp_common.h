@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <type_traits>
 
 #include "../../include/rp_api.h"
@@ -37,6 +38,14 @@ int rp_check_launch(const char* what);
   } while (0)
 
 static inline bool rp_aligned16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
+
+// Output store cache policy of a kernel family (rp_st16): the environment variable var (A/B) or
+// dflt.  0 plain, 1 sc1 write-through, 2 nt.  Callers cache the answer.
+static inline int rp_store_policy_env(const char* var, int dflt) {
+  const char* e = getenv(var);
+  const int v = e ? atoi(e) : dflt;
+  return (v < 0 || v > 2) ? dflt : v;
+}
 
 // ----------------------------------------------------------------------------------------------
 // dropout hash: lowbias32-style finaliser over (seed, index).  keep <=> (h & 0xffff) >= thresh16
@@ -176,6 +185,34 @@ __device__ __forceinline__ void rp_dma16(const void* g, uint32_t lds) {
       : "=&s"(keep)
       : "s"(lds), "v"(g)
       : "memory");
+}
+
+// A 16-byte output store under a cache policy: 0 plain (the line stays dirty in the XCD's L2 and is
+// written back at the kernel-end release), 1 sc1 (write-through: the bytes go on to HBM while the
+// epilogue runs), 2 nt (streaming).  The asm store ends in s_nop 1 so its data registers are read
+// before the next instruction can overwrite them.
+typedef uint32_t rp_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void rp_st16(void* p, uint4 v, int pol) {
+  const rp_u32x4 w = {v.x, v.y, v.z, v.w};
+  if (pol == 1)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+  else if (pol == 2)
+    __builtin_nontemporal_store(w, reinterpret_cast<rp_u32x4*>(p));
+  else
+    *reinterpret_cast<rp_u32x4*>(p) = w;
+}
+__device__ __forceinline__ void rp_st16(void* p, float4 v, int pol) {
+  rp_st16(p, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)), pol);
+}
+
+// A 16-byte fp32 load under a cache policy: 2 nt (streaming: the line is not kept), else plain
+typedef float rp_f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 rp_ld16f(const float* p, int pol) {
+  if (pol == 2) {
+    const rp_f32x4v w = __builtin_nontemporal_load(reinterpret_cast<const rp_f32x4v*>(p));
+    return make_float4(w.x, w.y, w.z, w.w);
+  }
+  return *reinterpret_cast<const float4*>(p);
 }
 
 __device__ __forceinline__ uint32_t rp_lds_addr(const void* p) {
