@@ -148,8 +148,8 @@ int rp_gemm_wgrad_grouped(int64_t K, const rp_wgrad_item* items, int n_items, in
  *                    (x, mean, rstd, gamma, dres -> dx fp32, dx_lp bf16 with dropout(lp_dropout_p,
  *                    lp_seed), gamma / beta partials per 32-row block as rp_layernorm_bwd writes them).
  *     dh itself is never written.  Replaces linear1 / in_proj dgrad followed by norm2 / norm1 backward.
- * Results are bitwise those of the unfused calls (same MFMA k order, same epilogue and LayerNorm
- * arithmetic).  M % 64 == 0, K % 64 == 0; one workgroup per 64 rows. */
+ * Without an exchange workspace (xchg below) results are bitwise those of the unfused calls (same MFMA
+ * k order, same epilogue and LayerNorm arithmetic).  M % 64 == 0, K % 64 == 0; one workgroup per 64 rows. */
 typedef struct rp_gemm_ln_args {
   const void* A;
   int64_t lda;
@@ -185,9 +185,17 @@ typedef struct rp_gemm_ln_args {
   float* dgamma_part; /* optional: [M/32][ld_part] */
   float* dbeta_part;
   int64_t ld_part;
+  /* optional: exchange workspace (rp_gemm_ln_xchg_bytes(M) bytes, 256-byte aligned, zero-filled before
+   * its first use; every launch leaves it zeroed, so one workspace serves the launches of a stream).
+   * With it and M % 128 == 0 the seam runs on 128 x 128 GEMM tiles (two workgroups per CU) whose four
+   * column tiles per 128-row block exchange the per-row LayerNorm statistics through it; x_out is then
+   * still bitwise the unfused GEMM's, h_out / mean / rstd / dx / dx_lp / the partials agree with the
+   * unfused LayerNorm to fp32 rounding of the row sums.  Null: the 64-row full-row kernels above. */
+  void* xchg;
 } rp_gemm_ln_args;
 int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* a, void* stream);
 int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* a, void* stream);
+int64_t rp_gemm_ln_xchg_bytes(int64_t M);
 
 /* ---------------------------------------------------------------------------------------- */
 /* LayerNorm over the last dim D (<= 4096, multiple of 4), one row per wavefront.

@@ -471,12 +471,22 @@ class _Schedule:
         # graph capture (graph.py): the model's device seed word, passed to every dropout launch
         self.sb = model._seed_base
         self.saved = None
-        # bf16 at d_model 512: GEMM + LayerNorm seams as single launches (rp_gemm_ln_*), opt-in with
-        # RP_GEMM_LN=1: bitwise the unfused pairs, but the 64 x 512 full-row tile streams the whole weight
-        # through every CU's LDS, and at one workgroup per CU that measured +0.17 ms per step at the bench
-        # shape (interleaved A/B) — the 128 x 128 GEMM + separate LayerNorm stays the default
-        self.fused_ln = (self.dt == torch.bfloat16 and self.M % 64 == 0 and model.d_model == 512
-                         and os.environ.get("RP_GEMM_LN", "0") == "1")
+        # bf16 at d_model 512: GEMM + LayerNorm seams as single launches (rp_gemm_ln_*).  On 128 x 128 tiles
+        # whose four column tiles exchange the row statistics (kernels._lnx_ws) when M % 128 == 0, else
+        # the 64 x 512 full-row kernels (bitwise the unfused pairs, but streaming the whole weight per 64
+        # rows at one workgroup per CU: +0.17 ms per step at the bench shape).  RP_GEMM_LN: auto (default:
+        # the exchange kernels where their grid fills every CU twice — bench shape 14.93 -> 14.39 ms per
+        # step; smaller grids keep the unfused pairs on 64 / 32-row GEMM tiles),
+        # 1 both directions, fwd / bwd one, 0 none
+        ln = os.environ.get("RP_GEMM_LN", "auto")
+        ok = self.dt == torch.bfloat16 and self.M % 64 == 0 and model.d_model == 512
+        if ln == "auto":
+            dev = model._flat.device
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
+            ln = "1" if (self.M % 128 == 0 and cus > 0 and (self.M // 128) * 4 >= 2 * cus
+                         and os.environ.get("RP_GEMM_LNX", "1") == "1") else "0"
+        self.fused_ln_fwd = ok and ln in ("1", "fwd")
+        self.fused_ln = ok and ln in ("1", "bwd")
 
     # ---- parameter access ----
     def P(self, name):  # fp32 master tensor
@@ -525,7 +535,7 @@ class _Schedule:
         layers = []
         # bf16 at d_model 512: every "Linear + residual -> LayerNorm" seam is one rp_gemm_ln_fwd launch
         # (out_proj -> norm2, linear2 -> the next norm1 / encoder_norm), bitwise the unfused pair
-        fused = self.fused_ln
+        fused = self.fused_ln_fwd
         _, h1, mu1, rs1 = K.layernorm_fwd(x, self.P("multimodal_encoder.layers.0.norm1.weight"),
                                           self.P("multimodal_encoder.layers.0.norm1.bias"),
                                           out_f32=False, lp_dtype=dt, save_stats=save)

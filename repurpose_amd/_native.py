@@ -58,7 +58,8 @@ class GemmLnArgs(ctypes.Structure):
                 ("ldx_out", c_i64), ("gamma", c_vp), ("beta", c_vp), ("eps", c_f), ("h_out", c_vp), ("ldh", c_i64),
                 ("mean", c_vp), ("rstd", c_vp), ("x", c_vp), ("ldx", c_i64), ("dres", c_vp), ("lddres", c_i64),
                 ("dx", c_vp), ("lddx", c_i64), ("dx_lp", c_vp), ("lddx_lp", c_i64), ("lp_dropout_p", c_f),
-                ("lp_seed", c_u32), ("dgamma_part", c_vp), ("dbeta_part", c_vp), ("ld_part", c_i64)]
+                ("lp_seed", c_u32), ("dgamma_part", c_vp), ("dbeta_part", c_vp), ("ld_part", c_i64),
+                ("xchg", c_vp)]
 
 
 class WgradItem(ctypes.Structure):
@@ -96,6 +97,7 @@ _SIGNATURES = {
     "rp_gemm_wgrad_grouped": (c_i, [c_i64, c_vp, c_i, c_i, c_vp]),
     "rp_gemm_ln_fwd": (c_i, [c_i64, c_i64, ctypes.POINTER(GemmLnArgs), c_vp]),
     "rp_gemm_ln_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(GemmLnArgs), c_vp]),
+    "rp_gemm_ln_xchg_bytes": (c_i64, [c_i64]),
     "rp_layernorm_fwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnFwdArgs), c_vp]),
     "rp_layernorm_bwd_blocks": (c_i64, [c_i64]),
     "rp_layernorm_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnBwdArgs), c_vp]),

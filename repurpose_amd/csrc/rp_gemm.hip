@@ -2044,6 +2044,335 @@ __global__ __launch_bounds__(GL_NT, 1) void gemm_ln_bwd_kernel(int64_t M, int64_
     __syncthreads();
   }
 }
+
+// ======= GEMM + LayerNorm on 128 x 128 tiles: row statistics exchanged between the column tiles =======
+// The 64 x 512 full-row kernels above keep a row in one workgroup but stream the whole weight per 64 rows
+// at one workgroup per CU.  These keep the 128 x 128 LDS-DMA GEMM (dma_mainloop, two workgroups per CU),
+// and the four column tiles of a 128-row block trade per-row partial statistics through a small global
+// workspace (rp_gemm_ln_xchg_bytes):
+//   fwd: per row (sum, M2 about the tile's own mean) of x_out over the tile's 128 columns, combined as a
+//        parallel variance: mean = sum / 512, M2 = sum_k M2_k + 128 (mean_k - mean)^2, var = M2 / 512;
+//   bwd: per row (sum g gamma, sum g gamma xhat) over the tile's columns (ln_bwd_kernel's s1, s2).
+// Protocol (cdna_hip_programming.md §6 Guideline 16, recipe R1): the payload stored write-through (sc1)
+// and drained by every storing wave, a barrier, one relaxed agent-scope arrive add per workgroup, one
+// polling lane (relaxed agent-scope loads + s_sleep, bounded: a wait that gives up sets the error word),
+// a barrier; the partners' payload read back with sc1 loads only.  The last of the four to finish
+// reading resets the row block's counters, so each launch starts from and leaves a zeroed workspace.
+// The four column tiles of a row block are consecutive logical tiles (blockIdx b, b + 8, b + 16, b + 24
+// after the XCD remap), dispatched in order, so the partners of a waiting workgroup are always
+// dispatched.  x_out is bitwise the unfused GEMM's; h / mean / rstd / dx agree with the unfused
+// LayerNorm to fp32 rounding of the row sums (associated per column tile, not per lane).
+constexpr int LX_TN = GL_N / BN;  // column tiles of a 512-wide row
+// Workspace: a 256-byte error word, then one record per row block (its layout independent of M, so
+// launches of any row counts can share the workspace): arrive / done counters, 248 bytes of padding,
+// then the [LX_TN][128] per-row partial pairs.
+constexpr int64_t LX_REC = 256 + LX_TN * BM * 8;
+struct LnxWs {
+  uint32_t* err;  // 1 when a wait gave up (never in a correct launch)
+  char* rec;      // row block rb's record at rec + rb * LX_REC
+  __device__ uint32_t* cnt(int rb) const { return (uint32_t*)(rec + rb * LX_REC); }
+  __device__ f32x2* part(int rb) const { return (f32x2*)(rec + rb * LX_REC + 256); }
+};
+
+__device__ __forceinline__ void lx_store_sc1(f32x2* p, f32x2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+// the row's pair from each of the row block's column tiles (sc1 loads, one wait)
+__device__ __forceinline__ void lx_load_sc1(const f32x2* base, f32x2 (&o)[LX_TN]) {
+  static_assert(LX_TN == 4, "four column tiles");
+  asm volatile(
+      "global_load_dwordx2 %0, %4, off sc1\n\t"
+      "global_load_dwordx2 %1, %5, off sc1\n\t"
+      "global_load_dwordx2 %2, %6, off sc1\n\t"
+      "global_load_dwordx2 %3, %7, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3])
+      : "v"(base), "v"(base + BM), "v"(base + 2 * BM), "v"(base + 3 * BM)
+      : "memory");
+}
+
+// every thread, after its payload stores: drain them, arrive, wait for the row block's column tiles
+__device__ __forceinline__ void lx_drain_arrive(const LnxWs& ws, int rb, int tid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_fetch_add(ws.cnt(rb), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lx_wait(const LnxWs& ws, int rb, int tid) {
+  if (tid == 0) {
+    uint32_t n = 0;
+    while (__hip_atomic_load(ws.cnt(rb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)LX_TN) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++n > (1u << 24)) {
+        __hip_atomic_store(ws.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+// after a barrier that follows every thread's partner reads: the last of the four resets the counters
+__device__ __forceinline__ void lx_done(const LnxWs& ws, int rb, int tid) {
+  if (tid == 0) {
+    uint32_t* c = ws.cnt(rb);
+    if (__hip_atomic_fetch_add(c + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(LX_TN - 1)) {
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__device__ __forceinline__ void lx_stage(const f32x4 (&acc)[4][4], float* cs, int lane, int wm, int wn) {
+  const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[(wm * 64 + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
+}
+
+constexpr int LX_CPR = BN / 4;             // float4 chunks per tile row
+constexpr int LX_IT = BM * LX_CPR / NT;    // chunks per thread (16): row = tid / 32 + 8 it
+constexpr int LX_LDS = CTILE_BYTES + 2 * BM * 4;
+static_assert(DmaCfg<0>::LDS <= CTILE_BYTES, "main loop fits the staging area");
+
+__global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws) {
+  __shared__ __attribute__((aligned(16))) char lds[LX_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int t = rp_xcd_remap(blockIdx.x, (int)gridDim.x);
+  const int rb = t / LX_TN, nt = t % LX_TN;
+  const int64_t m0 = (int64_t)rb * BM, n0 = (int64_t)nt * BN;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[8];
+  dma_mainloop<true, true, 0, 4>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane, wid,
+                                 wm, wn);
+  const int cc = (tid % LX_CPR) * 4;
+  float4 r[LX_IT];
+#pragma unroll
+  for (int it = 0; it < LX_IT; ++it)
+    r[it] = rp_ld16f(a.residual + (m0 + tid / LX_CPR + it * (NT / LX_CPR)) * a.ldr + n0 + cc, 2);
+  float* cs = reinterpret_cast<float*>(lds);
+  float* st = cs + BM * CST;  // per-row mean, rstd
+  lx_stage(acc, cs, lane, wm, wn);
+  __syncthreads();
+  // x_out = dropout(acc + bias) + residual: gemm_epilogue's RESB arithmetic, op for op
+  const float4 bi = *reinterpret_cast<const float4*>(a.bias + n0 + cc);
+  const uint32_t dseed = a.drop_thresh ? rp_seed_eff(a.seed_base, a.drop_seed) : 0u;
+#pragma unroll
+  for (int it = 0; it < LX_IT; ++it) {
+    const int row = tid / LX_CPR + it * (NT / LX_CPR);
+    const int64_t m = m0 + row, n = n0 + cc;
+    float* c = cs + row * CST + cc;
+    const float4 v = *reinterpret_cast<const float4*>(c);
+    float e4[4] = {v.x * 1.f + bi.x, v.y * 1.f + bi.y, v.z * 1.f + bi.z, v.w * 1.f + bi.w};
+    if (a.drop_thresh) {
+      const uint32_t kb = rp_keep_bits<4>(dseed, (uint32_t)(m * GL_N + n), a.drop_thresh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) e4[e] = ((kb >> e) & 1u) ? e4[e] * a.drop_scale : 0.f;
+    }
+    e4[0] += r[it].x; e4[1] += r[it].y; e4[2] += r[it].z; e4[3] += r[it].w;
+    const float4 o = make_float4(e4[0], e4[1], e4[2], e4[3]);
+    rp_st16(a.xo + m * a.ldxo + n, o, 2);
+    *reinterpret_cast<float4*>(c) = o;
+  }
+  __syncthreads();
+  // the tile's per-row (sum, M2): two threads per row, 64 columns each
+  const int row = tid >> 1, hf = tid & 1;
+  {
+    const float* rr = cs + row * CST + hf * 64;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float4 q = *reinterpret_cast<const float4*>(rr + 4 * j);
+      s += (q.x + q.y) + (q.z + q.w);
+    }
+    s += __shfl_xor(s, 1, 64);
+    const float mk = s * (1.f / BN);
+    float q2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float4 q = *reinterpret_cast<const float4*>(rr + 4 * j);
+      const float d0 = q.x - mk, d1 = q.y - mk, d2 = q.z - mk, d3 = q.w - mk;
+      q2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    }
+    q2 += __shfl_xor(q2, 1, 64);
+    if (hf == 0) lx_store_sc1(ws.part(rb) + nt * BM + row, f32x2{s, q2});
+  }
+  lx_drain_arrive(ws, rb, tid);
+  lx_wait(ws, rb, tid);
+  if (hf == 0) {
+    f32x2 o[LX_TN];
+    lx_load_sc1(ws.part(rb) + row, o);
+    const float mean = ((o[0].x + o[1].x) + (o[2].x + o[3].x)) * (1.f / GL_N);
+    float m2 = (o[0].y + o[1].y) + (o[2].y + o[3].y);
+#pragma unroll
+    for (int k = 0; k < LX_TN; ++k) {
+      const float d = o[k].x * (1.f / BN) - mean;
+      m2 += (float)BN * d * d;
+    }
+    st[row] = mean;
+    st[BM + row] = rsqrtf(m2 * (1.f / GL_N) + a.eps);
+  }
+  __syncthreads();
+  lx_done(ws, rb, tid);
+  // h = LayerNorm(x_out): ln_fwd_kernel's (v - mean) * rstd * gamma + beta, 8 columns per thread
+  const int c8 = (tid % (BN / 8)) * 8;
+  float gm[8], bt[8];
+  ld8(gm, a.gamma + n0 + c8);
+  ld8(bt, a.beta + n0 + c8);
+#pragma unroll 2
+  for (int it = 0; it < BM * (BN / 8) / NT; ++it) {
+    const int rw = tid / (BN / 8) + it * (NT / (BN / 8));
+    float v[8];
+    ld8(v, cs + rw * CST + c8);
+    const float mean = st[rw], rstd = st[BM + rw];
+    float y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) y[i] = (v[i] - mean) * rstd * gm[i] + bt[i];
+    st8bf(a.h + (m0 + rw) * a.ldh + n0 + c8, y);
+  }
+  if (nt == 0 && tid < BM) {
+    a.mean[m0 + tid] = st[tid];
+    a.rstd[m0 + tid] = st[BM + tid];
+  }
+}
+
+__global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws) {
+  __shared__ __attribute__((aligned(16))) char lds[LX_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int t = rp_xcd_remap(blockIdx.x, (int)gridDim.x);
+  const int rb = t / LX_TN, nt = t % LX_TN;
+  const int64_t m0 = (int64_t)rb * BM, n0 = (int64_t)nt * BN;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[8];
+  dma_mainloop<true, false, 0, 4>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane,
+                                  wid, wm, wn);
+  const int cc = (tid % LX_CPR) * 4, r0 = tid / LX_CPR;
+  float4 xh[LX_IT];  // x, then xhat
+#pragma unroll
+  for (int it = 0; it < LX_IT; ++it)
+    xh[it] = rp_ld16f(a.x + (m0 + r0 + it * (NT / LX_CPR)) * a.ldx + n0 + cc, 2);
+  float* cs = reinterpret_cast<float*>(lds);
+  float* st = cs + BM * CST;  // per-row s1 / 512, s2 / 512
+  lx_stage(acc, cs, lane, wm, wn);
+  __syncthreads();
+  const float4 gm = *reinterpret_cast<const float4*>(a.gamma + n0 + cc);
+  const float gam[4] = {gm.x, gm.y, gm.z, gm.w};
+  float pg[4][4], pb[4][4];  // gamma / beta partials per 32-row block and column
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pg[b][e] = pb[b][e] = 0.f;
+  f32x2* slot = ws.part(rb) + nt * BM;
+#pragma unroll
+  for (int it = 0; it < LX_IT; ++it) {
+    const int row = r0 + it * (NT / LX_CPR);
+    const int64_t m = m0 + row;
+    const float mu = a.mean[m], rs = a.rstd[m];
+    const float4 g4 = *reinterpret_cast<const float4*>(cs + row * CST + cc);
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+    float x[4] = {xh[it].x, xh[it].y, xh[it].z, xh[it].w};
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[e] = (x[e] - mu) * rs;
+      const float gg = g[e] * gam[e];
+      s1 += gg;
+      s2 += gg * x[e];
+      pg[it >> 2][e] += g[e] * x[e];
+      pb[it >> 2][e] += g[e];
+    }
+    xh[it] = make_float4(x[0], x[1], x[2], x[3]);
+#pragma unroll
+    for (int o = 1; o < LX_CPR; o <<= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    if ((tid % LX_CPR) == 0) lx_store_sc1(slot + row, f32x2{s1, s2});
+  }
+  lx_drain_arrive(ws, rb, tid);
+  float4 dr[LX_IT];  // the residual gradient, in flight while the row block gathers
+  if (a.dres) {
+#pragma unroll
+    for (int it = 0; it < LX_IT; ++it)
+      dr[it] = rp_ld16f(a.dres + (m0 + r0 + it * (NT / LX_CPR)) * a.lddres + n0 + cc, 2);
+  }
+  lx_wait(ws, rb, tid);
+  if (tid < BM) {
+    f32x2 o[LX_TN];
+    lx_load_sc1(ws.part(rb) + tid, o);
+    st[tid] = ((o[0].x + o[1].x) + (o[2].x + o[3].x)) * (1.f / GL_N);
+    st[BM + tid] = ((o[0].y + o[1].y) + (o[2].y + o[3].y)) * (1.f / GL_N);
+  }
+  __syncthreads();
+  lx_done(ws, rb, tid);
+  const uint32_t lseed = a.lp_thresh ? rp_seed_eff(a.seed_base, a.lp_seed) : 0u;
+#pragma unroll
+  for (int it = 0; it < LX_IT; ++it) {
+    const int row = r0 + it * (NT / LX_CPR);
+    const int64_t m = m0 + row, n = n0 + cc;
+    const float rs = a.rstd[m], s1 = st[row], s2 = st[BM + row];
+    const float4 g4 = *reinterpret_cast<const float4*>(cs + row * CST + cc);
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w}, x[4] = {xh[it].x, xh[it].y, xh[it].z, xh[it].w};
+    float dx[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dx[e] = rs * (g[e] * gam[e] - s1 - x[e] * s2);
+    if (a.dres) {
+      dx[0] += dr[it].x; dx[1] += dr[it].y; dx[2] += dr[it].z; dx[3] += dr[it].w;
+    }
+    *reinterpret_cast<float4*>(a.dx + m * a.lddx + n) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+    if (a.dx_lp) {
+      if (a.lp_thresh) {
+        const uint32_t kb = rp_keep_bits<4>(lseed, (uint32_t)(m * GL_N + n), a.lp_thresh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dx[e] = ((kb >> e) & 1u) ? dx[e] * a.lp_scale : 0.f;
+      }
+      bf16x4 q;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q[e] = (bf16)dx[e];
+      *reinterpret_cast<bf16x4*>(a.dx_lp + m * a.lddx_lp + n) = q;
+    }
+  }
+  // gamma / beta partials per 32-row block: the 8 threads of a column chunk (rows r0 + 8 it) summed in LDS
+  if (a.dgamma_part || a.dbeta_part) {
+    __syncthreads();  // every read of the staged tile is done
+    float* red = cs;   // [2][4 blocks][8 row groups][128 columns]
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[((0 * 4 + b) * 8 + r0) * BN + cc + e] = pg[b][e];
+        red[((1 * 4 + b) * 8 + r0) * BN + cc + e] = pb[b][e];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int id = tid + k * NT, b = id / BN, c = id % BN;  // (block, column): 512 per tile
+      float sg = 0.f, sb = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        sg += red[((0 * 4 + b) * 8 + q) * BN + c];
+        sb += red[((1 * 4 + b) * 8 + q) * BN + c];
+      }
+      const int64_t pr = m0 / 32 + b;
+      if (a.dgamma_part) a.dgamma_part[pr * a.ld_part + n0 + c] = sg;
+      if (a.dbeta_part) a.dbeta_part[pr * a.ld_part + n0 + c] = sb;
+    }
+  }
+}
 }  // namespace
 
 extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, int a_kmajor,
@@ -2236,6 +2565,12 @@ extern "C" int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const v
 }
 
 // ---- GEMM + LayerNorm entry points (include/rp_api.h) ----
+// exchange workspace of the 128 x 128 GEMM + LayerNorm kernels: error word, counters, partial pairs
+extern "C" int64_t rp_gemm_ln_xchg_bytes(int64_t M) {
+  return 256 + (M > 0 ? (M + BM - 1) / BM : 0) * LX_REC;
+}
+static LnxWs lnx_ws(void* base, int64_t) { return LnxWs{(uint32_t*)base, (char*)base + 256}; }
+
 static int gemm_ln_common(const char* fn, int64_t M, int64_t K, const rp_gemm_ln_args* p, GlnDev& d) {
   RP_REQUIRE(p, "%s: null args", fn);
   RP_REQUIRE(M >= 0 && K > 0 && M % GL_BM == 0 && K % GL_BK == 0, "%s: M must be a multiple of 64 and K of 64 (M=%lld K=%lld)",
@@ -2253,6 +2588,7 @@ static int gemm_ln_common(const char* fn, int64_t M, int64_t K, const rp_gemm_ln
   d.seed_base = p->seed_base;
   d.mean = p->mean; d.rstd = p->rstd;
   RP_REQUIRE(p->mean && p->rstd, "%s: null mean / rstd", fn);
+  RP_REQUIRE(!p->xchg || (((uintptr_t)p->xchg) & 255u) == 0, "%s: xchg must be 256-byte aligned", fn);
   return RP_OK;
 }
 
@@ -2272,6 +2608,11 @@ extern "C" int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   d.xo = p->x_out; d.ldxo = p->ldx_out;
   d.h = (bf16*)p->h_out; d.ldh = p->ldh;
   if (M == 0) return RP_OK;
+  if (p->xchg && M % BM == 0) {
+    hipLaunchKernelGGL(gemm_lnx_fwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
+                       lnx_ws(p->xchg, M));
+    return rp_check_launch("rp_gemm_ln_fwd");
+  }
   hipLaunchKernelGGL(gemm_ln_fwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
   return rp_check_launch("rp_gemm_ln_fwd");
 }
@@ -2297,6 +2638,11 @@ extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   d.lp_seed = p->lp_seed;
   d.dgamma_part = p->dgamma_part; d.dbeta_part = p->dbeta_part; d.ld_part = p->ld_part;
   if (M == 0) return RP_OK;
+  if (p->xchg && M % BM == 0) {
+    hipLaunchKernelGGL(gemm_lnx_bwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
+                       lnx_ws(p->xchg, M));
+    return rp_check_launch("rp_gemm_ln_bwd");
+  }
   hipLaunchKernelGGL(gemm_ln_bwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
   return rp_check_launch("rp_gemm_ln_bwd");
 }

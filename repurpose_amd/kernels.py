@@ -201,11 +201,31 @@ def linear_wgrad_grouped(items, accumulate=True):
 
 
 # ----------------------------------------------------------------------- GEMM + LayerNorm seams
+_LNX = {}
+
+
+def _lnx_ws(dev, M):
+    """The exchange workspace of the 128 x 128 GEMM + LayerNorm kernels (rp_gemm_ln_xchg_bytes, zero-filled
+    once; every launch leaves it zeroed), one per (device, stream) — launches on one stream are ordered,
+    launches on two streams may overlap and must not share counters — grown as needed.  RP_GEMM_LNX=0
+    (A/B) or M % 128 != 0: None, i.e. the 64-row full-row kernels."""
+    if M % 128 or os.environ.get("RP_GEMM_LNX", "1") != "1":
+        return None
+    need = int(N.load().rp_gemm_ln_xchg_bytes(M))
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    ws = _LNX.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.zeros(need, device=dev, dtype=torch.uint8)
+        _LNX[key] = ws
+    return ws
+
+
 def linear_ln_fwd(x, W, b, residual, gamma, beta, eps=1e-5, dropout_p=0.0, seed=0, seed_base=None):
     """One launch (rp_gemm_ln_fwd) for ``y = dropout(x W^T + b) + residual`` (fp32, returned) and
-    ``h = LayerNorm(y)`` (bf16) with its mean / rstd — bitwise linear_fwd(..., residual=...) followed by
-    layernorm_fwd(y, out_f32=False, lp_dtype=bf16).  x [M, K] bf16, W [512, K] bf16, M % 64 == 0.
-    Returns (y, h, mean, rstd)."""
+    ``h = LayerNorm(y)`` (bf16) with its mean / rstd — linear_fwd(..., residual=...) followed by
+    layernorm_fwd(y, out_f32=False, lp_dtype=bf16): y bitwise; h / mean / rstd bitwise on the 64-row
+    kernels, to fp32 rounding of the row sums on the 128 x 128 exchange kernels (M % 128 == 0, the
+    default; RP_GEMM_LNX=0 A/B).  x [M, K] bf16, W [512, K] bf16, M % 64 == 0.  Returns (y, h, mean, rstd)."""
     _gpu(x, W, b, residual, gamma, beta)
     _seed_word(seed_base)
     M, K = x.shape
@@ -218,7 +238,7 @@ def linear_ln_fwd(x, W, b, residual, gamma, beta, eps=1e-5, dropout_p=0.0, seed=
                      dropout_p=float(dropout_p), dropout_seed=int(seed) & 0xFFFFFFFF, seed_base=_p(seed_base).value,
                      residual=_p(residual).value, ldr=residual.stride(0), x_out=_p(y).value, ldx_out=512,
                      gamma=_p(gamma).value, beta=_p(beta).value, eps=float(eps), h_out=_p(h).value, ldh=512,
-                     mean=_p(mean).value, rstd=_p(rstd).value)
+                     mean=_p(mean).value, rstd=_p(rstd).value, xchg=_p(_lnx_ws(dev, M)).value)
     e0 = _tick("gemm_ln_fwd")
     N.call("rp_gemm_ln_fwd", M, K, ctypes.byref(a), _stream(x))
     _tock(e0, 2.0 * M * 512 * K)
@@ -228,8 +248,9 @@ def linear_ln_fwd(x, W, b, residual, gamma, beta, eps=1e-5, dropout_p=0.0, seed=
 def linear_ln_bwd(dy, W, x, mean, rstd, gamma, dres=None, lp_dtype=None, lp_dropout_p=0.0, lp_seed=0, dgamma=None,
                   dbeta=None, defer=None, ws=None, seed_base=None):
     """One launch (rp_gemm_ln_bwd) for ``dh = dy W`` (dy [M, K] bf16, W [K, 512] bf16) followed by the
-    LayerNorm backward of the LayerNorm whose input was x — bitwise linear_dgrad(dy, W, fp32) then
-    layernorm_bwd(dh, x, mean, rstd, gamma, dres=..., lp_dtype=..., ...); dh is never written.
+    LayerNorm backward of the LayerNorm whose input was x — linear_dgrad(dy, W, fp32) then
+    layernorm_bwd(dh, x, mean, rstd, gamma, dres=..., lp_dtype=..., ...), bitwise on the 64-row kernels and
+    to fp32 rounding of the row sums on the exchange kernels (as linear_ln_fwd); dh is never written.
     Returns (dx fp32, dx_lp or None); gamma / beta partials as layernorm_bwd (``defer`` / ``ws``)."""
     _gpu(dy, W, x, mean, rstd, gamma, dres)
     _seed_word(seed_base)
@@ -254,7 +275,7 @@ def linear_ln_bwd(dy, W, x, mean, rstd, gamma, dres=None, lp_dtype=None, lp_drop
                      ldx=x.stride(0), dres=_p(dres).value, lddres=dres.stride(0) if dres is not None else 0,
                      dx=_p(dx).value, lddx=D, dx_lp=_p(dxl).value, lddx_lp=D, lp_dropout_p=float(lp_dropout_p),
                      lp_seed=int(lp_seed) & 0xFFFFFFFF, dgamma_part=_p(pg).value, dbeta_part=_p(pb).value,
-                     ld_part=ld_part)
+                     ld_part=ld_part, xchg=_p(_lnx_ws(dev, M)).value)
     e0 = _tick("gemm_ln_bwd")
     N.call("rp_gemm_ln_bwd", M, K, ctypes.byref(a), _stream(dy))
     _tock(e0, 2.0 * M * 512 * K)
