@@ -1032,6 +1032,9 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 2, wn = wid & 3;
+#ifdef RP_GEMM_PROBE
+  const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -1199,8 +1202,21 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
   }
   if (wm == 0) rp_raw_barrier();  // match the lagging half's barrier count
   __syncthreads();
+#ifdef RP_GEMM_PROBE
+  const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
   gemm8_epilogue<TC, MODE, BNT, GATEB>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
   if (pf) asm volatile("" ::"v"(pfd[0]), "v"(pfd[1]));
+#ifdef RP_GEMM_PROBE
+  {  // tuning build only: per-workgroup phase stamps (start, main loop done, epilogue issued, drained)
+    const uint64_t ts2 = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t ts3 = __builtin_amdgcn_s_memrealtime();
+    const int bid = blockIdx.x + blockIdx.y * gridDim.x;
+    if (tid < 4 && bid < RP_PROBE_MAX)
+      g_gemm_probe[bid * 4 + tid] = tid == 0 ? ts0 : tid == 1 ? ts1 : tid == 2 ? ts2 : ts3;
+  }
+#endif
   if (want_bias) {
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);
