@@ -861,11 +861,13 @@ struct G8 {
   static constexpr int WN = BNT / 4;                  // output columns per wave
   static constexpr int JT = WN / 16;                  // MFMA column tiles per wave
   static constexpr int CST = BNT + 4;                 // fp32 row stride of an epilogue pass
-  static constexpr int EPI = 64 * CST * 4;            // one 64-row epilogue pass
+  static constexpr int PR = 128;                      // rows per epilogue pass (one wave row half)
+  static constexpr int EPI = PR * CST * 4;            // one epilogue pass
   static constexpr int LDS = S * SLOT > EPI ? S * SLOT : EPI;
 };
 
-// epilogue: four passes of 64 rows staged as fp32 in LDS, then 16-byte row chunks per thread.
+// epilogue: two passes of 128 rows (one wave row half each) staged as fp32 in LDS, then 16-byte row
+// chunks per thread (four 64-row passes before round 5: twice the barriers, half the stores in flight).
 // GATEB (bf16 C, bf16 gate: the linear2 dgrad): a pass's gate chunks are loaded before its stores
 // (16 bytes per chunk; inline, each waited behind the previous chunk's store, as the residual did in
 // the 128 x 128 epilogue)
@@ -881,20 +883,22 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
   TC* Cbase = Cout + (MODE == 1 ? (int64_t)split * M * ldc : 0);
   const uint32_t dseed = (MODE == 0 && ep.drop_thresh) ? rp_seed_eff(ep.seed_base, ep.drop_seed) : 0u;
   const int g = lane >> 4, cl = lane & 15;
+  constexpr int PPW = G::PR / 64;  // 64-row accumulator groups of a wave per pass
 #pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {
+  for (int pass = 0; pass < 256 / G::PR; ++pass) {
     if (pass) __syncthreads();
-    if (wm == (pass >> 1)) {
+    if (wm == pass * G::PR / 128) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4 * PPW; ++i)
 #pragma unroll
         for (int j = 0; j < G::JT; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            cs[(i * 16 + g * 4 + r) * G::CST + wn * G::WN + j * 16 + cl] = acc[(pass & 1) * 4 + i][j][r];
+            cs[(i * 16 + g * 4 + r) * G::CST + wn * G::WN + j * 16 + cl] =
+                acc[((pass * G::PR / 64) & 1) * 4 + i][j][r];
     }
     __syncthreads();
-    constexpr int ITER = 64 * CPRO / NT8;
+    constexpr int ITER = G::PR * CPRO / NT8;
     // fp32 C with a residual (the 256 x 128 tile's linear2 forward): the pass's residual chunks are
     // loaded before its first store (inline, each load would wait behind the previous chunk's store)
     constexpr bool RESV = std::is_same<TC, float>::value && MODE == 0;
@@ -904,7 +908,7 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
 #pragma unroll
         for (int it = 0; it < ITER; ++it) {
           const int id = tid + it * NT8;
-          const int64_t m = m0 + pass * 64 + id / CPRO, n = n0 + (id % CPRO) * OV;
+          const int64_t m = m0 + pass * G::PR + id / CPRO, n = n0 + (id % CPRO) * OV;
           rv[it] = (m < M && n < N) ? rp_ld16f(ep.residual + m * ep.ldr + n, ep.ld_pol)
                                     : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -916,7 +920,7 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
 #pragma unroll
       for (int it = 0; it < ITER; ++it) {
         const int id = tid + it * NT8;
-        const int64_t m = m0 + pass * 64 + id / CPRO, n = n0 + (id % CPRO) * OV;
+        const int64_t m = m0 + pass * G::PR + id / CPRO, n = n0 + (id % CPRO) * OV;
         if (m < M && n < N) gv[it] = *reinterpret_cast<const bf16x8*>((const bf16*)ep.gate + m * ep.ldg + n);
       }
     }
@@ -924,7 +928,7 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
     for (int it = 0; it < ITER; ++it) {
       const int id = tid + it * NT8;
       const int row = id / CPRO, cc = (id % CPRO) * OV;
-      const int64_t m = m0 + pass * 64 + row, n = n0 + cc;
+      const int64_t m = m0 + pass * G::PR + row, n = n0 + cc;
       if (m >= M || n >= N) continue;
       float v[OV];
 #pragma unroll
