@@ -840,6 +840,26 @@ def test_gemm8_dgrad_gate_prefetch_repeat_bitwise(dev, Kr):
             assert torch.equal(first, got)
 
 
+def test_gemm8_forward_dropout_bits(dev, monkeypatch):
+    """The 256-row kernel's bf16 forward with ReLU + element dropout (the encoder's linear1 at the bench
+    shape) drops exactly the elements the 128 x 128 kernel drops (the stream is a function of the element index; bias large enough that ReLU clips nothing),
+    keeps the rest within bf16 rounding of each other, and repeats bitwise."""
+    M, Nout, Kd = 16384, 2048, 512
+    x = rnd(M, Kd, dev=dev, seed=31).to(torch.bfloat16)
+    w = rnd(Nout, Kd, dev=dev, seed=32, scale=0.02).to(torch.bfloat16)
+    b = torch.full((Nout,), 8.0, device=dev)
+    y8 = K.linear_fwd(x, w, b, relu=True, dropout_p=0.1, seed=1234)
+    y8b = K.linear_fwd(x, w, b, relu=True, dropout_p=0.1, seed=1234)
+    monkeypatch.setenv("RP_GEMM8", "0")
+    y1 = K.linear_fwd(x, w, b, relu=True, dropout_p=0.1, seed=1234)
+    torch.cuda.synchronize()
+    assert torch.equal(y8, y8b)
+    assert torch.equal(y8 == 0, y1 == 0)
+    frac = (y8 == 0).float().mean().item()
+    assert abs(frac - 0.1) < 0.002, frac
+    close(y8.float(), y1.double(), atol=0.1, rtol=1e-2, what="gemm8 vs 128-tile dropout forward")
+
+
 @pytest.mark.parametrize("B,T,p", [(8, 2048, 0.1), (2, 384, 0.0)])
 def test_attn_dout_delta_fused_bitwise(dev, B, T, p):
     """rp_gemm_attn_dout_delta (the out_proj dgrad with the attention delta pre-pass in its epilogue)
