@@ -5,7 +5,8 @@
   device), each runs the eager DP step with the bucketed all-reduce; one JSON line, ``n_gpus`` and
   ``ranks_seen`` 2, a finite loss and bitwise identical parameters on both ranks after the last step;
 * the all-reduce buckets of every weight-gradient schedule the DP backward can take (the default
-  256 + 512 tile cut of the grouped launch, ``RP_WGRAD_GROUP_LAYERS`` cuts, per-layer split-K, fp32)
+  cuts of the grouped launch at each full round of tiles, ``RP_WGRAD_GROUP_LAYERS`` cuts, per-layer
+  split-K, fp32)
   tile ``[0, trainable_numel)`` exactly once, in reverse layout order;
 * the captured DP step (``CapturedTrainStep(capture_collectives=True)``: RCCL all-reduces captured into
   the HIP graph, tile cut active, backward writing the gradients) on a one-rank RCCL group gives bitwise
