@@ -669,6 +669,10 @@ constexpr int dma_tile_lds() {
 #ifdef RP_GEMM_PROBE
 constexpr int RP_PROBE_MAX = 8192;
 __device__ uint64_t g_gemm_probe[RP_PROBE_MAX * 4];
+__device__ uint64_t g_lnx_probe[RP_PROBE_MAX * 8];  // exchange kernels: 6 stamps per workgroup
+#define LX_STAMP(i) if (tid == 0 && blockIdx.x < RP_PROBE_MAX) g_lnx_probe[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define LX_STAMP(i)
 #endif
 
 template <bool AK, bool BKM, typename TC, int MODE, int CFG, bool RESB = false, int MI = 4>
@@ -2157,7 +2161,102 @@ constexpr int LX_IT = BM * LX_CPR / NT;    // chunks per thread (16): row = tid 
 constexpr int LX_LDS = CTILE_BYTES + 2 * BM * 4;
 static_assert(DmaCfg<0>::LDS <= CTILE_BYTES, "main loop fits the staging area");
 
-__global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws) {
+// glds_tile's fills issued through inline asm (rp_dma16): the compiler does not track them, so it adds
+// no vmcnt(0) ahead of the LDS reads, and loads the caller issues between fills stay in flight across
+// the loop's barriers; the caller orders every fill before its readers (counted vmcnt + barrier)
+template <bool KMAJ>
+__device__ __forceinline__ void glds_tile_u(const bf16* __restrict__ base, int64_t ld, int64_t rows_lim, int64_t row0,
+                                            int64_t k0, char* tile, int wid, int lane) {
+  constexpr int PER = BM * 64 * 2 / 1024 / (NT / 64);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int I = wid * PER + j;
+    const bf16* src;
+    if (KMAJ) {
+      const int r = I * 8 + (lane >> 3), lc = kswz(r, lane & 7);
+      int64_t rr = row0 + r;
+      if (rr >= rows_lim) rr = rows_lim - 1;
+      src = base + rr * ld + k0 + lc * 8;
+    } else {
+      const int k = I * 4 + (lane >> 4), lc = mswz(k, lane & 15);
+      int64_t cc = row0 + lc * 8;
+      if (cc >= rows_lim) cc = rows_lim - 8;
+      src = base + (k0 + k) * ld + cc;
+    }
+    rp_dma16(src, rp_lds_addr(tile + I * 1024));
+  }
+}
+
+// The 128 x 128 main loop of dma_mainloop (two 64-deep LDS stages, one barrier per K step, the same
+// MFMA order, so the same products bit for bit) with the fills untracked and a per-thread prefetch of
+// LX_IT 16-byte fp32 chunks of the epilogue's operand spread over the first K steps: LX_PF chunks
+// issued right after step kt's fill of stage kt + 1, waited for only one step later (the counted
+// vmcnt at the end of a step leaves exactly that step's prefetch in flight).  The lockstep grid keeps
+// HBM idle through the main loop, so these bytes leave the HBM-bound epilogue.
+constexpr int LX_PF = 2;                 // prefetch chunks per K step
+constexpr int LX_PFS = LX_IT / LX_PF;    // K steps that carry them (8)
+template <bool AK, bool BKM>
+__device__ __forceinline__ void lx_mainloop(const bf16* __restrict__ A, int64_t lda, int64_t M,
+                                            const bf16* __restrict__ B, int64_t ldb, int64_t m0, int64_t n0,
+                                            int64_t K, f32x4 (&acc)[4][4], char* lds, int lane, int wid, int wm,
+                                            int wn, const float* __restrict__ pf_base, int64_t pf_ld,
+                                            float4 (&pf)[LX_IT], int tid) {
+  constexpr int BK = 64, GT = BM * BK * 2, SG = 2 * GT;
+  const int nk = (int)(K / BK);
+  const float* pfp = pf_base + (m0 + tid / LX_CPR) * pf_ld + n0 + (tid % LX_CPR) * 4;
+  auto prefetch = [&](int c) { pf[c] = rp_ld16f(pfp + (int64_t)c * (NT / LX_CPR) * pf_ld, 2); };
+  auto fill = [&](int kt) {
+    char* buf = lds + (kt & 1) * SG;
+    glds_tile_u<AK>(A, lda, M, m0, (int64_t)kt * BK, buf, wid, lane);
+    glds_tile_u<BKM>(B, ldb, GL_N, n0, (int64_t)kt * BK, buf + GT, wid, lane);
+  };
+  auto compute = [&](int kt) {
+    const char* cur = lds + (kt & 1) * SG;
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 32) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[i] = AK ? frag_k_swz<BK>(cur, wm * 64 + i * 16, ks, lane) : frag_m_swz(cur, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[j] = BKM ? frag_k_swz<BK>(cur + GT, wn * 64 + j * 16, ks, lane) : frag_m_swz(cur + GT, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  // K >= 64 LX_PFS (the host's condition): every prefetch step is a main-loop step, straight-line code
+  fill(0);
+  rp_waitcnt<0, 15>();
+  rp_raw_barrier();
+  // steps that carry prefetch chunks: unrolled, so the chunk registers have compile-time indices
+#pragma unroll
+  for (int kt = 0; kt < LX_PFS; ++kt) {
+    if (kt + 1 < LX_PFS || nk > LX_PFS) fill(kt + 1);
+#pragma unroll
+    for (int c = 0; c < LX_PF; ++c) prefetch(kt * LX_PF + c);
+    compute(kt);
+    rp_waitcnt<LX_PF, 15>();  // stage kt + 1 has landed; this step's prefetch may stay in flight
+    rp_raw_barrier();
+  }
+  for (int kt = LX_PFS; kt < nk; ++kt) {
+    if (kt + 1 < nk) fill(kt + 1);
+    compute(kt);
+    rp_waitcnt<0, 15>();
+    rp_raw_barrier();
+  }
+}
+
+// RP_LNX_PF=0 (A/B): the exchange kernels on dma_mainloop, their epilogue operand loaded after it
+static int lnx_prefetch() {
+  static const int v = (getenv("RP_LNX_PF") && getenv("RP_LNX_PF")[0] == '0') ? 0 : 1;
+  return v;
+}
+
+__global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws,
+                                                             int pf) {
   __shared__ __attribute__((aligned(16))) char lds[LX_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2171,13 +2270,20 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc[8];
-  dma_mainloop<true, true, 0, 4>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane, wid,
-                                 wm, wn);
   const int cc = (tid % LX_CPR) * 4;
-  float4 r[LX_IT];
+  float4 r[LX_IT];  // the residual tile
+  LX_STAMP(0);
+  if (pf) {
+    lx_mainloop<true, true>(a.A, a.lda, M, a.W, a.ldw, m0, n0, K, acc, lds, lane, wid, wm, wn, a.residual, a.ldr, r,
+                            tid);
+  } else {
+    dma_mainloop<true, true, 0, 4>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane,
+                                   wid, wm, wn);
 #pragma unroll
-  for (int it = 0; it < LX_IT; ++it)
-    r[it] = rp_ld16f(a.residual + (m0 + tid / LX_CPR + it * (NT / LX_CPR)) * a.ldr + n0 + cc, 2);
+    for (int it = 0; it < LX_IT; ++it)
+      r[it] = rp_ld16f(a.residual + (m0 + tid / LX_CPR + it * (NT / LX_CPR)) * a.ldr + n0 + cc, 2);
+  }
+  LX_STAMP(1);
   float* cs = reinterpret_cast<float*>(lds);
   float* st = cs + BM * CST;  // per-row mean, rstd
   lx_stage(acc, cs, lane, wm, wn);
@@ -2225,8 +2331,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t 
     q2 += __shfl_xor(q2, 1, 64);
     if (hf == 0) lx_store_sc1(ws.part(rb) + nt * BM + row, f32x2{s, q2});
   }
+  LX_STAMP(2);
   lx_drain_arrive(ws, rb, tid);
+  LX_STAMP(3);
   lx_wait(ws, rb, tid);
+  LX_STAMP(4);
   if (hf == 0) {
     f32x2 o[LX_TN];
     lx_load_sc1(ws.part(rb) + row, o);
@@ -2262,9 +2371,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t 
     a.mean[m0 + tid] = st[tid];
     a.rstd[m0 + tid] = st[BM + tid];
   }
+#ifdef RP_GEMM_PROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  LX_STAMP(5);
+#endif
 }
 
-__global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws) {
+__global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws,
+                                                             int pf) {
   __shared__ __attribute__((aligned(16))) char lds[LX_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2278,13 +2392,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc[8];
-  dma_mainloop<true, false, 0, 4>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane,
-                                  wid, wm, wn);
   const int cc = (tid % LX_CPR) * 4, r0 = tid / LX_CPR;
   float4 xh[LX_IT];  // x, then xhat
+  LX_STAMP(0);
+  if (pf) {
+    lx_mainloop<true, false>(a.A, a.lda, M, a.W, a.ldw, m0, n0, K, acc, lds, lane, wid, wm, wn, a.x, a.ldx, xh, tid);
+  } else {
+    dma_mainloop<true, false, 0, 4>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane,
+                                    wid, wm, wn);
 #pragma unroll
-  for (int it = 0; it < LX_IT; ++it)
-    xh[it] = rp_ld16f(a.x + (m0 + r0 + it * (NT / LX_CPR)) * a.ldx + n0 + cc, 2);
+    for (int it = 0; it < LX_IT; ++it)
+      xh[it] = rp_ld16f(a.x + (m0 + r0 + it * (NT / LX_CPR)) * a.ldx + n0 + cc, 2);
+  }
+  LX_STAMP(1);
   float* cs = reinterpret_cast<float*>(lds);
   float* st = cs + BM * CST;  // per-row s1 / 512, s2 / 512
   lx_stage(acc, cs, lane, wm, wn);
@@ -2323,7 +2443,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
     }
     if ((tid % LX_CPR) == 0) lx_store_sc1(slot + row, f32x2{s1, s2});
   }
+  LX_STAMP(2);
   lx_drain_arrive(ws, rb, tid);
+  LX_STAMP(3);
   float4 dr[LX_IT];  // the residual gradient, in flight while the row block gathers
   if (a.dres) {
 #pragma unroll
@@ -2331,6 +2453,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
       dr[it] = rp_ld16f(a.dres + (m0 + r0 + it * (NT / LX_CPR)) * a.lddres + n0 + cc, 2);
   }
   lx_wait(ws, rb, tid);
+  LX_STAMP(4);
   if (tid < BM) {
     f32x2 o[LX_TN];
     lx_load_sc1(ws.part(rb) + tid, o);
@@ -2392,6 +2515,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
       if (a.dbeta_part) a.dbeta_part[pr * a.ld_part + n0 + c] = sb;
     }
   }
+#ifdef RP_GEMM_PROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  LX_STAMP(5);
+#endif
 }
 }  // namespace
 
@@ -2630,7 +2757,7 @@ extern "C" int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   if (M == 0) return RP_OK;
   if (p->xchg && M % BM == 0) {
     hipLaunchKernelGGL(gemm_lnx_fwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
-                       lnx_ws(p->xchg, M));
+                       lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * LX_PFS ? 1 : 0);
     return rp_check_launch("rp_gemm_ln_fwd");
   }
   hipLaunchKernelGGL(gemm_ln_fwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
@@ -2660,7 +2787,7 @@ extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   if (M == 0) return RP_OK;
   if (p->xchg && M % BM == 0) {
     hipLaunchKernelGGL(gemm_lnx_bwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
-                       lnx_ws(p->xchg, M));
+                       lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * LX_PFS ? 1 : 0);
     return rp_check_launch("rp_gemm_ln_bwd");
   }
   hipLaunchKernelGGL(gemm_ln_bwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
@@ -2668,6 +2795,10 @@ extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
 }
 
 #ifdef RP_GEMM_PROBE
+extern "C" int rp_debug_lnx_probe(uint64_t* host, int n) {
+  if (n > RP_PROBE_MAX * 8) n = RP_PROBE_MAX * 8;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lnx_probe), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
 extern "C" int rp_debug_gemm_probe(uint64_t* host, int n) {
   if (n > RP_PROBE_MAX * 4) n = RP_PROBE_MAX * 4;
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_probe), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
