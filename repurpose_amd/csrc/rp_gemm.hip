@@ -2158,7 +2158,7 @@ __device__ __forceinline__ void lx_stage(const f32x4 (&acc)[4][4], float* cs, in
 
 constexpr int LX_CPR = BN / 4;             // float4 chunks per tile row
 constexpr int LX_IT = BM * LX_CPR / NT;    // chunks per thread (16): row = tid / 32 + 8 it
-constexpr int LX_LDS = CTILE_BYTES + 2 * BM * 4;
+constexpr int LX_LDS = CTILE_BYTES + 4 * BM * 4;  // staged tile, per-row totals, (bwd) mean / rstd
 static_assert(DmaCfg<0>::LDS <= CTILE_BYTES, "main loop fits the staging area");
 
 // glds_tile's fills issued through inline asm (rp_dma16): the compiler does not track them, so it adds
@@ -2407,7 +2407,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
   LX_STAMP(1);
   float* cs = reinterpret_cast<float*>(lds);
   float* st = cs + BM * CST;  // per-row s1 / 512, s2 / 512
+  float* mr = st + 2 * BM;    // the tile rows' mean, rstd: loaded once, read by both passes
+  float mrv = 0.f;
+  if (tid < 2 * BM) mrv = tid < BM ? a.mean[m0 + tid] : a.rstd[m0 + tid - BM];
   lx_stage(acc, cs, lane, wm, wn);
+  if (tid < 2 * BM) mr[tid] = mrv;
   __syncthreads();
   const float4 gm = *reinterpret_cast<const float4*>(a.gamma + n0 + cc);
   const float gam[4] = {gm.x, gm.y, gm.z, gm.w};
@@ -2420,8 +2424,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
 #pragma unroll
   for (int it = 0; it < LX_IT; ++it) {
     const int row = r0 + it * (NT / LX_CPR);
-    const int64_t m = m0 + row;
-    const float mu = a.mean[m], rs = a.rstd[m];
+    const float mu = mr[row], rs = mr[BM + row];
     const float4 g4 = *reinterpret_cast<const float4*>(cs + row * CST + cc);
     const float g[4] = {g4.x, g4.y, g4.z, g4.w};
     float x[4] = {xh[it].x, xh[it].y, xh[it].z, xh[it].w};
@@ -2467,7 +2470,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
   for (int it = 0; it < LX_IT; ++it) {
     const int row = r0 + it * (NT / LX_CPR);
     const int64_t m = m0 + row, n = n0 + cc;
-    const float rs = a.rstd[m], s1 = st[row], s2 = st[BM + row];
+    const float rs = mr[BM + row], s1 = st[row], s2 = st[BM + row];
     const float4 g4 = *reinterpret_cast<const float4*>(cs + row * CST + cc);
     const float g[4] = {g4.x, g4.y, g4.z, g4.w}, x[4] = {xh[it].x, xh[it].y, xh[it].z, xh[it].w};
     float dx[4];
