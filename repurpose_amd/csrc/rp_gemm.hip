@@ -241,6 +241,19 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* l
   constexpr int CPRO = BN / OV;
   TC* Cbase = Cout + (MODE == 1 ? (int64_t)split * M * ldc : 0);
   const uint32_t dseed = (MODE == 0 && ep.drop_thresh) ? rp_seed_eff(ep.seed_base, ep.drop_seed) : 0u;
+  // a thread's output chunk column is the same in every pass and iteration (NT % CPRO == 0): its bias
+  // chunk is loaded once, not per chunk (the stores through C may alias it, so the compiler reloads)
+  static_assert(NT % CPRO == 0, "fixed chunk column per thread");
+  float bv[OV];
+#pragma unroll
+  for (int e = 0; e < OV; ++e) bv[e] = 0.f;
+  if (MODE == 0 && ep.bias && n0 + (tid % CPRO) * OV < N) {
+#pragma unroll
+    for (int e = 0; e < OV; e += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(ep.bias + n0 + (tid % CPRO) * OV + e);
+      bv[e] = q.x; bv[e + 1] = q.y; bv[e + 2] = q.z; bv[e + 3] = q.w;
+    }
+  }
   constexpr int NH = HALVES ? 2 : 1;  // staging passes
   constexpr int HR = MI * 32 / NH;     // rows per pass
 #pragma unroll 1
@@ -279,8 +292,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* l
       if (m >= M || n >= N) continue;
       float e4[4] = {v[it].x * alpha, v[it].y * alpha, v[it].z * alpha, v[it].w * alpha};
       if (ep.bias) {
-        const float4 q = *reinterpret_cast<const float4*>(ep.bias + n);
-        e4[0] += q.x; e4[1] += q.y; e4[2] += q.z; e4[3] += q.w;
+        e4[0] += bv[0]; e4[1] += bv[1]; e4[2] += bv[2]; e4[3] += bv[3];
       }
       if (n < ep.col_scale_n) {
 #pragma unroll
@@ -329,10 +341,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* l
     if (MODE == 0) {
       if (ep.bias) {
 #pragma unroll
-        for (int e = 0; e < OV; e += 4) {
-          float4 q = *reinterpret_cast<const float4*>(ep.bias + n + e);
-          v[e] += q.x; v[e + 1] += q.y; v[e + 2] += q.z; v[e + 3] += q.w;
-        }
+        for (int e = 0; e < OV; ++e) v[e] += bv[e];
       }
       if (n < ep.col_scale_n) {  // chunks never straddle col_scale_n (a multiple of 8)
 #pragma unroll
@@ -887,6 +896,18 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
   TC* Cbase = Cout + (MODE == 1 ? (int64_t)split * M * ldc : 0);
   const uint32_t dseed = (MODE == 0 && ep.drop_thresh) ? rp_seed_eff(ep.seed_base, ep.drop_seed) : 0u;
   const int g = lane >> 4, cl = lane & 15;
+  // the thread's chunk column is fixed (NT8 % CPRO == 0): its bias chunk loaded once (gemm_epilogue)
+  static_assert(NT8 % CPRO == 0, "fixed chunk column per thread");
+  float bv[OV];
+#pragma unroll
+  for (int e = 0; e < OV; ++e) bv[e] = 0.f;
+  if (MODE == 0 && ep.bias && n0 + (tid % CPRO) * OV < N) {
+#pragma unroll
+    for (int e = 0; e < OV; e += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(ep.bias + n0 + (tid % CPRO) * OV + e);
+      bv[e] = q.x; bv[e + 1] = q.y; bv[e + 2] = q.z; bv[e + 3] = q.w;
+    }
+  }
   constexpr int PPW = G::PR / 64;  // 64-row accumulator groups of a wave per pass
 #pragma unroll
   for (int pass = 0; pass < 256 / G::PR; ++pass) {
@@ -943,10 +964,7 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
       if (MODE == 0) {
         if (ep.bias) {
 #pragma unroll
-          for (int e = 0; e < OV; e += 4) {
-            float4 q = *reinterpret_cast<const float4*>(ep.bias + n + e);
-            v[e] += q.x; v[e + 1] += q.y; v[e + 2] += q.z; v[e + 3] += q.w;
-          }
+          for (int e = 0; e < OV; ++e) v[e] += bv[e];
         }
         if (n < ep.col_scale_n) {
 #pragma unroll
