@@ -2164,6 +2164,23 @@ __device__ __forceinline__ void lx_done(const LnxWs& ws, int rb, int tid) {
   }
 }
 
+// Cross-lane sums on the VALU (DPP lane moves + one v_permlane16_swap) instead of __shfl_xor, which
+// compiles to ds_bpermute: an LDS round trip per step, five dependent ones for a 32-lane sum
+template <int CTRL>
+__device__ __forceinline__ float lx_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lx_sum2(float v) { return v + lx_dpp<0xB1>(v); }  // lanes l, l ^ 1
+// the sum over the 32 lanes of the lane's half-wave, in every lane of it
+__device__ __forceinline__ float lx_sum32(float v) {
+  v += lx_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += lx_dpp<0x4E>(v);   // quad_perm [2,3,0,1]: the quad
+  v += lx_dpp<0x141>(v);  // row_half_mirror: the other quad of the 8
+  v += lx_dpp<0x140>(v);  // row_mirror: the other 8 of the row of 16
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);  // rows 0 + 1 (2 + 3)
+}
+
 __device__ __forceinline__ void lx_stage(const f32x4 (&acc)[4][4], float* cs, int lane, int wm, int wn) {
   const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
@@ -2337,7 +2354,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t 
       const float4 q = *reinterpret_cast<const float4*>(rr + 4 * j);
       s += (q.x + q.y) + (q.z + q.w);
     }
-    s += __shfl_xor(s, 1, 64);
+    s = lx_sum2(s);
     const float mk = s * (1.f / BN);
     float q2 = 0.f;
 #pragma unroll
@@ -2346,7 +2363,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t 
       const float d0 = q.x - mk, d1 = q.y - mk, d2 = q.z - mk, d3 = q.w - mk;
       q2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
     }
-    q2 += __shfl_xor(q2, 1, 64);
+    q2 = lx_sum2(q2);
     if (hf == 0) lx_store_sc1(ws.part(rb) + nt * BM + row, f32x2{s, q2});
   }
   LX_STAMP(2);
@@ -2457,11 +2474,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
       pb[it >> 2][e] += g[e];
     }
     xh[it] = make_float4(x[0], x[1], x[2], x[3]);
-#pragma unroll
-    for (int o = 1; o < LX_CPR; o <<= 1) {
-      s1 += __shfl_xor(s1, o, 64);
-      s2 += __shfl_xor(s2, o, 64);
-    }
+    static_assert(LX_CPR == 32, "a row's chunks fill a half-wave");
+    s1 = lx_sum32(s1);
+    s2 = lx_sum32(s2);
     if ((tid % LX_CPR) == 0) lx_store_sc1(slot + row, f32x2{s1, s2});
   }
   LX_STAMP(2);
