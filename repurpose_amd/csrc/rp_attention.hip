@@ -671,9 +671,7 @@ __global__ void attn_delta_kernel(MhaDev a) {
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += ((float)ov[r][j] + (a.out_lo ? (float)lv[r][j] : 0.f)) * (float)dv[r][j];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
+        s = rp_sum8(s);
         if ((lane & 7) == 0 && row0 + r < rows) delta_store(a, row0 + r, e, s);
       }
       return;
@@ -698,9 +696,7 @@ __global__ void attn_delta_kernel(MhaDev a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += (rp_ld(o + e + j) + (ol ? rp_ld(ol + e + j) : 0.f)) * rp_ld(d + e + j);
     }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
+    s = rp_sum8(s);
     if ((lane & 7) == 0) delta_store(a, row, e, s);
   }
 }

@@ -158,6 +158,19 @@ __device__ __forceinline__ float rp_wave_max(float v) {
   return v;
 }
 
+// Sum over the 8 lanes of the lane's aligned group, on the VALU: DPP quad_perm [1,0,3,2], [2,3,0,1],
+// then row_half_mirror.  Lane 8k gets bitwise the value of the __shfl_xor 1 / 2 / 4 tree (the same
+// pairs, fp addition commuting), without its three LDS round trips (ds_bpermute).
+template <int CTRL>
+__device__ __forceinline__ float rp_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float rp_sum8(float s) {
+  s += rp_dpp<0xB1>(s);
+  s += rp_dpp<0x4E>(s);
+  return s + rp_dpp<0x141>(s);
+}
+
 // XCD-aware bijective workgroup remap (MI355X: 8 XCDs, blocks dealt round-robin).
 // Consecutive logical tiles end up on one XCD so they share its L2.
 __device__ __forceinline__ int rp_xcd_remap(int bid, int nwg) {

@@ -391,16 +391,14 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* l
       if (MODE == 0 && ep.delta) {
         // the row dot of this chunk's 8 stored values with the output (hi + lo), then the 8 chunks of
         // the head (consecutive lanes: 16 chunks per row, M and N whole tiles so every lane is here)
-        // by xor 1, 2, 4 — attn_delta_kernel's order, so the planes are bitwise its
+        // by rp_sum8 — attn_delta_kernel's order, so the planes are bitwise its
         const bf16x8 oh = *reinterpret_cast<const bf16x8*>(ep.dot_hi + m * ep.ld_dot + n);
         bf16x8 ol;
         if (ep.dot_lo) ol = *reinterpret_cast<const bf16x8*>(ep.dot_lo + m * ep.ld_dot + n);
         float dsum = 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) dsum += ((float)oh[e] + (ep.dot_lo ? (float)ol[e] : 0.f)) * (float)ob[e];
-        dsum += __shfl_xor(dsum, 1, 64);
-        dsum += __shfl_xor(dsum, 2, 64);
-        dsum += __shfl_xor(dsum, 4, 64);
+        dsum = rp_sum8(dsum);
         if ((n & 63) == 0) {
           const int b = (int)(m / ep.dT), t = (int)(m % ep.dT);
           const int64_t at = ((int64_t)b * ep.dH + n / 64) * ep.dT + t, plane = (M / ep.dT) * ep.dH * ep.dT;
@@ -2166,17 +2164,13 @@ __device__ __forceinline__ void lx_done(const LnxWs& ws, int rb, int tid) {
 
 // Cross-lane sums on the VALU (DPP lane moves + one v_permlane16_swap) instead of __shfl_xor, which
 // compiles to ds_bpermute: an LDS round trip per step, five dependent ones for a 32-lane sum
-template <int CTRL>
-__device__ __forceinline__ float lx_dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float lx_sum2(float v) { return v + lx_dpp<0xB1>(v); }  // lanes l, l ^ 1
+__device__ __forceinline__ float lx_sum2(float v) { return v + rp_dpp<0xB1>(v); }  // lanes l, l ^ 1
 // the sum over the 32 lanes of the lane's half-wave, in every lane of it
 __device__ __forceinline__ float lx_sum32(float v) {
-  v += lx_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += lx_dpp<0x4E>(v);   // quad_perm [2,3,0,1]: the quad
-  v += lx_dpp<0x141>(v);  // row_half_mirror: the other quad of the 8
-  v += lx_dpp<0x140>(v);  // row_mirror: the other 8 of the row of 16
+  v += rp_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += rp_dpp<0x4E>(v);   // quad_perm [2,3,0,1]: the quad
+  v += rp_dpp<0x141>(v);  // row_half_mirror: the other quad of the 8
+  v += rp_dpp<0x140>(v);  // row_mirror: the other 8 of the row of 16
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(a[0]) + __uint_as_float(a[1]);  // rows 0 + 1 (2 + 3)
 }
