@@ -475,15 +475,16 @@ class _Schedule:
         # whose four column tiles exchange the row statistics (kernels._lnx_ws) when M % 128 == 0, else
         # the 64 x 512 full-row kernels (bitwise the unfused pairs, but streaming the whole weight per 64
         # rows at one workgroup per CU: +0.17 ms per step at the bench shape).  RP_GEMM_LN: auto (default:
-        # the exchange kernels where their grid fills every CU twice — bench shape 14.93 -> 14.39 ms per
-        # step; smaller grids keep the unfused pairs on 64 / 32-row GEMM tiles),
-        # 1 both directions, fwd / bwd one, 0 none
+        # the exchange kernels where their grid fills every CU — bench shape 14.93 -> 14.39 ms per step,
+        # config 2 (one tile per CU) 7.40 -> 7.10 ms; config 4's half-filled grid
+        # keeps the unfused pairs on 32-row GEMM tiles: forced there 7.14 -> 7.24 ms), 1 both directions,
+        # fwd / bwd one, 0 none
         ln = os.environ.get("RP_GEMM_LN", "auto")
         ok = self.dt == torch.bfloat16 and self.M % 64 == 0 and model.d_model == 512
         if ln == "auto":
             dev = model._flat.device
             cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
-            ln = "1" if (self.M % 128 == 0 and cus > 0 and (self.M // 128) * 4 >= 2 * cus
+            ln = "1" if (self.M % 128 == 0 and cus > 0 and (self.M // 128) * 4 >= cus
                          and os.environ.get("RP_GEMM_LNX", "1") == "1") else "0"
         self.fused_ln_fwd = ok and ln in ("1", "fwd")
         self.fused_ln = ok and ln in ("1", "bwd")
