@@ -206,17 +206,18 @@ _LNX = {}
 
 def _lnx_ws(dev, M):
     """The exchange workspace of the 128 x 128 GEMM + LayerNorm kernels (rp_gemm_ln_xchg_bytes, zero-filled
-    once; every launch leaves it zeroed), one per (device, stream) — launches on one stream are ordered,
-    launches on two streams may overlap and must not share counters — grown as needed.  RP_GEMM_LNX=0
-    (A/B) or M % 128 != 0: None, i.e. the 64-row full-row kernels."""
+    once; every launch leaves it zeroed), one per device, grown as needed.  Launches sharing it must be
+    ordered: the drop-in issues every seam on the device's current stream (a captured step replays on
+    the stream its eager steps use), so one per device suffices — and the capture stream does not get a
+    workspace of its own, whose zero fill would be captured into every replay.  RP_GEMM_LNX=0 (A/B) or
+    M % 128 != 0: None, i.e. the 64-row full-row kernels."""
     if M % 128 or os.environ.get("RP_GEMM_LNX", "1") != "1":
         return None
     need = int(N.load().rp_gemm_ln_xchg_bytes(M))
-    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
-    ws = _LNX.get(key)
+    ws = _LNX.get(dev)
     if ws is None or ws.numel() < need:
         ws = torch.zeros(need, device=dev, dtype=torch.uint8)
-        _LNX[key] = ws
+        _LNX[dev] = ws
     return ws
 
 

@@ -62,3 +62,36 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def spread():
+    """Main-loop time per workgroup against its XCD (blockIdx % 8) and its place in the XCD's tile range."""
+    dev = torch.device("cuda:0")
+    M, D, Kd = 16384, 512, 2048
+    g = torch.Generator().manual_seed(0)
+    res = torch.randn(M, D, generator=g).to(dev)
+    gm, bt = 1 + 0.1 * torch.randn(D, generator=g).to(dev), 0.1 * torch.randn(D, generator=g).to(dev)
+    b = 0.1 * torch.randn(D, generator=g).to(dev)
+    x = torch.randn(M, Kd, generator=g).to(dev, torch.bfloat16)
+    W = (torch.randn(D, Kd, generator=g) * 0.03).to(dev, torch.bfloat16)
+    for _ in range(6):
+        K.linear_ln_fwd(x, W, b, res, gm, bt, dropout_p=0.1, seed=3)
+    torch.cuda.synchronize()
+    nwg = (M // 128) * 4
+    s = stamps(nwg) * 10 / 1000.0
+    main = s[:, 1] - s[:, 0]
+    start = s[:, 0] - s[:, 0].min()
+    bid = np.arange(nwg)
+    xcd = bid % 8
+    print("fwd K=2048 main loop by XCD (median / max):",
+          " ".join(f"{x}:{np.median(main[xcd == x]):.1f}/{main[xcd == x].max():.1f}" for x in range(8)))
+    order = np.argsort(main)
+    print("slowest 12 workgroups (bid, xcd, start, main):",
+          [(int(i), int(i % 8), round(float(start[i]), 2), round(float(main[i]), 2)) for i in order[-12:]])
+    print("fastest 6:", [(int(i), int(i % 8), round(float(start[i]), 2), round(float(main[i]), 2)) for i in order[:6]])
+    # per CU pair? workgroups i and i + 256 dispatched to the same slot range
+    print("corr(start, main):", float(np.corrcoef(start, main)[0, 1]))
+
+
+if __name__ == "__main__" and os.environ.get("LNX_SPREAD"):
+    spread()
