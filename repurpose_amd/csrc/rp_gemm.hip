@@ -1271,17 +1271,18 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
 // barrier before any wave reads it: the leading half waits before its fourth barrier of K-tile t,
 // the lagging half before its third (both event 4t+4), vmcnt(2) leaving only B(t+2) in flight.
 // Same MFMA order per output element as the 128 x 128 kernel (K-tiles ascending, 32-deep halves).
-template <bool AK, bool BKM, typename TC, int MODE>
-__device__ __forceinline__ void gemm8_tile128(int64_t M, int64_t N, const bf16* __restrict__ A, int64_t lda,
-                                              const bf16* __restrict__ B, int64_t ldb, TC* __restrict__ Cout,
-                                              int64_t ldc, float alpha, const EpiDev& ep, int64_t kbeg, int64_t kend,
-                                              int64_t m0, int64_t n0, int split, char* lds) {
+// The main loop of the 256 x 128 phased tile (eight waves of 128 x 32: wm = wid >> 2 the row half, wn the
+// 32-column quarter), acc[i][j] = C[m0 + 128 wm + 16 i + 4 g + r][n0 + 32 wn + 16 j + c]; returns after the
+// last barrier (the caller synchronises before reusing the LDS)
+template <bool AK, bool BKM>
+__device__ __forceinline__ void g8_128_mainloop(int64_t M, int64_t N, const bf16* __restrict__ A, int64_t lda,
+                                                const bf16* __restrict__ B, int64_t ldb, int64_t kbeg, int64_t kend,
+                                                int64_t m0, int64_t n0, f32x4 (&acc)[8][2], char* lds) {
   using G = G8<128, 64, 2>;
   static_assert(G::NBH == 1 && G::JT == 2, "256 x 128 tile");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 2, wn = wid & 3;
-  f32x4 acc[8][2];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1376,6 +1377,18 @@ __device__ __forceinline__ void gemm8_tile128(int64_t M, int64_t N, const bf16* 
     rp_raw_barrier();
   }
   if (wm == 0) rp_raw_barrier();  // match the lagging half's barrier count
+}
+
+template <bool AK, bool BKM, typename TC, int MODE>
+__device__ __forceinline__ void gemm8_tile128(int64_t M, int64_t N, const bf16* __restrict__ A, int64_t lda,
+                                              const bf16* __restrict__ B, int64_t ldb, TC* __restrict__ Cout,
+                                              int64_t ldc, float alpha, const EpiDev& ep, int64_t kbeg, int64_t kend,
+                                              int64_t m0, int64_t n0, int split, char* lds) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  f32x4 acc[8][2];
+  g8_128_mainloop<AK, BKM>(M, N, A, lda, B, ldb, kbeg, kend, m0, n0, acc, lds);
   __syncthreads();
   gemm8_epilogue<TC, MODE, 128>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
 }
@@ -2185,10 +2198,19 @@ __device__ __forceinline__ void lx_stage(const f32x4 (&acc)[4][4], float* cs, in
       for (int r = 0; r < 4; ++r) cs[(wm * 64 + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
 }
 
-constexpr int LX_CPR = BN / 4;             // float4 chunks per tile row
-constexpr int LX_IT = BM * LX_CPR / NT;    // chunks per thread (16): row = tid / 32 + 8 it
-constexpr int LX_LDS = CTILE_BYTES + 4 * BM * 4;  // staged tile, per-row totals, (bwd) mean / rstd
+constexpr int LX_CPR = BN / 4;  // float4 chunks per tile row (a half-wave)
 static_assert(DmaCfg<0>::LDS <= CTILE_BYTES, "main loop fits the staging area");
+// An exchange epilogue over a staged TR x 128 tile with TNT threads: thread tid owns chunk column
+// tid % 32 of the rows tid / 32 + RS it, it < IT.  Row m0 + row's partials go to record
+// m0 / 128 + row / 128; the four column tiles arrive on record m0 / 128's counter.
+template <int TR, int TNT>
+struct LxG {
+  static constexpr int RS = TNT / LX_CPR;                // rows per chunk step
+  static constexpr int IT = TR / RS;                     // chunks per thread
+  static constexpr int LDS = TR * CST * 4 + 4 * TR * 4;  // staged tile, per-row totals, (bwd) mean / rstd
+  static_assert(TNT == 2 * TR && TR % BM == 0, "two threads per row, whole records");
+};
+constexpr int LX_IT = LxG<BM, NT>::IT;  // 16: row = tid / 32 + 8 it
 
 // glds_tile's fills issued through inline asm (rp_dma16): the compiler does not track them, so it adds
 // no vmcnt(0) ahead of the LDS reads, and loads the caller issues between fills stay in flight across
@@ -2284,9 +2306,218 @@ static int lnx_prefetch() {
   return v;
 }
 
+// Forward epilogue of a staged TR x 128 accumulator tile cs (r: the thread's residual chunks)
+template <int TR, int TNT>
+__device__ __forceinline__ void lx_fwd_tail(const GlnDev& a, const LnxWs& ws, int64_t m0, int64_t n0, int nt,
+                                            float* cs, const float4 (&r)[LxG<TR, TNT>::IT], int tid) {
+  using L = LxG<TR, TNT>;
+  float* st = cs + TR * CST;  // per-row mean, rstd
+  const int rb = (int)(m0 / BM), cc = (tid % LX_CPR) * 4;
+  // x_out = dropout(acc + bias) + residual: gemm_epilogue's RESB arithmetic, op for op
+  const float4 bi = *reinterpret_cast<const float4*>(a.bias + n0 + cc);
+  const uint32_t dseed = a.drop_thresh ? rp_seed_eff(a.seed_base, a.drop_seed) : 0u;
+#pragma unroll
+  for (int it = 0; it < L::IT; ++it) {
+    const int row = tid / LX_CPR + it * L::RS;
+    const int64_t m = m0 + row, n = n0 + cc;
+    float* c = cs + row * CST + cc;
+    const float4 v = *reinterpret_cast<const float4*>(c);
+    float e4[4] = {v.x * 1.f + bi.x, v.y * 1.f + bi.y, v.z * 1.f + bi.z, v.w * 1.f + bi.w};
+    if (a.drop_thresh) {
+      const uint32_t kb = rp_keep_bits<4>(dseed, (uint32_t)(m * GL_N + n), a.drop_thresh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) e4[e] = ((kb >> e) & 1u) ? e4[e] * a.drop_scale : 0.f;
+    }
+    e4[0] += r[it].x; e4[1] += r[it].y; e4[2] += r[it].z; e4[3] += r[it].w;
+    const float4 o = make_float4(e4[0], e4[1], e4[2], e4[3]);
+    rp_st16(a.xo + m * a.ldxo + n, o, 2);
+    *reinterpret_cast<float4*>(c) = o;
+  }
+  __syncthreads();
+  // the tile's per-row (sum, M2): two threads per row, 64 columns each
+  const int row = tid >> 1, hf = tid & 1;
+  f32x2* rec = ws.part(rb + row / BM) + row % BM;  // the row's pair of column tile 0
+  {
+    const float* rr = cs + row * CST + hf * 64;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float4 q = *reinterpret_cast<const float4*>(rr + 4 * j);
+      s += (q.x + q.y) + (q.z + q.w);
+    }
+    s = lx_sum2(s);
+    const float mk = s * (1.f / BN);
+    float q2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float4 q = *reinterpret_cast<const float4*>(rr + 4 * j);
+      const float d0 = q.x - mk, d1 = q.y - mk, d2 = q.z - mk, d3 = q.w - mk;
+      q2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    }
+    q2 = lx_sum2(q2);
+    if (hf == 0) lx_store_sc1(rec + nt * BM, f32x2{s, q2});
+  }
+  LX_STAMP(2);
+  lx_drain_arrive(ws, rb, tid);
+  LX_STAMP(3);
+  lx_wait(ws, rb, tid);
+  LX_STAMP(4);
+  if (hf == 0) {
+    f32x2 o[LX_TN];
+    lx_load_sc1(rec, o);
+    const float mean = ((o[0].x + o[1].x) + (o[2].x + o[3].x)) * (1.f / GL_N);
+    float m2 = (o[0].y + o[1].y) + (o[2].y + o[3].y);
+#pragma unroll
+    for (int k = 0; k < LX_TN; ++k) {
+      const float d = o[k].x * (1.f / BN) - mean;
+      m2 += (float)BN * d * d;
+    }
+    st[row] = mean;
+    st[TR + row] = rsqrtf(m2 * (1.f / GL_N) + a.eps);
+  }
+  __syncthreads();
+  lx_done(ws, rb, tid);
+  // h = LayerNorm(x_out): ln_fwd_kernel's (v - mean) * rstd * gamma + beta, 8 columns per thread
+  const int c8 = (tid % (BN / 8)) * 8;
+  float gm[8], bt[8];
+  ld8(gm, a.gamma + n0 + c8);
+  ld8(bt, a.beta + n0 + c8);
+#pragma unroll 2
+  for (int it = 0; it < TR * (BN / 8) / TNT; ++it) {
+    const int rw = tid / (BN / 8) + it * (TNT / (BN / 8));
+    float v[8];
+    ld8(v, cs + rw * CST + c8);
+    const float mean = st[rw], rstd = st[TR + rw];
+    float y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) y[i] = (v[i] - mean) * rstd * gm[i] + bt[i];
+    st8bf(a.h + (m0 + rw) * a.ldh + n0 + c8, y);
+  }
+  if (nt == 0 && tid < TR) {
+    a.mean[m0 + tid] = st[tid];
+    a.rstd[m0 + tid] = st[TR + tid];
+  }
+#ifdef RP_GEMM_PROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  LX_STAMP(5);
+#endif
+}
+
+// Backward epilogue of a staged TR x 128 gradient tile cs (rows' mean / rstd staged at
+// cs + TR CST + 2 TR; xh: the thread's x chunks)
+template <int TR, int TNT>
+__device__ __forceinline__ void lx_bwd_tail(const GlnDev& a, const LnxWs& ws, int64_t m0, int64_t n0, int nt,
+                                            float* cs, float4 (&xh)[LxG<TR, TNT>::IT], int tid) {
+  using L = LxG<TR, TNT>;
+  float* st = cs + TR * CST;  // per-row s1 / 512, s2 / 512
+  const float* mr = st + 2 * TR;
+  const int rb = (int)(m0 / BM), cc = (tid % LX_CPR) * 4, r0 = tid / LX_CPR;
+  const float4 gm = *reinterpret_cast<const float4*>(a.gamma + n0 + cc);
+  const float gam[4] = {gm.x, gm.y, gm.z, gm.w};
+  float pg[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f};  // the tile's gamma / beta partials
+#pragma unroll
+  for (int it = 0; it < L::IT; ++it) {
+    const int row = r0 + it * L::RS;
+    const float mu = mr[row], rs = mr[TR + row];
+    const float4 g4 = *reinterpret_cast<const float4*>(cs + row * CST + cc);
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+    float x[4] = {xh[it].x, xh[it].y, xh[it].z, xh[it].w};
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[e] = (x[e] - mu) * rs;
+      const float gg = g[e] * gam[e];
+      s1 += gg;
+      s2 += gg * x[e];
+      pg[e] += g[e] * x[e];
+      pb[e] += g[e];
+    }
+    xh[it] = make_float4(x[0], x[1], x[2], x[3]);
+    static_assert(LX_CPR == 32, "a row's chunks fill a half-wave");
+    s1 = lx_sum32(s1);
+    s2 = lx_sum32(s2);
+    if ((tid % LX_CPR) == 0) lx_store_sc1(ws.part(rb + row / BM) + nt * BM + row % BM, f32x2{s1, s2});
+  }
+  LX_STAMP(2);
+  lx_drain_arrive(ws, rb, tid);
+  LX_STAMP(3);
+  float4 dr[L::IT];  // the residual gradient, in flight while the row block gathers
+  if (a.dres) {
+#pragma unroll
+    for (int it = 0; it < L::IT; ++it) dr[it] = rp_ld16f(a.dres + (m0 + r0 + it * L::RS) * a.lddres + n0 + cc, 2);
+  }
+  lx_wait(ws, rb, tid);
+  LX_STAMP(4);
+  if (tid < TR) {
+    f32x2 o[LX_TN];
+    lx_load_sc1(ws.part(rb + tid / BM) + tid % BM, o);
+    st[tid] = ((o[0].x + o[1].x) + (o[2].x + o[3].x)) * (1.f / GL_N);
+    st[TR + tid] = ((o[0].y + o[1].y) + (o[2].y + o[3].y)) * (1.f / GL_N);
+  }
+  __syncthreads();
+  lx_done(ws, rb, tid);
+  const uint32_t lseed = a.lp_thresh ? rp_seed_eff(a.seed_base, a.lp_seed) : 0u;
+#pragma unroll
+  for (int it = 0; it < L::IT; ++it) {
+    const int row = r0 + it * L::RS;
+    const int64_t m = m0 + row, n = n0 + cc;
+    const float rs = mr[TR + row], s1 = st[row], s2 = st[TR + row];
+    const float4 g4 = *reinterpret_cast<const float4*>(cs + row * CST + cc);
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w}, x[4] = {xh[it].x, xh[it].y, xh[it].z, xh[it].w};
+    float dx[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dx[e] = rs * (g[e] * gam[e] - s1 - x[e] * s2);
+    if (a.dres) {
+      dx[0] += dr[it].x; dx[1] += dr[it].y; dx[2] += dr[it].z; dx[3] += dr[it].w;
+    }
+    *reinterpret_cast<float4*>(a.dx + m * a.lddx + n) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+    if (a.dx_lp) {
+      if (a.lp_thresh) {
+        const uint32_t kb = rp_keep_bits<4>(lseed, (uint32_t)(m * GL_N + n), a.lp_thresh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dx[e] = ((kb >> e) & 1u) ? dx[e] * a.lp_scale : 0.f;
+      }
+      bf16x4 q;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q[e] = (bf16)dx[e];
+      *reinterpret_cast<bf16x4*>(a.dx_lp + m * a.lddx_lp + n) = q;
+    }
+  }
+  // gamma / beta partials: the tile's column sums (the RS threads of a column chunk summed in LDS) in
+  // partial row m0 / 32, zeros in its other TR / 32 - 1 rows (the partial rows are 32-row blocks)
+  if (a.dgamma_part || a.dbeta_part) {
+    __syncthreads();  // every read of the staged tile is done
+    float* red = cs;  // [2][RS row groups][128 columns]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[(0 * L::RS + r0) * BN + cc + e] = pg[e];
+      red[(1 * L::RS + r0) * BN + cc + e] = pb[e];
+    }
+    __syncthreads();
+    const int64_t pr = m0 / 32;
+    if (tid < 2 * BN) {
+      const int k = tid / BN, c = tid % BN;
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < L::RS; ++q) s += red[(k * L::RS + q) * BN + c];
+      float* dst = k ? a.dbeta_part : a.dgamma_part;
+      if (dst) dst[pr * a.ld_part + n0 + c] = s;
+    }
+    for (int id = tid; id < (TR / 32 - 1) * 2 * BN; id += TNT) {
+      const int k = id / ((TR / 32 - 1) * BN), rr = (id / BN) % (TR / 32 - 1) + 1, c = id % BN;
+      float* dst = k ? a.dbeta_part : a.dgamma_part;
+      if (dst) dst[(pr + rr) * a.ld_part + n0 + c] = 0.f;
+    }
+  }
+#ifdef RP_GEMM_PROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  LX_STAMP(5);
+#endif
+}
+
 __global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws,
                                                              int pf) {
-  __shared__ __attribute__((aligned(16))) char lds[LX_LDS];
+  __shared__ __attribute__((aligned(16))) char lds[LxG<BM, NT>::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
@@ -2314,101 +2545,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t 
   }
   LX_STAMP(1);
   float* cs = reinterpret_cast<float*>(lds);
-  float* st = cs + BM * CST;  // per-row mean, rstd
   lx_stage(acc, cs, lane, wm, wn);
   __syncthreads();
-  // x_out = dropout(acc + bias) + residual: gemm_epilogue's RESB arithmetic, op for op
-  const float4 bi = *reinterpret_cast<const float4*>(a.bias + n0 + cc);
-  const uint32_t dseed = a.drop_thresh ? rp_seed_eff(a.seed_base, a.drop_seed) : 0u;
-#pragma unroll
-  for (int it = 0; it < LX_IT; ++it) {
-    const int row = tid / LX_CPR + it * (NT / LX_CPR);
-    const int64_t m = m0 + row, n = n0 + cc;
-    float* c = cs + row * CST + cc;
-    const float4 v = *reinterpret_cast<const float4*>(c);
-    float e4[4] = {v.x * 1.f + bi.x, v.y * 1.f + bi.y, v.z * 1.f + bi.z, v.w * 1.f + bi.w};
-    if (a.drop_thresh) {
-      const uint32_t kb = rp_keep_bits<4>(dseed, (uint32_t)(m * GL_N + n), a.drop_thresh);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) e4[e] = ((kb >> e) & 1u) ? e4[e] * a.drop_scale : 0.f;
-    }
-    e4[0] += r[it].x; e4[1] += r[it].y; e4[2] += r[it].z; e4[3] += r[it].w;
-    const float4 o = make_float4(e4[0], e4[1], e4[2], e4[3]);
-    rp_st16(a.xo + m * a.ldxo + n, o, 2);
-    *reinterpret_cast<float4*>(c) = o;
-  }
-  __syncthreads();
-  // the tile's per-row (sum, M2): two threads per row, 64 columns each
-  const int row = tid >> 1, hf = tid & 1;
-  {
-    const float* rr = cs + row * CST + hf * 64;
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float4 q = *reinterpret_cast<const float4*>(rr + 4 * j);
-      s += (q.x + q.y) + (q.z + q.w);
-    }
-    s = lx_sum2(s);
-    const float mk = s * (1.f / BN);
-    float q2 = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float4 q = *reinterpret_cast<const float4*>(rr + 4 * j);
-      const float d0 = q.x - mk, d1 = q.y - mk, d2 = q.z - mk, d3 = q.w - mk;
-      q2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-    }
-    q2 = lx_sum2(q2);
-    if (hf == 0) lx_store_sc1(ws.part(rb) + nt * BM + row, f32x2{s, q2});
-  }
-  LX_STAMP(2);
-  lx_drain_arrive(ws, rb, tid);
-  LX_STAMP(3);
-  lx_wait(ws, rb, tid);
-  LX_STAMP(4);
-  if (hf == 0) {
-    f32x2 o[LX_TN];
-    lx_load_sc1(ws.part(rb) + row, o);
-    const float mean = ((o[0].x + o[1].x) + (o[2].x + o[3].x)) * (1.f / GL_N);
-    float m2 = (o[0].y + o[1].y) + (o[2].y + o[3].y);
-#pragma unroll
-    for (int k = 0; k < LX_TN; ++k) {
-      const float d = o[k].x * (1.f / BN) - mean;
-      m2 += (float)BN * d * d;
-    }
-    st[row] = mean;
-    st[BM + row] = rsqrtf(m2 * (1.f / GL_N) + a.eps);
-  }
-  __syncthreads();
-  lx_done(ws, rb, tid);
-  // h = LayerNorm(x_out): ln_fwd_kernel's (v - mean) * rstd * gamma + beta, 8 columns per thread
-  const int c8 = (tid % (BN / 8)) * 8;
-  float gm[8], bt[8];
-  ld8(gm, a.gamma + n0 + c8);
-  ld8(bt, a.beta + n0 + c8);
-#pragma unroll 2
-  for (int it = 0; it < BM * (BN / 8) / NT; ++it) {
-    const int rw = tid / (BN / 8) + it * (NT / (BN / 8));
-    float v[8];
-    ld8(v, cs + rw * CST + c8);
-    const float mean = st[rw], rstd = st[BM + rw];
-    float y[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) y[i] = (v[i] - mean) * rstd * gm[i] + bt[i];
-    st8bf(a.h + (m0 + rw) * a.ldh + n0 + c8, y);
-  }
-  if (nt == 0 && tid < BM) {
-    a.mean[m0 + tid] = st[tid];
-    a.rstd[m0 + tid] = st[BM + tid];
-  }
-#ifdef RP_GEMM_PROBE
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  LX_STAMP(5);
-#endif
+  lx_fwd_tail<BM, NT>(a, ws, m0, n0, nt, cs, r, tid);
 }
 
 __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws,
                                                              int pf) {
-  __shared__ __attribute__((aligned(16))) char lds[LX_LDS];
+  __shared__ __attribute__((aligned(16))) char lds[LxG<BM, NT>::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
@@ -2435,120 +2579,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
   }
   LX_STAMP(1);
   float* cs = reinterpret_cast<float*>(lds);
-  float* st = cs + BM * CST;  // per-row s1 / 512, s2 / 512
-  float* mr = st + 2 * BM;    // the tile rows' mean, rstd: loaded once, read by both passes
+  float* mr = cs + BM * CST + 2 * BM;  // the tile rows' mean, rstd: loaded once, read by both passes
   float mrv = 0.f;
   if (tid < 2 * BM) mrv = tid < BM ? a.mean[m0 + tid] : a.rstd[m0 + tid - BM];
   lx_stage(acc, cs, lane, wm, wn);
   if (tid < 2 * BM) mr[tid] = mrv;
   __syncthreads();
-  const float4 gm = *reinterpret_cast<const float4*>(a.gamma + n0 + cc);
-  const float gam[4] = {gm.x, gm.y, gm.z, gm.w};
-  float pg[4][4], pb[4][4];  // gamma / beta partials per 32-row block and column
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) pg[b][e] = pb[b][e] = 0.f;
-  f32x2* slot = ws.part(rb) + nt * BM;
-#pragma unroll
-  for (int it = 0; it < LX_IT; ++it) {
-    const int row = r0 + it * (NT / LX_CPR);
-    const float mu = mr[row], rs = mr[BM + row];
-    const float4 g4 = *reinterpret_cast<const float4*>(cs + row * CST + cc);
-    const float g[4] = {g4.x, g4.y, g4.z, g4.w};
-    float x[4] = {xh[it].x, xh[it].y, xh[it].z, xh[it].w};
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      x[e] = (x[e] - mu) * rs;
-      const float gg = g[e] * gam[e];
-      s1 += gg;
-      s2 += gg * x[e];
-      pg[it >> 2][e] += g[e] * x[e];
-      pb[it >> 2][e] += g[e];
-    }
-    xh[it] = make_float4(x[0], x[1], x[2], x[3]);
-    static_assert(LX_CPR == 32, "a row's chunks fill a half-wave");
-    s1 = lx_sum32(s1);
-    s2 = lx_sum32(s2);
-    if ((tid % LX_CPR) == 0) lx_store_sc1(slot + row, f32x2{s1, s2});
-  }
-  LX_STAMP(2);
-  lx_drain_arrive(ws, rb, tid);
-  LX_STAMP(3);
-  float4 dr[LX_IT];  // the residual gradient, in flight while the row block gathers
-  if (a.dres) {
-#pragma unroll
-    for (int it = 0; it < LX_IT; ++it)
-      dr[it] = rp_ld16f(a.dres + (m0 + r0 + it * (NT / LX_CPR)) * a.lddres + n0 + cc, 2);
-  }
-  lx_wait(ws, rb, tid);
-  LX_STAMP(4);
-  if (tid < BM) {
-    f32x2 o[LX_TN];
-    lx_load_sc1(ws.part(rb) + tid, o);
-    st[tid] = ((o[0].x + o[1].x) + (o[2].x + o[3].x)) * (1.f / GL_N);
-    st[BM + tid] = ((o[0].y + o[1].y) + (o[2].y + o[3].y)) * (1.f / GL_N);
-  }
-  __syncthreads();
-  lx_done(ws, rb, tid);
-  const uint32_t lseed = a.lp_thresh ? rp_seed_eff(a.seed_base, a.lp_seed) : 0u;
-#pragma unroll
-  for (int it = 0; it < LX_IT; ++it) {
-    const int row = r0 + it * (NT / LX_CPR);
-    const int64_t m = m0 + row, n = n0 + cc;
-    const float rs = mr[BM + row], s1 = st[row], s2 = st[BM + row];
-    const float4 g4 = *reinterpret_cast<const float4*>(cs + row * CST + cc);
-    const float g[4] = {g4.x, g4.y, g4.z, g4.w}, x[4] = {xh[it].x, xh[it].y, xh[it].z, xh[it].w};
-    float dx[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) dx[e] = rs * (g[e] * gam[e] - s1 - x[e] * s2);
-    if (a.dres) {
-      dx[0] += dr[it].x; dx[1] += dr[it].y; dx[2] += dr[it].z; dx[3] += dr[it].w;
-    }
-    *reinterpret_cast<float4*>(a.dx + m * a.lddx + n) = make_float4(dx[0], dx[1], dx[2], dx[3]);
-    if (a.dx_lp) {
-      if (a.lp_thresh) {
-        const uint32_t kb = rp_keep_bits<4>(lseed, (uint32_t)(m * GL_N + n), a.lp_thresh);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dx[e] = ((kb >> e) & 1u) ? dx[e] * a.lp_scale : 0.f;
-      }
-      bf16x4 q;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) q[e] = (bf16)dx[e];
-      *reinterpret_cast<bf16x4*>(a.dx_lp + m * a.lddx_lp + n) = q;
-    }
-  }
-  // gamma / beta partials per 32-row block: the 8 threads of a column chunk (rows r0 + 8 it) summed in LDS
-  if (a.dgamma_part || a.dbeta_part) {
-    __syncthreads();  // every read of the staged tile is done
-    float* red = cs;   // [2][4 blocks][8 row groups][128 columns]
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        red[((0 * 4 + b) * 8 + r0) * BN + cc + e] = pg[b][e];
-        red[((1 * 4 + b) * 8 + r0) * BN + cc + e] = pb[b][e];
-      }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int id = tid + k * NT, b = id / BN, c = id % BN;  // (block, column): 512 per tile
-      float sg = 0.f, sb = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        sg += red[((0 * 4 + b) * 8 + q) * BN + c];
-        sb += red[((1 * 4 + b) * 8 + q) * BN + c];
-      }
-      const int64_t pr = m0 / 32 + b;
-      if (a.dgamma_part) a.dgamma_part[pr * a.ld_part + n0 + c] = sg;
-      if (a.dbeta_part) a.dbeta_part[pr * a.ld_part + n0 + c] = sb;
-    }
-  }
-#ifdef RP_GEMM_PROBE
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  LX_STAMP(5);
-#endif
+  lx_bwd_tail<BM, NT>(a, ws, m0, n0, nt, cs, xh, tid);
 }
 }  // namespace
 

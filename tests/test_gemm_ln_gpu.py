@@ -218,7 +218,7 @@ def test_model_fused_seams_exchange(dev, monkeypatch):
 def test_linear_ln_exchange_mixed_rows(dev):
     """One workspace shared by launches of different row counts (the record of a row block does not move
     with M): each launch agrees with the unfused pair and leaves the counters zeroed."""
-    for M in (4096, 8192, 16384, 1024, 8192):
+    for M in (4096, 8192, 16384, 1024, 8192, 384):
         g = torch.Generator().manual_seed(M)
         x, W = _r(g, M, 512, dev=dev), _r(g, D, 512, dev=dev, sc=0.03)
         b, res = _r(g, D, dev=dev, dt=torch.float32, sc=0.1), _r(g, M, D, dev=dev, dt=torch.float32)
