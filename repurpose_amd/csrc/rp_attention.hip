@@ -64,20 +64,6 @@ __device__ __forceinline__ int lds_off(int row, int byte) {
     return row * AttnCfg<T>::ROWB + byte;
 }
 
-// The image of the 32x32x16 dK/dV body (swizzle kind 1): 16-byte chunk ^ ((((row >> 1) & 1) << 2) |
-// ((row >> 2) & 3)).  Conflict-free for its two read kinds: ds_read_b128 row fragments (32 rows at one
-// chunk: each 16-lane group's even rows, and its odd rows, take 8 distinct chunks) and ds_read_b64_tr_b16
-// column fragments (4 consecutive rows x 64 bytes per 32-lane half: rows r and r + 2 fall in opposite
-// 64-byte halves of their 128-byte rows).  Kind 0 is lds_swz.
-template <int SW>
-__device__ __forceinline__ int lds_swz_k(int row) {
-  return SW ? ((((row >> 1) & 1) << 2) | ((row >> 2) & 3)) : lds_swz(row);
-}
-template <int SW>
-__device__ __forceinline__ int lds_off_k(int row, int byte) {
-  return row * 128 + (byte ^ (lds_swz_k<SW>(row) << 4));
-}
-
 // keep-bit mask layout (the forward's register layout, so the forward and dQ kernels move one
 // 16-bit word per lane and key tile): [B*H][KT = ceil(T/64)][4 lane groups g][ldm = roundup(T,128)]
 // (a row covers every query of the last 128-query block, so block-wide stores and DMA pieces of a
@@ -254,50 +240,6 @@ __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, con
 __device__ __forceinline__ f32x4 mfma_f32(float a, float b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
-// 32x32x16 operands (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) holds A[row r][k = 8h + j]
-// and B[k = 8h + j][col r]; C register e holds row (e & 3) + 8 (e >> 2) + 4h, column r
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-// row fragment of a 32-row block: lane holds X[r0 + (l & 31)][k0 + 8 (l >> 5) + j]
-template <int SW>
-__device__ __forceinline__ bf16x8 row32_frag_lds(const char* lds, int r0, int k0, int lane) {
-  return *reinterpret_cast<const bf16x8*>(lds + lds_off_k<SW>(r0 + (lane & 31), (k0 + 8 * (lane >> 5)) * 2));
-}
-__device__ __forceinline__ bf16x8 row32_frag_gmem(const bf16* base, int64_t ld, int r0, int nrows, int k0, int lane) {
-  const int r = r0 + (lane & 31);
-  if (r >= nrows) {
-    bf16x8 z;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
-    return z;
-  }
-  return *reinterpret_cast<const bf16x8*>(base + (int64_t)r * ld + k0 + 8 * (lane >> 5));
-}
-// column fragment for a 32x32x16 B operand that sums over rows R .. R + 15 of X in the k-slot order of
-// a 32x32 accumulator's registers 8c .. 8c + 7 (rows R + 4h + {0..3}, then R + 8 + 4h + {0..3}): lane
-// l receives X[those rows][c0 + (l & 31)] through two ds_read_b64_tr_b16 (per 16-lane group G: rows
-// R + 4h + (i >> 2), columns c0 + 16 (G & 1) + 4 (i & 3), i = l & 15)
-template <int SW>
-__device__ __forceinline__ bf16x8 col32_frag_lds(const char* lds, int R, int c0, int lane) {
-  const int G = lane >> 4, i = lane & 15, h = G >> 1;
-  const int row = R + 4 * h + (i >> 2), col = c0 + 16 * (G & 1) + 4 * (i & 3);
-  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds + lds_off_k<SW>(row, col * 2)));
-  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds + lds_off_k<SW>(row + 8, col * 2)));
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
-}
-// accumulator registers 8c .. 8c + 7 -> bf16x8 (the k-slot order of col32_frag_lds)
-__device__ __forceinline__ bf16x8 pack8_32(const f32x16& x, int c) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)x[8 * c + j];
-  return r;
-}
-
 // f32 scalar LDS read X[r][c]
 __device__ __forceinline__ float ldsf(const char* lds, int r, int c) {
   return *reinterpret_cast<const float*>(lds + r * AttnCfg<float>::ROWB + c * 4);
@@ -1115,7 +1057,6 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
 // rows [row0, row0 + 64) of a [rows][64] bf16 operand (row stride ld) -> the swizzled 8 KB image of
 // lds_off<bf16>: eight 1 KB pieces (8 rows each), two per wave; lane l of a piece lands at physical
 // 16-byte chunk l & 7 of row l >> 3, which holds logical chunk (l & 7) ^ lds_swz(row)
-template <int SW = 0>
 __device__ __forceinline__ void dma_rows64(const bf16* __restrict__ base, int64_t ld, int row0, int nrows, char* tile,
                                            int w, int lane) {
   const uint32_t t = lds_addr(tile);
@@ -1123,7 +1064,7 @@ __device__ __forceinline__ void dma_rows64(const bf16* __restrict__ base, int64_
   for (int j = 0; j < 2; ++j) {
     const int I = w * 2 + j;
     const int r = I * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ lds_swz_k<SW>(r);
+    const int c = (lane & 7) ^ lds_swz(r);
     int rr = row0 + r;
     rr = rr < nrows ? rr : nrows - 1;
     dma16(base + (int64_t)rr * ld + c * 8, t + I * 1024);
@@ -1199,13 +1140,12 @@ struct Rows64 {
   rp_srd srd;
   uint32_t vo0, vo1, rowbytes;
   bool fast;  // every full tile's byte offsets fit 32 bits
-  template <int SW = 0>
   __device__ __forceinline__ void init(const bf16* b, int64_t ld_, int nrows, int w, int lane) {
     base = b;
     ld = ld_;
     srd = make_srd(b);
     const int r0 = (w * 2) * 8 + (lane >> 3), r1 = r0 + 8;
-    const int c0 = (lane & 7) ^ lds_swz_k<SW>(r0), c1 = (lane & 7) ^ lds_swz_k<SW>(r1);
+    const int c0 = (lane & 7) ^ lds_swz(r0), c1 = (lane & 7) ^ lds_swz(r1);
     vo0 = (uint32_t)((r0 * ld_ + c0 * 8) * 2);
     vo1 = (uint32_t)((r1 * ld_ + c1 * 8) * 2);
     rowbytes = (uint32_t)(ld_ * 2);
@@ -1234,14 +1174,8 @@ constexpr int KV_DMA_BUF = 2 * KV_QT * AttnCfg<bf16>::ROWB + 4 * 1024;
 // the same key block over the second half of the query tiles on a ring of their own, and the two
 // halves' dK / dV partials are added through LDS at the end (dK = own + partner on half 0, which stores
 // dK; dV likewise on half 1) — two waves per SIMD where one 4-wave workgroup per CU had one
-// M32: the S / dP / dV / dK products on 32x32x16 MFMAs (one wave's 32 keys x a 32-query half per
-// product, 32 MFMAs per query tile instead of 64 16x16x32: half the cycles they hold the wave's vector
-// issue), the row constants as the S / dP accumulators' start as before, the Q / dO images in swizzle
-// kind 1 (lds_swz_k)
-template <bool DROP, int KTW, bool PIPE, int SPL = 1, bool M32 = false>
+template <bool DROP, int KTW, bool PIPE, int SPL = 1>
 __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int blk, char* lds) {
-  static_assert(!M32 || (KTW == 2 && PIPE && SPL == 1), "32x32x16 form: 32 keys per wave, one query half set");
-  constexpr int SW = M32 ? 1 : 0;
   constexpr int KB = NW * 16 * KTW;  // keys per workgroup
   using C = AttnCfg<bf16>;
   constexpr int TILE = KV_QT * C::ROWB;
@@ -1291,45 +1225,25 @@ __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int 
 
   // K, V as B operands of S = Q' K^T and dP = dO V^T: lane holds X[kw0 + kt*16 + i][dk slots]
   bf16x8 kf[KTW][2], vf[KTW][2];
-  // M32: B operands of S = Q' K^T and dP = dO V^T, lane holds X[kw0 + (l & 31)][16c + 8h + j]
-  bf16x8 kf32[4], vf32[4];
-  if constexpr (M32) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      kf32[c] = row32_frag_gmem(Kg, ldk, kw0, Tk, 16 * c, lane);
-      vf32[c] = row32_frag_gmem(Vg, ldv, kw0, Tk, 16 * c, lane);
+  for (int kt = 0; kt < KTW; ++kt)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      kf[kt][s] = row_frag_gmem(Kg, ldk, kw0 + kt * 16, Tk, s * 32, lane);
+      vf[kt][s] = row_frag_gmem(Vg, ldv, kw0 + kt * 16, Tk, s * 32, lane);
     }
+  // consume K / V here, before the loop: otherwise the compiler places the wait for these loads at
+  // their first use inside the loop body, where it runs every ring cycle as a full vmcnt(0)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) asm volatile("" ::"v"(kf32[c]), "v"(vf32[c]));
-  } else {
+  for (int kt = 0; kt < KTW; ++kt)
 #pragma unroll
-    for (int kt = 0; kt < KTW; ++kt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        kf[kt][s] = row_frag_gmem(Kg, ldk, kw0 + kt * 16, Tk, s * 32, lane);
-        vf[kt][s] = row_frag_gmem(Vg, ldv, kw0 + kt * 16, Tk, s * 32, lane);
-      }
-    // consume K / V here, before the loop: otherwise the compiler places the wait for these loads at
-    // their first use inside the loop body, where it runs every ring cycle as a full vmcnt(0)
-#pragma unroll
-    for (int kt = 0; kt < KTW; ++kt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(kf[kt][s]), "v"(vf[kt][s]));
-  }
+    for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(kf[kt][s]), "v"(vf[kt][s]));
 
   f32x4 dk[KTW][4], dv[KTW][4];
-  f32x16 dk32[2], dv32[2];  // M32: X[kw0 + (e & 3) + 8 (e >> 2) + 4h][32 dc + (l & 31)]
-  if constexpr (M32) {
 #pragma unroll
-    for (int dc = 0; dc < 2; ++dc)
+  for (int kt = 0; kt < KTW; ++kt)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) dk32[dc][e] = dv32[dc][e] = 0.f;
-  } else {
-#pragma unroll
-    for (int kt = 0; kt < KTW; ++kt)
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dk[kt][dt] = dv[kt][dt] = zero4();
-  }
+    for (int dt = 0; dt < 4; ++dt) dk[kt][dt] = dv[kt][dt] = zero4();
 
   auto ring = [&](auto bi) -> char* {
     constexpr int BI = decltype(bi)::value;
@@ -1346,8 +1260,8 @@ __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int 
   // (wave 1; -inf past Tq) and dP start (wave 2) rows and the keep-bit words (wave 3, with dropout):
   // D = 4 DMA instructions per wave, 5 for waves 1, 2 and (with dropout) 3
   Rows64 rq, rdo;
-  rq.template init<SW>(Qg, ldq, Tq, w, lane);
-  rdo.template init<SW>(dOg, lddo, Tq, w, lane);
+  rq.init(Qg, ldq, Tq, w, lane);
+  rdo.init(dOg, lddo, Tq, w, lane);
   // the wave's fifth piece: wave 1 the lse row constants, wave 2 the delta ones (lanes 0..15 cover the
   // tile's 64 floats, the other lanes repeat them), wave 3 the keep bits, the rest a dummy delta row
   const bool xmask = DROP && w == 3;
@@ -1382,8 +1296,8 @@ __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int 
                 (uint32_t)qs0 * rdo.rowbytes, pq);
       dma16b(srd_x, vo_x, (uint32_t)qs0 * bpr_x, t + xo);
     } else {  // partial tile: clamped rows, -inf S start past Tq
-      dma_rows64<SW>(Qg, ldq, qs0, Tq, buf, w, lane);
-      dma_rows64<SW>(dOg, lddo, qs0, Tq, buf + TILE, w, lane);
+      dma_rows64(Qg, ldq, qs0, Tq, buf, w, lane);
+      dma_rows64(dOg, lddo, qs0, Tq, buf + TILE, w, lane);
       const int q = qs0 + lane;
       if (xmask) {
         const int r = (lane >> 3) & ((KB / 64) * 4 - 1), cch = (lane & 7) ^ ((lane >> 4) & 1);
@@ -1495,90 +1409,7 @@ __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int 
       }
       RP_PRIO(0);
     };
-    if constexpr (M32) {
-      const int h = lane >> 5;
-      // one half = 32 queries: S and dP (4 + 4 MFMAs), C started at the row constants: register e holds
-      // query 32 hf + (e & 3) + 8 (e >> 2) + 4h
-      auto sdp32 = [&](int hf, f32x16& s, f32x16& dp) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const f32x4 nl = *reinterpret_cast<const f32x4*>(lrow + 32 * hf + 8 * b + 4 * h);
-          const f32x4 nd = *reinterpret_cast<const f32x4*>(drow + 32 * hf + 8 * b + 4 * h);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            s[4 * b + e] = nl[e];
-            dp[4 * b + e] = nd[e];
-          }
-        }
-        RP_PRIO(1);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const bf16x8 qa = row32_frag_lds<SW>(Ql, 32 * hf, 16 * c, lane);
-          const bf16x8 da = row32_frag_lds<SW>(dOl, 32 * hf, 16 * c, lane);
-          s = mfma32(qa, kf32[c], s);
-          dp = mfma32(da, vf32[c], dp);
-        }
-        RP_PRIO(0);
-      };
-      // P and dS of the lane's key (kw0 + (l & 31)), packed as the A operands of dV / dK (registers
-      // 8c .. 8c + 7 = queries 16c + 4h + {0..3} and 16c + 8 + 4h + {0..3} of the half)
-      auto prob32 = [&](int hf, f32x16& s, f32x16& dp, bf16x8 (&pa)[2], bf16x8 (&sa)[2]) {
-        const int kw = w * 32 + (lane & 31), ko = kw & 63;
-        const int mrow_l = (kw >> 6) * 4 + ((ko & 15) >> 2);
-        const int bit = (ko >> 4) * 4 + (ko & 3);
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int qrow = 32 * hf + 8 * b + 4 * h;
-          uint2 bits = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-          f32x4 nd = zero4();
-          if constexpr (DROP) {
-            nd = *reinterpret_cast<const f32x4*>(drow + qrow);
-            bits = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(mw) + mrow_l * (KV_QT * 2) +
-                                                   ((((qrow >> 3) ^ ((mrow_l >> 1) & 1)) << 4) | ((qrow & 7) << 1)));
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * b + e;
-            const float pr = rp_exp2(s[r]);
-            if constexpr (DROP) {
-              const uint32_t km = keep_mask(e < 2 ? bits.x : bits.y, bit + 16 * (e & 1));
-              s[r] = bfi_select(km, pr, 0.f);
-              dp[r] = pr * bfi_select(km, dp[r], nd[e]);
-            } else {
-              s[r] = pr;
-              dp[r] = pr * dp[r];
-            }
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          pa[c] = pack8_32(s, c);
-          sa[c] = pack8_32(dp, c);
-        }
-      };
-      // dV += P^T dO, dK += dS^T Q' over the half's 32 queries (2 d-halves x 2 query chunks each)
-      auto dvdk32 = [&](int hf, const bf16x8 (&pa)[2], const bf16x8 (&sa)[2]) {
-        RP_PRIO(1);
-#pragma unroll
-        for (int dc = 0; dc < 2; ++dc)
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const bf16x8 dob = col32_frag_lds<SW>(dOl, 32 * hf + 16 * c, 32 * dc, lane);
-            const bf16x8 qb = col32_frag_lds<SW>(Ql, 32 * hf + 16 * c, 32 * dc, lane);
-            dv32[dc] = mfma32(pa[c], dob, dv32[dc]);
-            dk32[dc] = mfma32(sa[c], qb, dk32[dc]);
-          }
-        RP_PRIO(0);
-      };
-      f32x16 s0, dp0, s1, dp1;
-      bf16x8 pa0[2], sa0[2], pa1[2], sa1[2];
-      sdp32(0, s0, dp0);
-      sdp32(1, s1, dp1);
-      prob32(0, s0, dp0, pa0, sa0);
-      dvdk32(0, pa0, sa0);
-      prob32(1, s1, dp1, pa1, sa1);
-      dvdk32(1, pa1, sa1);
-    } else if constexpr (PIPE) {
+    if constexpr (PIPE) {
       // both halves' S / dP products are issued before the first half's VALU, so the VALU of half 0
       // runs beside the MFMAs of half 1 and the VALU of half 1 beside the dV / dK MFMAs of half 0
       f32x4 s0[2][KTW], dp0[2][KTW], nd0[2], s1[2][KTW], dp1[2][KTW], nd1[2];
@@ -1639,20 +1470,6 @@ __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int 
   const bool st_k = SPL == 1 || hv == 0, st_v = SPL == 1 || hv == 1;
   bf16* dK = (bf16*)a.dk + (int64_t)b * Tk * a.lddk + h * HD;
   bf16* dV = (bf16*)a.dv + (int64_t)b * Tk * a.lddv + h * HD;
-  if constexpr (M32) {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int key = kw0 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-      if (key >= Tk) continue;
-      const bool ok = kvalid[(int64_t)b * Tk + key] != 0;
-#pragma unroll
-      for (int dc = 0; dc < 2; ++dc) {
-        rp_st(dK + (int64_t)key * a.lddk + 32 * dc + (lane & 31), ok ? dk32[dc][e] * (1.f / LOG2E) : 0.f);
-        rp_st(dV + (int64_t)key * a.lddv + 32 * dc + (lane & 31), ok ? dv32[dc][e] : 0.f);
-      }
-    }
-    return;
-  }
 #pragma unroll
   for (int kt = 0; kt < KTW; ++kt)
 #pragma unroll
@@ -2318,12 +2135,12 @@ __global__ __launch_bounds__(NT * SPL, 2 / SPL) void attn_bwd_q_dma_kernel(MhaDe
 // as eight-wave split workgroups one per CU: here 512 four-wave workgroups two per CU, the dQ blocks
 // beside the dK/dV ones, with no partial merge and no cross-stream wait (RP_ATTN_BWD_OVERLAP: 42-68 us).
 constexpr int ROLES_LDS = 3 * KV_DMA_BUF > QD_DMA_LDS(1) ? 3 * KV_DMA_BUF : QD_DMA_LDS(1);
-template <bool DROP, bool M32 = false>
+template <bool DROP>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_roles_kernel(MhaDev a, int nkv) {
   __shared__ __attribute__((aligned(1024))) char lds[ROLES_LDS];
   const int blk = blockIdx.x;
   if (blk < nkv)
-    attn_bwd_kv_dma_body<DROP, 2, true, 1, M32>(a, blk, lds);
+    attn_bwd_kv_dma_body<DROP, 2, true, 1>(a, blk, lds);
   else
     attn_bwd_q_dma_body<DROP, 1, false>(a, blk - nkv, lds);
 }
@@ -2864,11 +2681,10 @@ int launch_mha_bwd(int phases, const MhaDev& a, hipStream_t s) {
       hipLaunchKernelGGL(attn_delta_kernel<T>, delta_grid<T>(a), dim3(256), 0, s, a);
     const int nkv = nkb * a.B * a.H;
     const dim3 grid((unsigned)(nkv + (a.Tq + FW_QB - 1) / FW_QB * a.B * a.H));
-    const char* e32 = getenv("RP_ATTN_KV32");
-    const bool m32 = e32 && e32[0] == '1';
-    void (*kern)(MhaDev, int) = a.drop_thresh ? (m32 ? attn_bwd_roles_kernel<true, true> : attn_bwd_roles_kernel<true, false>)
-                                              : (m32 ? attn_bwd_roles_kernel<false, true> : attn_bwd_roles_kernel<false, false>);
-    hipLaunchKernelGGL(kern, grid, dim3(NT), 0, s, a, nkv);
+    if (a.drop_thresh)
+      hipLaunchKernelGGL(attn_bwd_roles_kernel<true>, grid, dim3(NT), 0, s, a, nkv);
+    else
+      hipLaunchKernelGGL(attn_bwd_roles_kernel<false>, grid, dim3(NT), 0, s, a, nkv);
     return rp_check_launch("rp_mha_bwd");
   }
   // dQ: 128-query blocks unless that leaves fewer than one workgroup per CU (then 64, as the forward)

@@ -717,17 +717,14 @@ def test_gemm_64_row_tiles_bitwise(dev, monkeypatch, M):
 
 
 @pytest.mark.parametrize("B,T,qpre,roles", [(8, 2048, False, "1"), (8, 2048, True, "1"), (8, 2048, True, "0"),
-                                            (1, 4096, True, "1"), (8, 2048, True, "32"), (1, 4096, True, "32")])
+                                            (1, 4096, True, "1")])
 def test_attention_metric_shape_bf16_dropout(dev, monkeypatch, B, T, qpre, roles):
     """Attention at the bench shape (B = 8, T = 2048, H = 8, dk = 64) and at config 4's (B = 1, T = 4096)
     with dropout 0.1 and ragged key padding: forward output and all three gradients against an fp64
     torch restatement (same bf16 inputs, the restated keep bits) on a sample of (batch, head) pairs.
     With the producer's Q prescale (qpre, what the model runs) the shipping LDS-DMA kernels run: the
     delta pass and the two-role launch (attn_bwd_roles_kernel) at both shapes — asserted — and with
-    RP_ATTN_ROLES=0 the fused-delta dQ kernel then the 128-key dK/dV kernel (the per-phase form);
-    "32": the two-role launch with its dK/dV blocks on 32x32x16 MFMAs (RP_ATTN_KV32=1)."""
-    monkeypatch.setenv("RP_ATTN_KV32", "1" if roles == "32" else "0")
-    roles = "1" if roles == "32" else roles
+    RP_ATTN_ROLES=0 the fused-delta dQ kernel then the 128-key dK/dV kernel (the per-phase form)."""
     monkeypatch.setenv("RP_ATTN_ROLES", roles)
     H = 8
     qkv0 = rnd(B * T, 3 * H * 64, dev=dev, seed=21).to(torch.bfloat16)
@@ -764,17 +761,14 @@ def test_attention_metric_shape_bf16_dropout(dev, monkeypatch, B, T, qpre, roles
         assert torch.count_nonzero(dk[bb, hh][~valid]) == 0 and torch.count_nonzero(dv[bb, hh][~valid]) == 0
 
 
-@pytest.mark.parametrize("kv32", ["0", "1"])
 @pytest.mark.parametrize("B,T,p", [(1, 4096, 0.1), (1, 4096, 0.0), (2, 2048, 0.1), (1, 4000, 0.1)])
-def test_attention_bwd_roles_matches_two_kernels(dev, monkeypatch, B, T, p, kv32):
+def test_attention_bwd_roles_matches_two_kernels(dev, monkeypatch, B, T, p):
     """The two-role backward (one launch: dK/dV blocks and dQ blocks side by side, delta formed by its
     own pass; chosen where each grid alone fills the CUs once but not twice — config 4) against the
     two-kernel form (RP_ATTN_ROLES=0: fused-delta dQ, then dK/dV, as eight-wave split workgroups), Q
     prescaled, ragged keys: equal up to delta's rounding, and bitwise repeatable.  Also the key-padded
-    T = 4000 (a partial last 128-block on both sides) and B = 2, T = 2048 (grids of 256 too); kv32: the
-    two-role launch's dK/dV blocks on 32x32x16 MFMAs."""
+    T = 4000 (a partial last 128-block on both sides) and B = 2, T = 2048 (grids of 256 too)."""
     H = 8
-    monkeypatch.setenv("RP_ATTN_KV32", kv32)
     qkv = rnd(B * T, 3 * H * 64, dev=dev, seed=41).to(torch.bfloat16)
     qkv[:, :H * 64] = (qkv[:, :H * 64].float() * (0.125 * K.LOG2E)).to(torch.bfloat16)
     lens = torch.tensor([T, T - 77][:B], device=dev)
