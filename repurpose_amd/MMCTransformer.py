@@ -471,20 +471,19 @@ class _Schedule:
         # graph capture (graph.py): the model's device seed word, passed to every dropout launch
         self.sb = model._seed_base
         self.saved = None
-        # bf16 at d_model 512: GEMM + LayerNorm seams as single launches (rp_gemm_ln_*).  On 128 x 128 tiles
-        # whose four column tiles exchange the row statistics (kernels._lnx_ws) when M % 128 == 0, else
-        # the 64 x 512 full-row kernels (bitwise the unfused pairs, but streaming the whole weight per 64
-        # rows at one workgroup per CU: +0.17 ms per step at the bench shape).  RP_GEMM_LN: auto (default:
-        # the exchange kernels where their grid fills every CU — bench shape 14.93 -> 14.39 ms per step,
-        # config 2 (one tile per CU) 7.40 -> 7.10 ms; config 4's half-filled grid
-        # keeps the unfused pairs on 32-row GEMM tiles: forced there 7.14 -> 7.24 ms), 1 both directions,
-        # fwd / bwd one, 0 none
+        # bf16 at d_model 512: GEMM + LayerNorm seams as single launches (rp_gemm_ln_*).  On 128 x 128 (or
+        # 64 x 128) tiles whose four column tiles exchange the row statistics (kernels._lnx_ws); with
+        # RP_GEMM_LNX=0 the 64 x 512 full-row kernels (bitwise the unfused pairs, but streaming the whole
+        # weight per 64 rows at one workgroup per CU: +0.17 ms per step at the bench shape).  RP_GEMM_LN:
+        # auto (default: the exchange kernels where their grid gives every CU a workgroup — bench shape
+        # 14.93 -> 14.39 ms per step, config 2 7.40 -> 7.10 ms, config 4 on 64-row tiles, DESIGN.md §8
+        # round 5), 1 both directions, fwd / bwd one, 0 none
         ln = os.environ.get("RP_GEMM_LN", "auto")
         ok = self.dt == torch.bfloat16 and self.M % 64 == 0 and model.d_model == 512
         if ln == "auto":
             dev = model._flat.device
             cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
-            ln = "1" if (self.M % 128 == 0 and cus > 0 and (self.M // 128) * 4 >= cus
+            ln = "1" if (self.M % 64 == 0 and cus > 0 and (self.M // 64) * 4 >= cus
                          and os.environ.get("RP_GEMM_LNX", "1") == "1") else "0"
         self.fused_ln_fwd = ok and ln in ("1", "fwd")
         self.fused_ln = ok and ln in ("1", "bwd")

@@ -2116,15 +2116,18 @@ __global__ __launch_bounds__(GL_NT, 1) void gemm_ln_bwd_kernel(int64_t M, int64_
 // dispatched.  x_out is bitwise the unfused GEMM's; h / mean / rstd / dx agree with the unfused
 // LayerNorm to fp32 rounding of the row sums (associated per column tile, not per lane).
 constexpr int LX_TN = GL_N / BN;  // column tiles of a 512-wide row
-// Workspace: a 256-byte error word, then one record per row block (its layout independent of M, so
-// launches of any row counts can share the workspace): arrive / done counters, 248 bytes of padding,
+// Workspace: a 256-byte error word, then one record per 128 rows (its layout independent of M and of the
+// tile height, so launches of any row counts and either kernel can share the workspace): two pairs of
+// arrive / done counters (one per 64-row block: the 128-row tiles use the first), 240 bytes of padding,
 // then the [LX_TN][128] per-row partial pairs.
 constexpr int64_t LX_REC = 256 + LX_TN * BM * 8;
 struct LnxWs {
   uint32_t* err;  // 1 when a wait gave up (never in a correct launch)
-  char* rec;      // row block rb's record at rec + rb * LX_REC
-  __device__ uint32_t* cnt(int rb) const { return (uint32_t*)(rec + rb * LX_REC); }
-  __device__ f32x2* part(int rb) const { return (f32x2*)(rec + rb * LX_REC + 256); }
+  char* rec;      // rows [128 r, 128 r + 128): record r at rec + r * LX_REC
+  // the arrive / done counters of the row block (tile row group) that starts at row m0
+  __device__ uint32_t* cnt(int64_t m0) const { return (uint32_t*)(rec + (m0 / BM) * LX_REC) + 2 * ((m0 / 64) & 1); }
+  // row m's pair of column tile 0 (column tile nt's at + nt * BM)
+  __device__ f32x2* part(int64_t m) const { return (f32x2*)(rec + (m / BM) * LX_REC + 256) + m % BM; }
 };
 
 __device__ __forceinline__ void lx_store_sc1(f32x2* p, f32x2 v) {
@@ -2146,15 +2149,15 @@ __device__ __forceinline__ void lx_load_sc1(const f32x2* base, f32x2 (&o)[LX_TN]
 }
 
 // every thread, after its payload stores: drain them, arrive, wait for the row block's column tiles
-__device__ __forceinline__ void lx_drain_arrive(const LnxWs& ws, int rb, int tid) {
+__device__ __forceinline__ void lx_drain_arrive(uint32_t* cnt, int tid) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) __hip_atomic_fetch_add(ws.cnt(rb), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void lx_wait(const LnxWs& ws, int rb, int tid) {
+__device__ __forceinline__ void lx_wait(const LnxWs& ws, uint32_t* cnt, int tid) {
   if (tid == 0) {
     uint32_t n = 0;
-    while (__hip_atomic_load(ws.cnt(rb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)LX_TN) {
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)LX_TN) {
       __builtin_amdgcn_s_sleep(1);
       if (++n > (1u << 24)) {
         __hip_atomic_store(ws.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2165,9 +2168,8 @@ __device__ __forceinline__ void lx_wait(const LnxWs& ws, int rb, int tid) {
   __syncthreads();
 }
 // after a barrier that follows every thread's partner reads: the last of the four resets the counters
-__device__ __forceinline__ void lx_done(const LnxWs& ws, int rb, int tid) {
+__device__ __forceinline__ void lx_done(uint32_t* c, int tid) {
   if (tid == 0) {
-    uint32_t* c = ws.cnt(rb);
     if (__hip_atomic_fetch_add(c + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(LX_TN - 1)) {
       __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(c + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2178,6 +2180,10 @@ __device__ __forceinline__ void lx_done(const LnxWs& ws, int rb, int tid) {
 // Cross-lane sums on the VALU (DPP lane moves + one v_permlane16_swap) instead of __shfl_xor, which
 // compiles to ds_bpermute: an LDS round trip per step, five dependent ones for a 32-lane sum
 __device__ __forceinline__ float lx_sum2(float v) { return v + rp_dpp<0xB1>(v); }  // lanes l, l ^ 1
+__device__ __forceinline__ float lx_sum4(float v) {  // the lane's quad
+  v += rp_dpp<0xB1>(v);
+  return v + rp_dpp<0x4E>(v);
+}
 // the sum over the 32 lanes of the lane's half-wave, in every lane of it
 __device__ __forceinline__ float lx_sum32(float v) {
   v += rp_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
@@ -2188,27 +2194,32 @@ __device__ __forceinline__ float lx_sum32(float v) {
   return __uint_as_float(a[0]) + __uint_as_float(a[1]);  // rows 0 + 1 (2 + 3)
 }
 
-__device__ __forceinline__ void lx_stage(const f32x4 (&acc)[4][4], float* cs, int lane, int wm, int wn) {
+// dma_mainloop's (32 MI) x 128 accumulator tile -> cs[row][CST]
+template <int MI>
+__device__ __forceinline__ void lx_stage(const f32x4 (&acc)[MI][4], float* cs, int lane, int wm, int wn) {
   const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cs[(wm * 64 + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r)
+        cs[(wm * (MI * 16) + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
 }
 
 constexpr int LX_CPR = BN / 4;  // float4 chunks per tile row (a half-wave)
 static_assert(DmaCfg<0>::LDS <= CTILE_BYTES, "main loop fits the staging area");
 // An exchange epilogue over a staged TR x 128 tile with TNT threads: thread tid owns chunk column
-// tid % 32 of the rows tid / 32 + RS it, it < IT.  Row m0 + row's partials go to record
-// m0 / 128 + row / 128; the four column tiles arrive on record m0 / 128's counter.
+// tid % 32 of the rows tid / 32 + RS it, it < IT; the forward's row statistics take TPR threads per row.
+// Row m's partials go to its record (LnxWs::part); the four column tiles of rows [m0, m0 + TR) arrive on
+// LnxWs::cnt(m0).
 template <int TR, int TNT>
 struct LxG {
   static constexpr int RS = TNT / LX_CPR;                // rows per chunk step
   static constexpr int IT = TR / RS;                     // chunks per thread
+  static constexpr int TPR = TNT / TR;                   // threads per row (forward statistics)
   static constexpr int LDS = TR * CST * 4 + 4 * TR * 4;  // staged tile, per-row totals, (bwd) mean / rstd
-  static_assert(TNT == 2 * TR && TR % BM == 0, "two threads per row, whole records");
+  static_assert((TPR == 2 || TPR == 4) && TR % 64 == 0 && TR <= BM, "row statistics lanes, row blocks");
 };
 constexpr int LX_IT = LxG<BM, NT>::IT;  // 16: row = tid / 32 + 8 it
 
@@ -2312,7 +2323,8 @@ __device__ __forceinline__ void lx_fwd_tail(const GlnDev& a, const LnxWs& ws, in
                                             float* cs, const float4 (&r)[LxG<TR, TNT>::IT], int tid) {
   using L = LxG<TR, TNT>;
   float* st = cs + TR * CST;  // per-row mean, rstd
-  const int rb = (int)(m0 / BM), cc = (tid % LX_CPR) * 4;
+  uint32_t* const cnt = ws.cnt(m0);
+  const int cc = (tid % LX_CPR) * 4;
   // x_out = dropout(acc + bias) + residual: gemm_epilogue's RESB arithmetic, op for op
   const float4 bi = *reinterpret_cast<const float4*>(a.bias + n0 + cc);
   const uint32_t dseed = a.drop_thresh ? rp_seed_eff(a.seed_base, a.drop_seed) : 0u;
@@ -2334,33 +2346,35 @@ __device__ __forceinline__ void lx_fwd_tail(const GlnDev& a, const LnxWs& ws, in
     *reinterpret_cast<float4*>(c) = o;
   }
   __syncthreads();
-  // the tile's per-row (sum, M2): two threads per row, 64 columns each
-  const int row = tid >> 1, hf = tid & 1;
-  f32x2* rec = ws.part(rb + row / BM) + row % BM;  // the row's pair of column tile 0
+  // the tile's per-row (sum, M2): TPR threads per row (adjacent lanes), 128 / TPR columns each
+  constexpr int CPT = BN / L::TPR / 4;  // float4 chunks per thread
+  const int row = tid / L::TPR, hf = tid % L::TPR;
+  f32x2* rec = ws.part(m0 + row);  // the row's pair of column tile 0
+  auto lane_sum = [](float v) { return L::TPR == 2 ? lx_sum2(v) : lx_sum4(v); };
   {
-    const float* rr = cs + row * CST + hf * 64;
+    const float* rr = cs + row * CST + hf * (BN / L::TPR);
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < CPT; ++j) {
       const float4 q = *reinterpret_cast<const float4*>(rr + 4 * j);
       s += (q.x + q.y) + (q.z + q.w);
     }
-    s = lx_sum2(s);
+    s = lane_sum(s);
     const float mk = s * (1.f / BN);
     float q2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < CPT; ++j) {
       const float4 q = *reinterpret_cast<const float4*>(rr + 4 * j);
       const float d0 = q.x - mk, d1 = q.y - mk, d2 = q.z - mk, d3 = q.w - mk;
       q2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
     }
-    q2 = lx_sum2(q2);
+    q2 = lane_sum(q2);
     if (hf == 0) lx_store_sc1(rec + nt * BM, f32x2{s, q2});
   }
   LX_STAMP(2);
-  lx_drain_arrive(ws, rb, tid);
+  lx_drain_arrive(cnt, tid);
   LX_STAMP(3);
-  lx_wait(ws, rb, tid);
+  lx_wait(ws, cnt, tid);
   LX_STAMP(4);
   if (hf == 0) {
     f32x2 o[LX_TN];
@@ -2376,7 +2390,7 @@ __device__ __forceinline__ void lx_fwd_tail(const GlnDev& a, const LnxWs& ws, in
     st[TR + row] = rsqrtf(m2 * (1.f / GL_N) + a.eps);
   }
   __syncthreads();
-  lx_done(ws, rb, tid);
+  lx_done(cnt, tid);
   // h = LayerNorm(x_out): ln_fwd_kernel's (v - mean) * rstd * gamma + beta, 8 columns per thread
   const int c8 = (tid % (BN / 8)) * 8;
   float gm[8], bt[8];
@@ -2411,7 +2425,8 @@ __device__ __forceinline__ void lx_bwd_tail(const GlnDev& a, const LnxWs& ws, in
   using L = LxG<TR, TNT>;
   float* st = cs + TR * CST;  // per-row s1 / 512, s2 / 512
   const float* mr = st + 2 * TR;
-  const int rb = (int)(m0 / BM), cc = (tid % LX_CPR) * 4, r0 = tid / LX_CPR;
+  uint32_t* const cnt = ws.cnt(m0);
+  const int cc = (tid % LX_CPR) * 4, r0 = tid / LX_CPR;
   const float4 gm = *reinterpret_cast<const float4*>(a.gamma + n0 + cc);
   const float gam[4] = {gm.x, gm.y, gm.z, gm.w};
   float pg[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f};  // the tile's gamma / beta partials
@@ -2436,26 +2451,26 @@ __device__ __forceinline__ void lx_bwd_tail(const GlnDev& a, const LnxWs& ws, in
     static_assert(LX_CPR == 32, "a row's chunks fill a half-wave");
     s1 = lx_sum32(s1);
     s2 = lx_sum32(s2);
-    if ((tid % LX_CPR) == 0) lx_store_sc1(ws.part(rb + row / BM) + nt * BM + row % BM, f32x2{s1, s2});
+    if ((tid % LX_CPR) == 0) lx_store_sc1(ws.part(m0 + row) + nt * BM, f32x2{s1, s2});
   }
   LX_STAMP(2);
-  lx_drain_arrive(ws, rb, tid);
+  lx_drain_arrive(cnt, tid);
   LX_STAMP(3);
   float4 dr[L::IT];  // the residual gradient, in flight while the row block gathers
   if (a.dres) {
 #pragma unroll
     for (int it = 0; it < L::IT; ++it) dr[it] = rp_ld16f(a.dres + (m0 + r0 + it * L::RS) * a.lddres + n0 + cc, 2);
   }
-  lx_wait(ws, rb, tid);
+  lx_wait(ws, cnt, tid);
   LX_STAMP(4);
   if (tid < TR) {
     f32x2 o[LX_TN];
-    lx_load_sc1(ws.part(rb + tid / BM) + tid % BM, o);
+    lx_load_sc1(ws.part(m0 + tid), o);
     st[tid] = ((o[0].x + o[1].x) + (o[2].x + o[3].x)) * (1.f / GL_N);
     st[TR + tid] = ((o[0].y + o[1].y) + (o[2].y + o[3].y)) * (1.f / GL_N);
   }
   __syncthreads();
-  lx_done(ws, rb, tid);
+  lx_done(cnt, tid);
   const uint32_t lseed = a.lp_thresh ? rp_seed_eff(a.seed_base, a.lp_seed) : 0u;
 #pragma unroll
   for (int it = 0; it < L::IT; ++it) {
@@ -2586,6 +2601,47 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
   if (tid < 2 * BM) mr[tid] = mrv;
   __syncthreads();
   lx_bwd_tail<BM, NT>(a, ws, m0, n0, nt, cs, xh, tid);
+}
+
+// 64 x 128 exchange tiles (dma_mainloop MI = 2, each wave 32 x 64) for grids whose 128-row tiles would
+// leave CUs idle (config 4, M = 4096: 128 -> 256 workgroups): the same epilogue tails — the forward's row
+// statistics four threads per row — on the 64-row block's own counters (LnxWs::cnt)
+constexpr int LX64_LDS = dma_tile_lds<0, 2>() > LxG<64, NT>::LDS ? dma_tile_lds<0, 2>() : LxG<64, NT>::LDS;
+template <bool FWD>
+__global__ __launch_bounds__(NT, 2) void gemm_lnx64_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws) {
+  __shared__ __attribute__((aligned(16))) char lds[LX64_LDS];
+  using L = LxG<64, NT>;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int t = rp_xcd_remap(blockIdx.x, (int)gridDim.x);
+  const int nt = t % LX_TN;
+  const int64_t m0 = (int64_t)(t / LX_TN) * 64, n0 = (int64_t)nt * BN;
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[8];
+  dma_mainloop<true, FWD, 0, 2>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane, wid,
+                                wm, wn);
+  // the epilogue's fp32 operand (fwd: the residual, bwd: x), and (bwd) the rows' mean / rstd
+  const float* src = FWD ? a.residual : a.x;
+  const int64_t ld = FWD ? a.ldr : a.ldx;
+  const int cc = (tid % LX_CPR) * 4, r0 = tid / LX_CPR;
+  float4 xr[L::IT];
+#pragma unroll
+  for (int it = 0; it < L::IT; ++it) xr[it] = rp_ld16f(src + (m0 + r0 + it * L::RS) * ld + n0 + cc, 2);
+  float mrv = 0.f;
+  if (!FWD && tid < 128) mrv = tid < 64 ? a.mean[m0 + tid] : a.rstd[m0 + tid - 64];
+  float* cs = reinterpret_cast<float*>(lds);  // dma_mainloop ended on a barrier: its stages are free
+  lx_stage<2>(acc, cs, lane, wm, wn);
+  if (!FWD && tid < 128) cs[64 * CST + 2 * 64 + tid] = mrv;
+  __syncthreads();
+  if constexpr (FWD)
+    lx_fwd_tail<64, NT>(a, ws, m0, n0, nt, cs, xr, tid);
+  else
+    lx_bwd_tail<64, NT>(a, ws, m0, n0, nt, cs, xr, tid);
 }
 }  // namespace
 
@@ -2785,6 +2841,18 @@ extern "C" int64_t rp_gemm_ln_xchg_bytes(int64_t M) {
 }
 static LnxWs lnx_ws(void* base, int64_t) { return LnxWs{(uint32_t*)base, (char*)base + 256}; }
 
+// Exchange tile height: 128 where the 128-row grid gives every CU two workgroups, else 64 (M is a
+// multiple of 64).  Interleaved whole-step A/B (profiles/r05_lnx64_ab.txt): bench shape (M = 16384)
+// 13.98 ms on 128-row tiles vs 15.11 on 64-row ones; config 2 (M = 8192, one 128-row tile per CU) 7.11
+// vs 7.04; config 4 (M = 4096) 7.03 on 64-row tiles vs 7.12 unfused.  RP_LNX_ROWS = 64 | 128 (A/B,
+// read per launch) prefers that height where M allows it.
+static int lnx_rows(int64_t M) {
+  const char* e = getenv("RP_LNX_ROWS");
+  if (e && e[0] == '6') return 64;
+  if (e && e[0] == '1') return M % 128 == 0 ? 128 : 64;
+  return (M % 128 == 0 && (M / 128) * LX_TN >= 2 * gemm_cu_count()) ? 128 : 64;
+}
+
 static int gemm_ln_common(const char* fn, int64_t M, int64_t K, const rp_gemm_ln_args* p, GlnDev& d) {
   RP_REQUIRE(p, "%s: null args", fn);
   RP_REQUIRE(M >= 0 && K > 0 && M % GL_BM == 0 && K % GL_BK == 0, "%s: M must be a multiple of 64 and K of 64 (M=%lld K=%lld)",
@@ -2822,7 +2890,12 @@ extern "C" int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   d.xo = p->x_out; d.ldxo = p->ldx_out;
   d.h = (bf16*)p->h_out; d.ldh = p->ldh;
   if (M == 0) return RP_OK;
-  if (p->xchg && M % BM == 0) {
+  if (p->xchg && lnx_rows(M) == 64) {
+    hipLaunchKernelGGL(gemm_lnx64_kernel<true>, dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M,
+                       K, d, lnx_ws(p->xchg, M));
+    return rp_check_launch("rp_gemm_ln_fwd");
+  }
+  if (p->xchg) {
     hipLaunchKernelGGL(gemm_lnx_fwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
                        lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * LX_PFS ? 1 : 0);
     return rp_check_launch("rp_gemm_ln_fwd");
@@ -2852,7 +2925,12 @@ extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   d.lp_seed = p->lp_seed;
   d.dgamma_part = p->dgamma_part; d.dbeta_part = p->dbeta_part; d.ld_part = p->ld_part;
   if (M == 0) return RP_OK;
-  if (p->xchg && M % BM == 0) {
+  if (p->xchg && lnx_rows(M) == 64) {
+    hipLaunchKernelGGL(gemm_lnx64_kernel<false>, dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M,
+                       K, d, lnx_ws(p->xchg, M));
+    return rp_check_launch("rp_gemm_ln_bwd");
+  }
+  if (p->xchg) {
     hipLaunchKernelGGL(gemm_lnx_bwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
                        lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * LX_PFS ? 1 : 0);
     return rp_check_launch("rp_gemm_ln_bwd");

@@ -205,13 +205,14 @@ _LNX = {}
 
 
 def _lnx_ws(dev, M):
-    """The exchange workspace of the 128 x 128 GEMM + LayerNorm kernels (rp_gemm_ln_xchg_bytes, zero-filled
-    once; every launch leaves it zeroed), one per device, grown as needed.  Launches sharing it must be
-    ordered: the drop-in issues every seam on the device's current stream (a captured step replays on
-    the stream its eager steps use), so one per device suffices — and the capture stream does not get a
-    workspace of its own, whose zero fill would be captured into every replay.  RP_GEMM_LNX=0 (A/B) or
-    M % 128 != 0: None, i.e. the 64-row full-row kernels."""
-    if M % 128 or os.environ.get("RP_GEMM_LNX", "1") != "1":
+    """The exchange workspace of the GEMM + LayerNorm exchange kernels (128 x 128 tiles, or 64 x 128 where
+    the 128-row grid would leave CUs idle; rp_gemm_ln_xchg_bytes, zero-filled once; every launch leaves
+    it zeroed), one per device, grown as needed.  Launches sharing it must be ordered: the drop-in issues
+    every seam on the device's current stream (a captured step replays on the stream its eager steps
+    use), so one per device suffices — and the capture stream does not get a workspace of its own, whose
+    zero fill would be captured into every replay.  RP_GEMM_LNX=0 (A/B): None, i.e. the 64-row full-row
+    kernels."""
+    if M % 64 or os.environ.get("RP_GEMM_LNX", "1") != "1":
         return None
     need = int(N.load().rp_gemm_ln_xchg_bytes(M))
     ws = _LNX.get(dev)
@@ -225,8 +226,7 @@ def linear_ln_fwd(x, W, b, residual, gamma, beta, eps=1e-5, dropout_p=0.0, seed=
     """One launch (rp_gemm_ln_fwd) for ``y = dropout(x W^T + b) + residual`` (fp32, returned) and
     ``h = LayerNorm(y)`` (bf16) with its mean / rstd — linear_fwd(..., residual=...) followed by
     layernorm_fwd(y, out_f32=False, lp_dtype=bf16): y bitwise; h / mean / rstd bitwise on the 64-row
-    kernels, to fp32 rounding of the row sums on the 128 x 128 exchange kernels (M % 128 == 0, the
-    default; RP_GEMM_LNX=0 A/B).  x [M, K] bf16, W [512, K] bf16, M % 64 == 0.  Returns (y, h, mean, rstd)."""
+    kernels, to fp32 rounding of the row sums on the exchange kernels (the default; RP_GEMM_LNX=0 A/B).  x [M, K] bf16, W [512, K] bf16, M % 64 == 0.  Returns (y, h, mean, rstd)."""
     _gpu(x, W, b, residual, gamma, beta)
     _seed_word(seed_base)
     M, K = x.shape

@@ -101,6 +101,14 @@ def test_model_fused_seams_bitwise(dev, monkeypatch):
     assert torch.equal(g0, g1), f"grads: {(g0 - g1).abs().max().item():.3e}"
 
 
+@pytest.fixture(params=["64", "128"])
+def lnx_rows(request, monkeypatch):
+    """The exchange tile height: 64 x 128 tiles (the host's choice where 128-row tiles would leave CUs
+    idle) or 128 x 128 ones (M % 128 == 0, else 64), RP_LNX_ROWS read per launch."""
+    monkeypatch.setenv("RP_LNX_ROWS", request.param)
+    return request.param
+
+
 def _ws_clean(dev, M):
     """The error word and the arrive / done counters of every row block are zero again (the partial
     pairs after them are data)."""
@@ -108,8 +116,9 @@ def _ws_clean(dev, M):
     assert ws is not None
     torch.cuda.synchronize()
     assert int(ws[:4].count_nonzero().item()) == 0, "an exchange wait gave up"
-    rec = 256 + 4 * 128 * 8  # one row block's record: counters (8 of 256 bytes), then its partial pairs
-    head = ws[256:256 + (M // 128) * rec].view(M // 128, rec)[:, :8]
+    rec = 256 + 4 * 128 * 8  # one 128-row record: two counter pairs (16 of 256 bytes), then its partial pairs
+    nr = (M + 127) // 128
+    head = ws[256:256 + nr * rec].view(nr, rec)[:, :16]
     assert int(head.count_nonzero().item()) == 0, "exchange counters not left zeroed"
 
 
@@ -122,8 +131,8 @@ def _close_bf16(u, v):
 
 
 @pytest.mark.parametrize("M,Kd,p", [(1024, 512, 0.0), (1024, 2048, 0.1), (16384, 512, 0.1), (16384, 2048, 0.1),
-                                    (128, 1536, 0.1)])
-def test_linear_ln_fwd_exchange(dev, M, Kd, p):
+                                    (128, 1536, 0.1), (4096, 512, 0.1), (192, 2048, 0.1)])
+def test_linear_ln_fwd_exchange(dev, lnx_rows, M, Kd, p):
     g = torch.Generator().manual_seed(M + Kd + 1)
     x, W = _r(g, M, Kd, dev=dev), _r(g, D, Kd, dev=dev, sc=0.03)
     b = _r(g, D, dev=dev, dt=torch.float32, sc=0.1)
@@ -144,9 +153,9 @@ def test_linear_ln_fwd_exchange(dev, M, Kd, p):
 
 
 @pytest.mark.parametrize("M,Kd,lp", [(1024, 2048, 0.1), (1024, 1536, 0.0), (16384, 2048, 0.1), (16384, 1536, 0.1),
-                                     (128, 512, 0.1)])
+                                     (128, 512, 0.1), (4096, 2048, 0.1), (192, 512, 0.0)])
 @pytest.mark.parametrize("with_lp", [True, False])
-def test_linear_ln_bwd_exchange(dev, M, Kd, lp, with_lp):
+def test_linear_ln_bwd_exchange(dev, lnx_rows, M, Kd, lp, with_lp):
     g = torch.Generator().manual_seed(3 * M + Kd + 1)
     dy, W = _r(g, M, Kd, dev=dev), _r(g, Kd, D, dev=dev, sc=0.03)
     x = _r(g, M, D, dev=dev, dt=torch.float32)
@@ -177,7 +186,7 @@ def test_linear_ln_bwd_exchange(dev, M, Kd, lp, with_lp):
     _ws_clean(dev, M)
 
 
-def test_model_fused_seams_exchange(dev, monkeypatch):
+def test_model_fused_seams_exchange(dev, lnx_rows, monkeypatch):
     """A bf16 training step with every seam on the exchange kernels: against the unfused bf16 step the
     loss and logits agree to bf16 rounding; against the fp32 step (dropout off) its gradients are as close
     as the unfused bf16 step's (within 1.25x: the two bf16 steps differ from each other by about as much
@@ -215,10 +224,13 @@ def test_model_fused_seams_exchange(dev, monkeypatch):
     _ws_clean(dev, 512)
 
 
-def test_linear_ln_exchange_mixed_rows(dev):
-    """One workspace shared by launches of different row counts (the record of a row block does not move
-    with M): each launch agrees with the unfused pair and leaves the counters zeroed."""
-    for M in (4096, 8192, 16384, 1024, 8192, 384):
+def test_linear_ln_exchange_mixed_rows(dev, monkeypatch):
+    """One workspace shared by launches of different row counts and tile heights (the record of a row
+    block does not move with M or the kernel): each launch agrees with the unfused pair and leaves the
+    counters zeroed."""
+    for M, rows in ((4096, "128"), (8192, "64"), (16384, "128"), (1024, "64"), (8192, "128"), (384, "64"),
+                    (4096, "64"), (320, "128")):
+        monkeypatch.setenv("RP_LNX_ROWS", rows)
         g = torch.Generator().manual_seed(M)
         x, W = _r(g, M, 512, dev=dev), _r(g, D, 512, dev=dev, sc=0.03)
         b, res = _r(g, D, dev=dev, dt=torch.float32, sc=0.1), _r(g, M, D, dev=dev, dt=torch.float32)
