@@ -909,21 +909,10 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
   constexpr int PPW = G::PR / 64;  // 64-row accumulator groups of a wave per pass
 #pragma unroll
   for (int pass = 0; pass < 256 / G::PR; ++pass) {
-    if (pass) __syncthreads();
-    if (wm == pass * G::PR / 128) {
-#pragma unroll
-      for (int i = 0; i < 4 * PPW; ++i)
-#pragma unroll
-        for (int j = 0; j < G::JT; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            cs[(i * 16 + g * 4 + r) * G::CST + wn * G::WN + j * 16 + cl] =
-                acc[((pass * G::PR / 64) & 1) * 4 + i][j][r];
-    }
-    __syncthreads();
     constexpr int ITER = G::PR * CPRO / NT8;
-    // fp32 C with a residual (the 256 x 128 tile's linear2 forward): the pass's residual chunks are
-    // loaded before its first store (inline, each load would wait behind the previous chunk's store)
+    // fp32 C with a residual (the 256 x 128 tile's linear2 forward) / a bf16 gate (linear2 dgrad): the
+    // pass's chunks are loaded before its staging (in flight across the staging and its barriers) and
+    // before its first store (inline, each load would wait behind the previous chunk's store)
     constexpr bool RESV = std::is_same<TC, float>::value && MODE == 0;
     float4 rv[RESV ? ITER : 1];
     if constexpr (RESV) {
@@ -947,6 +936,18 @@ __device__ __forceinline__ void gemm8_epilogue(const f32x4 (&acc)[8][BNT / 64], 
         if (m < M && n < N) gv[it] = *reinterpret_cast<const bf16x8*>((const bf16*)ep.gate + m * ep.ldg + n);
       }
     }
+    if (pass) __syncthreads();
+    if (wm == pass * G::PR / 128) {
+#pragma unroll
+      for (int i = 0; i < 4 * PPW; ++i)
+#pragma unroll
+        for (int j = 0; j < G::JT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cs[(i * 16 + g * 4 + r) * G::CST + wn * G::WN + j * 16 + cl] =
+                acc[((pass * G::PR / 64) & 1) * 4 + i][j][r];
+    }
+    __syncthreads();
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int id = tid + it * NT8;
