@@ -2770,10 +2770,21 @@ extern "C" int rp_gemm_attn_dout_delta(const void* dY, int64_t ldy, const void* 
   e.dH = H;
   e.dscale = dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f;
   // dO = dY W: k-major A = dY [M, K], B = W [K, N] row-major (the nn.Linear weight's dgrad layout),
-  // 128 x 128 tiles, configuration 0 — the only path that carries the fused delta
-  const dim3 grid((unsigned)((M / BM) * (N / BN)));
-  hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, bf16, 0, 0>), grid, dim3(NT), 0, (hipStream_t)stream, M, N, K,
-                     (const bf16*)dY, ldy, (const bf16*)W, ldw, (bf16*)dO, ldo, 1.f, e, (int64_t)0, (float*)nullptr);
+  // configuration 0 — the only path that carries the fused delta — on 128-, 64- or 32-row tiles by the
+  // plain GEMMs' rule (rp_gemm_bm64 / rp_gemm_bm32: config 4's 128 tiles -> 512)
+  const int mi = rp_gemm_bm64(M, N) ? (rp_gemm_bm32(M, N) ? 1 : 2) : 4;
+  const dim3 grid((unsigned)((M / (32 * mi)) * (N / BN)));
+  if (mi == 4)
+    hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, bf16, 0, 0>), grid, dim3(NT), 0, (hipStream_t)stream, M, N,
+                       K, (const bf16*)dY, ldy, (const bf16*)W, ldw, (bf16*)dO, ldo, 1.f, e, (int64_t)0, (float*)nullptr);
+  else if (mi == 2)
+    hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, bf16, 0, 0, false, 2>), grid, dim3(NT), 0, (hipStream_t)stream,
+                       M, N, K, (const bf16*)dY, ldy, (const bf16*)W, ldw, (bf16*)dO, ldo, 1.f, e, (int64_t)0,
+                       (float*)nullptr);
+  else
+    hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, bf16, 0, 0, false, 1>), grid, dim3(NT), 0, (hipStream_t)stream,
+                       M, N, K, (const bf16*)dY, ldy, (const bf16*)W, ldw, (bf16*)dO, ldo, 1.f, e, (int64_t)0,
+                       (float*)nullptr);
   return rp_check_launch("rp_gemm_attn_dout_delta");
 }
 

@@ -860,12 +860,13 @@ def test_gemm8_forward_dropout_bits(dev, monkeypatch):
     close(y8.float(), y1.double(), atol=0.1, rtol=1e-2, what="gemm8 vs 128-tile dropout forward")
 
 
-@pytest.mark.parametrize("B,T,p", [(8, 2048, 0.1), (2, 384, 0.0)])
+@pytest.mark.parametrize("B,T,p", [(8, 2048, 0.1), (2, 384, 0.0), (4, 2048, 0.1), (1, 4096, 0.1)])
 def test_attn_dout_delta_fused_bitwise(dev, B, T, p):
     """rp_gemm_attn_dout_delta (the out_proj dgrad with the attention delta pre-pass in its epilogue)
     against the two launches it replaces: dO bitwise the plain dgrad GEMM's, the three delta planes
     bitwise rp_attn_bwd_delta's on that dO, and the attention backward fed those planes bitwise the
-    backward that forms them itself (two-role launch at the metric shape)."""
+    backward that forms them itself (two-role launch at the metric shape).  Tile heights: 128 rows at
+    the metric shape, 64 at M = 8192, 32 at config 4 (M = 4096) and M = 768."""
     H, d = 8, 512
     M = B * T
     g1 = rnd(M, d, dev=dev, seed=51).to(torch.bfloat16)
