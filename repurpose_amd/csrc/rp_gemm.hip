@@ -2118,15 +2118,15 @@ __global__ __launch_bounds__(GL_NT, 1) void gemm_ln_bwd_kernel(int64_t M, int64_
 // LayerNorm to fp32 rounding of the row sums (associated per column tile, not per lane).
 constexpr int LX_TN = GL_N / BN;  // column tiles of a 512-wide row
 // Workspace: a 256-byte error word, then one record per 128 rows (its layout independent of M and of the
-// tile height, so launches of any row counts and either kernel can share the workspace): two pairs of
-// arrive / done counters (one per 64-row block: the 128-row tiles use the first), 240 bytes of padding,
-// then the [LX_TN][128] per-row partial pairs.
+// tile height, so launches of any row counts and tile heights can share the workspace): four pairs of
+// arrive / done counters (one per 32-row block: a 128-row tile uses the first, a 64-row tile the first
+// of its half), 224 bytes of padding, then the [LX_TN][128] per-row partial pairs.
 constexpr int64_t LX_REC = 256 + LX_TN * BM * 8;
 struct LnxWs {
   uint32_t* err;  // 1 when a wait gave up (never in a correct launch)
   char* rec;      // rows [128 r, 128 r + 128): record r at rec + r * LX_REC
   // the arrive / done counters of the row block (tile row group) that starts at row m0
-  __device__ uint32_t* cnt(int64_t m0) const { return (uint32_t*)(rec + (m0 / BM) * LX_REC) + 2 * ((m0 / 64) & 1); }
+  __device__ uint32_t* cnt(int64_t m0) const { return (uint32_t*)(rec + (m0 / BM) * LX_REC) + 2 * ((m0 / 32) & 3); }
   // row m's pair of column tile 0 (column tile nt's at + nt * BM)
   __device__ f32x2* part(int64_t m) const { return (f32x2*)(rec + (m / BM) * LX_REC + 256) + m % BM; }
 };
@@ -2220,7 +2220,7 @@ struct LxG {
   static constexpr int IT = TR / RS;                     // chunks per thread
   static constexpr int TPR = TNT / TR;                   // threads per row (forward statistics)
   static constexpr int LDS = TR * CST * 4 + 4 * TR * 4;  // staged tile, per-row totals, (bwd) mean / rstd
-  static_assert((TPR == 2 || TPR == 4) && TR % 64 == 0 && TR <= BM, "row statistics lanes, row blocks");
+  static_assert((TPR == 2 || TPR == 4 || TPR == 8) && TR % 32 == 0 && TR <= BM, "row statistics lanes, row blocks");
 };
 constexpr int LX_IT = LxG<BM, NT>::IT;  // 16: row = tid / 32 + 8 it
 
@@ -2351,7 +2351,7 @@ __device__ __forceinline__ void lx_fwd_tail(const GlnDev& a, const LnxWs& ws, in
   constexpr int CPT = BN / L::TPR / 4;  // float4 chunks per thread
   const int row = tid / L::TPR, hf = tid % L::TPR;
   f32x2* rec = ws.part(m0 + row);  // the row's pair of column tile 0
-  auto lane_sum = [](float v) { return L::TPR == 2 ? lx_sum2(v) : lx_sum4(v); };
+  auto lane_sum = [](float v) { return L::TPR == 2 ? lx_sum2(v) : (L::TPR == 4 ? lx_sum4(v) : rp_sum8(v)); };
   {
     const float* rr = cs + row * CST + hf * (BN / L::TPR);
     float s = 0.f;
@@ -2604,28 +2604,33 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
   lx_bwd_tail<BM, NT>(a, ws, m0, n0, nt, cs, xh, tid);
 }
 
-// 64 x 128 exchange tiles (dma_mainloop MI = 2, each wave 32 x 64) for grids whose 128-row tiles would
-// leave CUs idle (config 4, M = 4096: 128 -> 256 workgroups): the same epilogue tails — the forward's row
-// statistics four threads per row — on the 64-row block's own counters (LnxWs::cnt)
-constexpr int LX64_LDS = dma_tile_lds<0, 2>() > LxG<64, NT>::LDS ? dma_tile_lds<0, 2>() : LxG<64, NT>::LDS;
-template <bool FWD>
+// 64 x 128 and 32 x 128 exchange tiles (dma_mainloop MI = 2 / 1: each wave 32 / 16 x 64) for grids whose
+// 128-row tiles would leave CUs idle (config 4, M = 4096: 128 -> 256 / 512 workgroups): the same epilogue
+// tails — the forward's row statistics four / eight threads per row — on the row block's own counter pair
+// (LnxWs::cnt)
+template <int MI>
+constexpr int lx_small_lds() {
+  return dma_tile_lds<0, MI>() > LxG<32 * MI, NT>::LDS ? dma_tile_lds<0, MI>() : LxG<32 * MI, NT>::LDS;
+}
+template <bool FWD, int MI>
 __global__ __launch_bounds__(NT, 2) void gemm_lnx64_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws) {
-  __shared__ __attribute__((aligned(16))) char lds[LX64_LDS];
-  using L = LxG<64, NT>;
+  constexpr int TR = 32 * MI;
+  __shared__ __attribute__((aligned(16))) char lds[lx_small_lds<MI>()];
+  using L = LxG<TR, NT>;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int t = rp_xcd_remap(blockIdx.x, (int)gridDim.x);
   const int nt = t % LX_TN;
-  const int64_t m0 = (int64_t)(t / LX_TN) * 64, n0 = (int64_t)nt * BN;
-  f32x4 acc[2][4];
+  const int64_t m0 = (int64_t)(t / LX_TN) * TR, n0 = (int64_t)nt * BN;
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc[8];
-  dma_mainloop<true, FWD, 0, 2>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane, wid,
-                                wm, wn);
+  dma_mainloop<true, FWD, 0, MI>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane, wid,
+                                 wm, wn);
   // the epilogue's fp32 operand (fwd: the residual, bwd: x), and (bwd) the rows' mean / rstd
   const float* src = FWD ? a.residual : a.x;
   const int64_t ld = FWD ? a.ldr : a.ldx;
@@ -2634,15 +2639,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx64_kernel(int64_t M, int64_t K,
 #pragma unroll
   for (int it = 0; it < L::IT; ++it) xr[it] = rp_ld16f(src + (m0 + r0 + it * L::RS) * ld + n0 + cc, 2);
   float mrv = 0.f;
-  if (!FWD && tid < 128) mrv = tid < 64 ? a.mean[m0 + tid] : a.rstd[m0 + tid - 64];
+  if (!FWD && tid < 2 * TR) mrv = tid < TR ? a.mean[m0 + tid] : a.rstd[m0 + tid - TR];
   float* cs = reinterpret_cast<float*>(lds);  // dma_mainloop ended on a barrier: its stages are free
-  lx_stage<2>(acc, cs, lane, wm, wn);
-  if (!FWD && tid < 128) cs[64 * CST + 2 * 64 + tid] = mrv;
+  lx_stage<MI>(acc, cs, lane, wm, wn);
+  if (!FWD && tid < 2 * TR) cs[TR * CST + 2 * TR + tid] = mrv;
   __syncthreads();
   if constexpr (FWD)
-    lx_fwd_tail<64, NT>(a, ws, m0, n0, nt, cs, xr, tid);
+    lx_fwd_tail<TR, NT>(a, ws, m0, n0, nt, cs, xr, tid);
   else
-    lx_bwd_tail<64, NT>(a, ws, m0, n0, nt, cs, xr, tid);
+    lx_bwd_tail<TR, NT>(a, ws, m0, n0, nt, cs, xr, tid);
 }
 }  // namespace
 
@@ -2853,16 +2858,19 @@ extern "C" int64_t rp_gemm_ln_xchg_bytes(int64_t M) {
 }
 static LnxWs lnx_ws(void* base, int64_t) { return LnxWs{(uint32_t*)base, (char*)base + 256}; }
 
-// Exchange tile height: 128 where the 128-row grid gives every CU two workgroups, else 64 (M is a
-// multiple of 64).  Interleaved whole-step A/B (profiles/r05_lnx64_ab.txt): bench shape (M = 16384)
-// 13.98 ms on 128-row tiles vs 15.11 on 64-row ones; config 2 (M = 8192, one 128-row tile per CU) 7.11
-// vs 7.04; config 4 (M = 4096) 7.03 on 64-row tiles vs 7.12 unfused.  RP_LNX_ROWS = 64 | 128 (A/B,
-// read per launch) prefers that height where M allows it.
+// Exchange tile height: the tallest of 128 / 64 / 32 rows whose grid gives every CU two workgroups, else
+// 32 (M is a multiple of 64).  Interleaved whole-step A/B (profiles/r05_lnx64_ab.txt): bench shape
+// (M = 16384) 13.98 ms on 128-row tiles vs 15.11 on 64-row ones; config 2 (M = 8192, one 128-row tile per
+// CU) 7.11 vs 7.04 on 64-row tiles; config 4 (M = 4096) 7.03 on 64-row tiles vs 7.12 unfused.
+// RP_LNX_ROWS = 32 | 64 | 128 (A/B, read per launch) prefers that height where M allows it.
 static int lnx_rows(int64_t M) {
   const char* e = getenv("RP_LNX_ROWS");
+  if (e && e[0] == '3') return 32;
   if (e && e[0] == '6') return 64;
   if (e && e[0] == '1') return M % 128 == 0 ? 128 : 64;
-  return (M % 128 == 0 && (M / 128) * LX_TN >= 2 * gemm_cu_count()) ? 128 : 64;
+  const int64_t two = 2 * gemm_cu_count();
+  if (M % 128 == 0 && (M / 128) * LX_TN >= two) return 128;
+  return (M / 64) * LX_TN >= two ? 64 : 32;
 }
 
 static int gemm_ln_common(const char* fn, int64_t M, int64_t K, const rp_gemm_ln_args* p, GlnDev& d) {
@@ -2902,9 +2910,14 @@ extern "C" int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   d.xo = p->x_out; d.ldxo = p->ldx_out;
   d.h = (bf16*)p->h_out; d.ldh = p->ldh;
   if (M == 0) return RP_OK;
-  if (p->xchg && lnx_rows(M) == 64) {
-    hipLaunchKernelGGL(gemm_lnx64_kernel<true>, dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M,
-                       K, d, lnx_ws(p->xchg, M));
+  const int xrows = p->xchg ? lnx_rows(M) : 0;
+  if (xrows == 64 || xrows == 32) {
+    if (xrows == 64)
+      hipLaunchKernelGGL((gemm_lnx64_kernel<true, 2>), dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
+                         M, K, d, lnx_ws(p->xchg, M));
+    else
+      hipLaunchKernelGGL((gemm_lnx64_kernel<true, 1>), dim3((unsigned)(M / 32 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
+                         M, K, d, lnx_ws(p->xchg, M));
     return rp_check_launch("rp_gemm_ln_fwd");
   }
   if (p->xchg) {
@@ -2937,9 +2950,14 @@ extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   d.lp_seed = p->lp_seed;
   d.dgamma_part = p->dgamma_part; d.dbeta_part = p->dbeta_part; d.ld_part = p->ld_part;
   if (M == 0) return RP_OK;
-  if (p->xchg && lnx_rows(M) == 64) {
-    hipLaunchKernelGGL(gemm_lnx64_kernel<false>, dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M,
-                       K, d, lnx_ws(p->xchg, M));
+  const int xrows = p->xchg ? lnx_rows(M) : 0;
+  if (xrows == 64 || xrows == 32) {
+    if (xrows == 64)
+      hipLaunchKernelGGL((gemm_lnx64_kernel<false, 2>), dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
+                         M, K, d, lnx_ws(p->xchg, M));
+    else
+      hipLaunchKernelGGL((gemm_lnx64_kernel<false, 1>), dim3((unsigned)(M / 32 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
+                         M, K, d, lnx_ws(p->xchg, M));
     return rp_check_launch("rp_gemm_ln_bwd");
   }
   if (p->xchg) {

@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 
 SHORT = {"attn_bwd_roles_kernel": "attn_bwd_roles", "gemm_lnx_fwd_kernel": "gemm_lnx_fwd",
-         "gemm_lnx_bwd_kernel": "gemm_lnx_bwd", "gemm_lnx64_kernel": "gemm_lnx64",
+         "gemm_lnx_bwd_kernel": "gemm_lnx_bwd", "gemm_lnx64_kernel": "gemm_lnx_small",
          "attn_bwd_kv_dma_kernel": "attn_bwd_dkdv", "attn_bwd_kv_kernel": "attn_bwd_dkdv",
          "attn_bwd_q_dma_kernel": "attn_bwd_dq", "attn_fwd_dma_kernel": "attn_fwd", "attn_fwd_pp_kernel": "attn_fwd",
          "attn_fwd32_kernel": "attn_fwd", "wgrad8_grouped_kernel": "wgrad_grouped", "concat_kernel": "concat",

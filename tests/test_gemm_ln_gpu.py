@@ -101,10 +101,10 @@ def test_model_fused_seams_bitwise(dev, monkeypatch):
     assert torch.equal(g0, g1), f"grads: {(g0 - g1).abs().max().item():.3e}"
 
 
-@pytest.fixture(params=["64", "128"])
+@pytest.fixture(params=["32", "64", "128"])
 def lnx_rows(request, monkeypatch):
-    """The exchange tile height: 64 x 128 tiles (the host's choice where 128-row tiles would leave CUs
-    idle) or 128 x 128 ones (M % 128 == 0, else 64), RP_LNX_ROWS read per launch."""
+    """The exchange tile height: 32 x 128 or 64 x 128 tiles (the host's choices where taller tiles would
+    leave CUs idle) or 128 x 128 ones (M % 128 == 0, else 64), RP_LNX_ROWS read per launch."""
     monkeypatch.setenv("RP_LNX_ROWS", request.param)
     return request.param
 
@@ -116,9 +116,9 @@ def _ws_clean(dev, M):
     assert ws is not None
     torch.cuda.synchronize()
     assert int(ws[:4].count_nonzero().item()) == 0, "an exchange wait gave up"
-    rec = 256 + 4 * 128 * 8  # one 128-row record: two counter pairs (16 of 256 bytes), then its partial pairs
+    rec = 256 + 4 * 128 * 8  # one 128-row record: four counter pairs (32 of 256 bytes), then its partial pairs
     nr = (M + 127) // 128
-    head = ws[256:256 + nr * rec].view(nr, rec)[:, :16]
+    head = ws[256:256 + nr * rec].view(nr, rec)[:, :32]
     assert int(head.count_nonzero().item()) == 0, "exchange counters not left zeroed"
 
 
@@ -229,7 +229,7 @@ def test_linear_ln_exchange_mixed_rows(dev, monkeypatch):
     block does not move with M or the kernel): each launch agrees with the unfused pair and leaves the
     counters zeroed."""
     for M, rows in ((4096, "128"), (8192, "64"), (16384, "128"), (1024, "64"), (8192, "128"), (384, "64"),
-                    (4096, "64"), (320, "128")):
+                    (4096, "32"), (320, "128"), (8192, "32"), (4096, "64"), (192, "32")):
         monkeypatch.setenv("RP_LNX_ROWS", rows)
         g = torch.Generator().manual_seed(M)
         x, W = _r(g, M, 512, dev=dev), _r(g, D, 512, dev=dev, sc=0.03)
