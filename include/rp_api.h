@@ -187,10 +187,9 @@ typedef struct rp_gemm_ln_args {
   int64_t ld_part;
   /* optional: exchange workspace (rp_gemm_ln_xchg_bytes(M) bytes, 256-byte aligned, zero-filled before
    * its first use; every launch leaves it zeroed, so one workspace serves the launches of a stream).
-   * With it the seam runs on 128 x 128 GEMM tiles (two workgroups per CU; where M % 128 == 0 and that grid
-   * gives every CU two workgroups) or else on 64 x 128 tiles, whose four column tiles per row block
-   * exchange the per-row LayerNorm statistics through it (RP_LNX_ROWS = 64 | 128 prefers one height where
-   * M allows it); x_out is then
+   * With it the seam runs on 128 x 128, 64 x 128 or 32 x 128 GEMM tiles (the tallest whose grid gives
+   * every CU two workgroups), whose four column tiles per row block exchange the per-row LayerNorm
+   * statistics through it (RP_LNX_ROWS = 32 | 64 | 128 prefers one height where M allows it); x_out is then
    * still bitwise the unfused GEMM's, h_out / mean / rstd / dx / dx_lp / the partials agree with the
    * unfused LayerNorm to fp32 rounding of the row sums.  Null: the 64-row full-row kernels above. */
   void* xchg;
