@@ -2629,9 +2629,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx64_kernel(int64_t M, int64_t K,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc[8];
-  dma_mainloop<true, FWD, 0, MI>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane, wid,
-                                 wm, wn);
-  // the epilogue's fp32 operand (fwd: the residual, bwd: x), and (bwd) the rows' mean / rstd
+  // the epilogue's fp32 operand (fwd: the residual, bwd: x) and (bwd) the rows' mean / rstd, issued
+  // before the main loop: in flight under its first fills
   const float* src = FWD ? a.residual : a.x;
   const int64_t ld = FWD ? a.ldr : a.ldx;
   const int cc = (tid % LX_CPR) * 4, r0 = tid / LX_CPR;
@@ -2640,6 +2639,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx64_kernel(int64_t M, int64_t K,
   for (int it = 0; it < L::IT; ++it) xr[it] = rp_ld16f(src + (m0 + r0 + it * L::RS) * ld + n0 + cc, 2);
   float mrv = 0.f;
   if (!FWD && tid < 2 * TR) mrv = tid < TR ? a.mean[m0 + tid] : a.rstd[m0 + tid - TR];
+  dma_mainloop<true, FWD, 0, MI>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane, wid,
+                                 wm, wn);
   float* cs = reinterpret_cast<float*>(lds);  // dma_mainloop ended on a barrier: its stages are free
   lx_stage<MI>(acc, cs, lane, wm, wn);
   if (!FWD && tid < 2 * TR) cs[TR * CST + 2 * TR + tid] = mrv;
