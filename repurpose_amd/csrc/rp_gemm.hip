@@ -270,7 +270,58 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* l
           cs[((HALVES ? 0 : wm * (MI * 16)) + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
   }
   __syncthreads();
-  if constexpr (RESB) {
+  if constexpr (RESB && std::is_same<TC, bf16>::value) {
+    // bf16 C gated by a bf16 tensor (the d_ff dgrad through ReLU + dropout; no residual, no delta): the
+    // pass's gate chunks loaded before its first store, as the residual below
+    static_assert(MODE == 0 && OV == 8, "RESB bf16: MODE 0");
+    constexpr int ITER = HR * CPRO / NT;
+    static_assert(HR * CPRO % NT == 0, "whole chunks per thread");
+    bf16x8 gv[ITER];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int id = tid + it * NT;
+      const int64_t m = m0 + id / CPRO + half * HR, n = n0 + (id % CPRO) * OV;
+      if (m < M && n < N) gv[it] = *reinterpret_cast<const bf16x8*>((const bf16*)ep.gate + m * ep.ldg + n);
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int id = tid + it * NT;
+      const int row = id / CPRO + half * HR, cc = (id % CPRO) * OV;
+      const int64_t m = m0 + row, n = n0 + cc;
+      if (m >= M || n >= N) continue;
+      float v[OV];
+#pragma unroll
+      for (int e = 0; e < OV; e += 4) {
+        float4 q = *reinterpret_cast<const float4*>(cs + (row - half * HR) * CST + cc + e);
+        v[e] = q.x * alpha; v[e + 1] = q.y * alpha; v[e + 2] = q.z * alpha; v[e + 3] = q.w * alpha;
+      }
+      if (ep.bias) {
+#pragma unroll
+        for (int e = 0; e < OV; ++e) v[e] += bv[e];
+      }
+      if (n < ep.col_scale_n) {
+#pragma unroll
+        for (int e = 0; e < OV; ++e) v[e] *= ep.col_scale;
+      }
+      if (ep.relu) {
+#pragma unroll
+        for (int e = 0; e < OV; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (ep.drop_thresh) {
+        const uint32_t kb = rp_keep_bits<OV>(dseed, (uint32_t)(m * N + n), ep.drop_thresh);
+#pragma unroll
+        for (int e = 0; e < OV; ++e) v[e] = ((kb >> e) & 1u) ? v[e] * ep.drop_scale : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < OV; ++e) v[e] = (float)gv[it][e] > 0.f ? v[e] * ep.gate_scale : 0.f;
+      uint4 o;
+      bf16* ob = reinterpret_cast<bf16*>(&o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ob[e] = (bf16)v[e];
+      rp_st16((TC*)Cbase + m * ldc + n, o, ep.st_pol);
+    }
+    continue;
+  } else if constexpr (RESB) {
     static_assert(std::is_same<TC, float>::value && MODE == 0, "RESB: fp32 C, MODE 0");
     constexpr int ITER = HR * CPRO / NT;
     static_assert(HR * CPRO % NT == 0, "whole chunks per thread");
@@ -1630,6 +1681,12 @@ int launch_gemm8(int bn, int64_t M, int64_t N, int64_t K, const bf16* a, int64_t
 // fewer than two workgroups per CU: config 4 (M = 4096) has 128 such tiles on its d_model = 512 GEMMs
 // (half the CUs idle; step 7.92 -> 7.60 ms), config 2 (M = 8192) 256 (7.95 -> 7.66 ms).  RP_GEMM_BM64=0
 // never, =1 wherever legal (tests, A/B), unset: fewer 128 x 128 tiles than twice the CUs.  Per call.
+// RP_GEMM_GATEB=0 (A/B, read per call): the gated bf16 dgrads on the per-chunk epilogue
+static bool rp_gate_batch() {
+  const char* e = getenv("RP_GEMM_GATEB");
+  return !(e && e[0] == '0');
+}
+
 static bool rp_gemm_bm64(int64_t M, int64_t N) {
   const char* e = getenv("RP_GEMM_BM64");
   if (e && e[0] == '0') return false;
@@ -1677,6 +1734,11 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
       default: RP_DMA_LAUNCH1(AKV, BKV, MODEV, 2, GRID); break;               \
     }                                                                         \
   } while (0)
+      // bf16 C gated by a bf16 tensor, nothing else read (the d_ff dgrad): the gate-batched epilogue
+      bool gateb = false;
+      if constexpr (std::is_same<TC, bf16>::value)
+        gateb = splits == 0 && ak && !bk && ep.gate && ep.gate_bf16 && !ep.residual && !ep.delta && !ep.accumulate &&
+                rp_gate_batch();
       if (splits == 0 && ak && cfg == 0 && rp_gemm_bm64(M, N) && rp_gemm_bm32(M, N)) {  // 32 x 128 tiles
         const dim3 grid((unsigned)(((M + 31) / 32) * ((N + BN - 1) / BN)));
         bool done = false;
@@ -1686,6 +1748,10 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
                                ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
             done = true;
           }
+        } else if (gateb) {
+          hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, TC, 0, 0, true, 1>), grid, dim3(NT), 0, s, M, N, K, ab,
+                             lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
+          done = true;
         }
         if (!done) {
           if (bk)
@@ -1706,6 +1772,10 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
                                ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
             done = true;
           }
+        } else if (gateb) {
+          hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, TC, 0, 0, true, 2>), grid, dim3(NT), 0, s, M, N, K, ab,
+                             lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab);
+          done = true;
         }
         if (!done) {
           if (bk)
@@ -1730,6 +1800,18 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
           }
           return rp_check_launch("rp_gemm");
         }
+      }
+      if (gateb) {
+        dim3 grid((unsigned)tiles);
+        switch (cfg) {
+          case 0: hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, TC, 0, 0, true>), grid, dim3(NT), 0, s, M, N, K, ab,
+                                     lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab); break;
+          case 1: hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, TC, 0, 1, true>), grid, dim3(NT), 0, s, M, N, K, ab,
+                                     lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab); break;
+          default: hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, TC, 0, 2, true>), grid, dim3(NT), 0, s, M, N, K,
+                                      ab, lda, bb, ldb, c, ldc, alpha, ep, kchunk, bslab); break;
+        }
+        return rp_check_launch("rp_gemm");
       }
       if (splits == 0) {
         dim3 grid((unsigned)tiles);

@@ -716,6 +716,29 @@ def test_gemm_64_row_tiles_bitwise(dev, monkeypatch, M):
         assert torch.equal(a, c) and torch.equal(c, d) and torch.equal(a, e)
 
 
+@pytest.mark.parametrize("M", [384, 4096, 8192])
+@pytest.mark.parametrize("tiles", ["128", "64", "32"])
+def test_gemm_gate_batched_bitwise(dev, monkeypatch, M, tiles):
+    """The gated bf16 dgrad (d_ff backward through ReLU + dropout) with the pass's gate chunks loaded
+    before its stores (the default) is bitwise the per-chunk epilogue (RP_GEMM_GATEB=0) on 128-, 64- and
+    32-row tiles (all three staging forms), ragged M included, and matches fp64."""
+    monkeypatch.setenv("RP_GEMM_BM64", "0" if tiles == "128" else "1")
+    monkeypatch.setenv("RP_GEMM_BM32", "1" if tiles == "32" else "0")
+    monkeypatch.setenv("RP_GEMM8", "0")
+    n, k = 512, 2048
+    dy = rnd(M, n, dev=dev, seed=M + 1).to(torch.bfloat16)
+    w = rnd(n, k, dev=dev, seed=M + 2, scale=0.05).to(torch.bfloat16)
+    gate = rnd(M, k, dev=dev, seed=M + 3).to(torch.bfloat16)
+    outs = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("RP_GEMM_GATEB", flag)
+        outs[flag] = K.linear_dgrad(dy, w, out_dtype=torch.bfloat16, gate=gate, gate_scale=1.25)
+    torch.cuda.synchronize()
+    assert torch.equal(outs["0"], outs["1"])
+    ref = (dy.double() @ w.double()) * 1.25 * (gate.double() > 0)
+    close(outs["1"], ref, atol=2e-3 * math.sqrt(n), rtol=1e-2, what=f"gated dgrad M={M}")
+
+
 @pytest.mark.parametrize("B,T,qpre,roles", [(8, 2048, False, "1"), (8, 2048, True, "1"), (8, 2048, True, "0"),
                                             (1, 4096, True, "1")])
 def test_attention_metric_shape_bf16_dropout(dev, monkeypatch, B, T, qpre, roles):
