@@ -2309,10 +2309,11 @@ constexpr int LX_IT = LxG<BM, NT>::IT;  // 16: row = tid / 32 + 8 it
 // glds_tile's fills issued through inline asm (rp_dma16): the compiler does not track them, so it adds
 // no vmcnt(0) ahead of the LDS reads, and loads the caller issues between fills stay in flight across
 // the loop's barriers; the caller orders every fill before its readers (counted vmcnt + barrier)
-template <bool KMAJ>
+template <bool KMAJ, int ROWS = BM>
 __device__ __forceinline__ void glds_tile_u(const bf16* __restrict__ base, int64_t ld, int64_t rows_lim, int64_t row0,
                                             int64_t k0, char* tile, int wid, int lane) {
-  constexpr int PER = BM * 64 * 2 / 1024 / (NT / 64);
+  constexpr int PER = ROWS * 64 * 2 / 1024 / (NT / 64);  // 1 KB pieces per wave
+  static_assert(PER >= 1 && (KMAJ || ROWS == BM), "whole pieces; m-major images are 128 columns wide");
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int I = wid * PER + j;
@@ -2332,42 +2333,50 @@ __device__ __forceinline__ void glds_tile_u(const bf16* __restrict__ base, int64
   }
 }
 
-// The 128 x 128 main loop of dma_mainloop (two 64-deep LDS stages, one barrier per K step, the same
+// The (32 MI) x 128 main loop of dma_mainloop (two 64-deep LDS stages, one barrier per K step, the same
 // MFMA order, so the same products bit for bit) with the fills untracked and a per-thread prefetch of
-// LX_IT 16-byte fp32 chunks of the epilogue's operand spread over the first K steps: LX_PF chunks
+// the 4 MI 16-byte fp32 chunks of the epilogue's operand spread over the first K steps: LX_PF chunks
 // issued right after step kt's fill of stage kt + 1, waited for only one step later (the counted
 // vmcnt at the end of a step leaves exactly that step's prefetch in flight).  The lockstep grid keeps
-// HBM idle through the main loop, so these bytes leave the HBM-bound epilogue.
-constexpr int LX_PF = 2;                 // prefetch chunks per K step
-constexpr int LX_PFS = LX_IT / LX_PF;    // K steps that carry them (8)
-template <bool AK, bool BKM>
+// HBM idle through the main loop, so these bytes leave the HBM-bound epilogue.  Each step also waits
+// for its own LDS reads (lgkmcnt(0)) before the barrier: after it another wave's fill of step kt + 1
+// overwrites the stage read in step kt, and an LDS read still queued behind that traffic would read the
+// new bytes (the compiler leaves the last reads of a step outstanding across the barrier otherwise).
+constexpr int LX_PF = 2;  // prefetch chunks per K step
+template <int MI>
+constexpr int lx_pfs() { return LxG<32 * MI, NT>::IT / LX_PF; }  // K steps that carry them (8 at MI = 4)
+template <bool AK, bool BKM, int MI = 4>
 __device__ __forceinline__ void lx_mainloop(const bf16* __restrict__ A, int64_t lda, int64_t M,
                                             const bf16* __restrict__ B, int64_t ldb, int64_t m0, int64_t n0,
-                                            int64_t K, f32x4 (&acc)[4][4], char* lds, int lane, int wid, int wm,
+                                            int64_t K, f32x4 (&acc)[MI][4], char* lds, int lane, int wid, int wm,
                                             int wn, const float* __restrict__ pf_base, int64_t pf_ld,
-                                            float4 (&pf)[LX_IT], int tid) {
-  constexpr int BK = 64, GT = BM * BK * 2, SG = 2 * GT;
+                                            float4 (&pf)[LxG<32 * MI, NT>::IT], int tid) {
+  constexpr int LX_PFS = lx_pfs<MI>();
+  static_assert(AK || MI == 4, "64- / 32-row images: k-major A");
+  constexpr int BK = 64, GTA = MI * 32 * BK * 2, GT = BM * BK * 2, SG = GTA + GT;
   const int nk = (int)(K / BK);
   const float* pfp = pf_base + (m0 + tid / LX_CPR) * pf_ld + n0 + (tid % LX_CPR) * 4;
   auto prefetch = [&](int c) { pf[c] = rp_ld16f(pfp + (int64_t)c * (NT / LX_CPR) * pf_ld, 2); };
   auto fill = [&](int kt) {
     char* buf = lds + (kt & 1) * SG;
-    glds_tile_u<AK>(A, lda, M, m0, (int64_t)kt * BK, buf, wid, lane);
-    glds_tile_u<BKM>(B, ldb, GL_N, n0, (int64_t)kt * BK, buf + GT, wid, lane);
+    glds_tile_u<AK, MI * 32>(A, lda, M, m0, (int64_t)kt * BK, buf, wid, lane);
+    glds_tile_u<BKM>(B, ldb, GL_N, n0, (int64_t)kt * BK, buf + GTA, wid, lane);
   };
   auto compute = [&](int kt) {
     const char* cur = lds + (kt & 1) * SG;
 #pragma unroll
     for (int ks = 0; ks < BK; ks += 32) {
-      bf16x8 fa[4], fb[4];
+      bf16x8 fa[MI], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        fa[i] = AK ? frag_k_swz<BK>(cur, wm * 64 + i * 16, ks, lane) : frag_m_swz(cur, wm * 64 + i * 16, ks, lane);
+      for (int i = 0; i < MI; ++i)
+        fa[i] = AK ? frag_k_swz<BK>(cur, wm * (MI * 16) + i * 16, ks, lane)
+                   : frag_m_swz(cur, wm * (MI * 16) + i * 16, ks, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        fb[j] = BKM ? frag_k_swz<BK>(cur + GT, wn * 64 + j * 16, ks, lane) : frag_m_swz(cur + GT, wn * 64 + j * 16, ks, lane);
+        fb[j] = BKM ? frag_k_swz<BK>(cur + GTA, wn * 64 + j * 16, ks, lane)
+                    : frag_m_swz(cur + GTA, wn * 64 + j * 16, ks, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
@@ -2383,13 +2392,13 @@ __device__ __forceinline__ void lx_mainloop(const bf16* __restrict__ A, int64_t 
 #pragma unroll
     for (int c = 0; c < LX_PF; ++c) prefetch(kt * LX_PF + c);
     compute(kt);
-    rp_waitcnt<LX_PF, 15>();  // stage kt + 1 has landed; this step's prefetch may stay in flight
+    rp_waitcnt<LX_PF, 0>();  // stage kt + 1 has landed; this step's prefetch may stay in flight
     rp_raw_barrier();
   }
   for (int kt = LX_PFS; kt < nk; ++kt) {
     if (kt + 1 < nk) fill(kt + 1);
     compute(kt);
-    rp_waitcnt<0, 15>();
+    rp_waitcnt<0, 0>();
     rp_raw_barrier();
   }
 }
@@ -2695,7 +2704,8 @@ constexpr int lx_small_lds() {
   return dma_tile_lds<0, MI>() > LxG<32 * MI, NT>::LDS ? dma_tile_lds<0, MI>() : LxG<32 * MI, NT>::LDS;
 }
 template <bool FWD, int MI>
-__global__ __launch_bounds__(NT, 2) void gemm_lnx64_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws) {
+__global__ __launch_bounds__(NT, 2) void gemm_lnx64_kernel(int64_t M, int64_t K, const GlnDev a, const LnxWs ws,
+                                                           int pf) {
   constexpr int TR = 32 * MI;
   __shared__ __attribute__((aligned(16))) char lds[lx_small_lds<MI>()];
   using L = LxG<TR, NT>;
@@ -2711,18 +2721,23 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx64_kernel(int64_t M, int64_t K,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc[8];
-  // the epilogue's fp32 operand (fwd: the residual, bwd: x) and (bwd) the rows' mean / rstd, issued
-  // before the main loop: in flight under its first fills
+  // the epilogue's fp32 operand (fwd: the residual, bwd: x): prefetched across the first K steps of the
+  // untracked main loop (pf), or issued before dma_mainloop (in flight under its first fills); and (bwd)
+  // the rows' mean / rstd
   const float* src = FWD ? a.residual : a.x;
   const int64_t ld = FWD ? a.ldr : a.ldx;
   const int cc = (tid % LX_CPR) * 4, r0 = tid / LX_CPR;
   float4 xr[L::IT];
-#pragma unroll
-  for (int it = 0; it < L::IT; ++it) xr[it] = rp_ld16f(src + (m0 + r0 + it * L::RS) * ld + n0 + cc, 2);
   float mrv = 0.f;
   if (!FWD && tid < 2 * TR) mrv = tid < TR ? a.mean[m0 + tid] : a.rstd[m0 + tid - TR];
-  dma_mainloop<true, FWD, 0, MI>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane, wid,
-                                 wm, wn);
+  if (pf) {
+    lx_mainloop<true, FWD, MI>(a.A, a.lda, M, a.W, a.ldw, m0, n0, K, acc, lds, lane, wid, wm, wn, src, ld, xr, tid);
+  } else {
+#pragma unroll
+    for (int it = 0; it < L::IT; ++it) xr[it] = rp_ld16f(src + (m0 + r0 + it * L::RS) * ld + n0 + cc, 2);
+    dma_mainloop<true, FWD, 0, MI>(a.A, a.lda, M, a.W, a.ldw, GL_N, m0, n0, 0, K, false, acc, bacc, lds, tid, lane,
+                                   wid, wm, wn);
+  }
   float* cs = reinterpret_cast<float*>(lds);  // dma_mainloop ended on a barrier: its stages are free
   lx_stage<MI>(acc, cs, lane, wm, wn);
   if (!FWD && tid < 2 * TR) cs[TR * CST + 2 * TR + tid] = mrv;
@@ -2997,15 +3012,15 @@ extern "C" int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   if (xrows == 64 || xrows == 32) {
     if (xrows == 64)
       hipLaunchKernelGGL((gemm_lnx64_kernel<true, 2>), dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
-                         M, K, d, lnx_ws(p->xchg, M));
+                         M, K, d, lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<2>() ? 1 : 0);
     else
       hipLaunchKernelGGL((gemm_lnx64_kernel<true, 1>), dim3((unsigned)(M / 32 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
-                         M, K, d, lnx_ws(p->xchg, M));
+                         M, K, d, lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<1>() ? 1 : 0);
     return rp_check_launch("rp_gemm_ln_fwd");
   }
   if (p->xchg) {
     hipLaunchKernelGGL(gemm_lnx_fwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
-                       lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * LX_PFS ? 1 : 0);
+                       lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<4>() ? 1 : 0);
     return rp_check_launch("rp_gemm_ln_fwd");
   }
   hipLaunchKernelGGL(gemm_ln_fwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
@@ -3037,15 +3052,15 @@ extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   if (xrows == 64 || xrows == 32) {
     if (xrows == 64)
       hipLaunchKernelGGL((gemm_lnx64_kernel<false, 2>), dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
-                         M, K, d, lnx_ws(p->xchg, M));
+                         M, K, d, lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<2>() ? 1 : 0);
     else
       hipLaunchKernelGGL((gemm_lnx64_kernel<false, 1>), dim3((unsigned)(M / 32 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
-                         M, K, d, lnx_ws(p->xchg, M));
+                         M, K, d, lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<1>() ? 1 : 0);
     return rp_check_launch("rp_gemm_ln_bwd");
   }
   if (p->xchg) {
     hipLaunchKernelGGL(gemm_lnx_bwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
-                       lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * LX_PFS ? 1 : 0);
+                       lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<4>() ? 1 : 0);
     return rp_check_launch("rp_gemm_ln_bwd");
   }
   hipLaunchKernelGGL(gemm_ln_bwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
