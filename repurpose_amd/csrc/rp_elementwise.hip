@@ -29,12 +29,13 @@ __global__ void concat_kernel(const float* __restrict__ v, int dv, const float* 
     for (int u = 0; u < CU; ++u) {
       const int c = c0 + u * blockDim.x * 4;
       if (c >= D) break;
+      // the features are read once: non-temporal (the output stays cached for the projection GEMM)
       if (c < dv)
-        q[u] = *reinterpret_cast<const float4*>(v + r * dv + c);
+        q[u] = rp_ld16f(v + r * dv + c, 2);
       else if (c < dv + da)
-        q[u] = *reinterpret_cast<const float4*>(a + r * da + (c - dv));
+        q[u] = rp_ld16f(a + r * da + (c - dv), 2);
       else
-        q[u] = *reinterpret_cast<const float4*>(t + r * dt + (c - dv - da));
+        q[u] = rp_ld16f(t + r * dt + (c - dv - da), 2);
     }
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
