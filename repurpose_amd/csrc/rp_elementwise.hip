@@ -312,12 +312,15 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   } else {
     c[0] = c0; c[1] = c1; c[2] = c2; c[3] = c3; c[4] = c4; c[5] = c5;
   }
+  // the fp32 master, the moments and the gradient are touched once per step: non-temporal (the bf16
+  // operand copy, read by the next forward's GEMMs, is stored plainly)
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float pi = p[i], mi = m[i], vi = v[i];
-    adam_elem(pi, g[i], mi, vi, c);
-    p[i] = pi;
-    m[i] = mi;
-    v[i] = vi;
+    float pi = __builtin_nontemporal_load(p + i), mi = __builtin_nontemporal_load(m + i),
+          vi = __builtin_nontemporal_load(v + i);
+    adam_elem(pi, __builtin_nontemporal_load(g + i), mi, vi, c);
+    __builtin_nontemporal_store(pi, p + i);
+    __builtin_nontemporal_store(mi, m + i);
+    __builtin_nontemporal_store(vi, v + i);
     if (plp) plp[i] = (bf16)pi;
   }
 }
