@@ -443,9 +443,10 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* l
         // the row dot of this chunk's 8 stored values with the output (hi + lo), then the 8 chunks of
         // the head (consecutive lanes: 16 chunks per row, M and N whole tiles so every lane is here)
         // by rp_sum8 — attn_delta_kernel's order, so the planes are bitwise its
-        const bf16x8 oh = *reinterpret_cast<const bf16x8*>(ep.dot_hi + m * ep.ld_dot + n);
+        // the attention output (hi, lo) is read once, here: non-temporal
+        const bf16x8 oh = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(ep.dot_hi + m * ep.ld_dot + n));
         bf16x8 ol;
-        if (ep.dot_lo) ol = *reinterpret_cast<const bf16x8*>(ep.dot_lo + m * ep.ld_dot + n);
+        if (ep.dot_lo) ol = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(ep.dot_lo + m * ep.ld_dot + n));
         float dsum = 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) dsum += ((float)oh[e] + (ep.dot_lo ? (float)ol[e] : 0.f)) * (float)ob[e];
