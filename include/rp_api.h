@@ -189,14 +189,27 @@ typedef struct rp_gemm_ln_args {
    * its first use; every launch leaves it zeroed, so one workspace serves the launches of a stream).
    * With it the seam runs on 128 x 128, 64 x 128 or 32 x 128 GEMM tiles (the tallest whose grid gives
    * every CU two workgroups), whose four column tiles per row block exchange the per-row LayerNorm
-   * statistics through it (RP_LNX_ROWS = 32 | 64 | 128 prefers one height where M allows it); x_out is then
+   * statistics through it; x_out is then
    * still bitwise the unfused GEMM's, h_out / mean / rstd / dx / dx_lp / the partials agree with the
-   * unfused LayerNorm to fp32 rounding of the row sums.  Null: the 64-row full-row kernels above. */
+   * unfused LayerNorm to fp32 rounding of the row sums.  Null: the 64-row full-row kernels above.
+   * Launches sharing one workspace must be ordered (one stream, or event-ordered).
+   * Progress: a seam is issued as launches of at most the co-resident capacity (CUs x workgroups per CU
+   * from the occupancy query, at most 2) whole row blocks each, so every partner of a waiting workgroup
+   * is resident, or becomes resident once other streams' kernels retire.  A partner wait is bounded
+   * (10 s); one that gives up sets a process-wide fault word: from then on rp_gemm_ln_fwd / bwd and
+   * rp_gemm_ln_status return RP_ERR_LAUNCH (the outputs of that launch are invalid and its workspace is
+   * inconsistent) until rp_gemm_ln_reset re-zeroes the workspace. */
   void* xchg;
 } rp_gemm_ln_args;
 int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* a, void* stream);
 int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* a, void* stream);
 int64_t rp_gemm_ln_xchg_bytes(int64_t M);
+/* RP_OK, or RP_ERR_LAUNCH when an exchange wait gave up since the last reset (no synchronisation: a
+ * launch is seen once it has run). */
+int rp_gemm_ln_status(void);
+/* After a give-up: synchronise `stream`, zero the workspace (rp_gemm_ln_xchg_bytes(M) bytes; xchg may be
+ * NULL) and clear the fault word. */
+int rp_gemm_ln_reset(void* xchg, int64_t M, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* LayerNorm over the last dim D (<= 4096, multiple of 4), one row per wavefront.
@@ -306,6 +319,8 @@ int rp_sumsq_batched(const rp_sumsq_item* items, int n_items, void* stream);
  * backward unchanged.  Without the flag the kernels compute the same bf16(Q * scale * log2 e)
  * themselves (the forward and dQ kernels in registers, the dK/dV kernel as it stages Q tiles). */
 enum { RP_ATTN_Q_PRESCALED = 0x100 };
+/* 0x200 (RP_ATTN_NO_SPLIT of rounds 1-4, removed with the split kernels' switch) is still accepted in the
+ * dtype argument and ignored. */
 
 /* Multi-head self attention, flash-style (no T x T materialisation).
  * qkv: [B*T, 3*H*dk] rows = (q heads | k heads | v heads), dk == 64.
@@ -535,6 +550,19 @@ int rp_tiou_hits(const float* pred, const int* pred_count, int P, const double* 
 int rp_diou_fwd(const float* pred, const float* gt, int64_t n, float eps, int reduction, float* out, void* stream);
 int rp_diou_bwd(const float* pred, const float* gt, int64_t n, float eps, const float* grad_out, int per_elem,
                 float grad_scale, float* dpred, float* dgt, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Test hooks (not used by the product path).
+ * rp_debug_gemm_ln_partial: the exchange launch of rp_gemm_ln_fwd (fwd != 0) / bwd with only its first
+ *   `tiles` workgroups and a give-up bound of timeout_s: a row block whose partner is never launched must
+ *   set the fault word (rp_gemm_ln_status), not hang or return silently wrong statistics.
+ * rp_debug_occupy: `blocks` 256-thread workgroups with 64 KiB of LDS each that hold their CU slots for
+ *   `us` microseconds (a seam launched beside another stream's long kernel).
+ * rp_debug_set_lnx_rows: force the exchange tile height (32, 64 or 128 rows; 0 = automatic) process-wide. */
+int rp_debug_gemm_ln_partial(int fwd, int64_t M, int64_t K, const rp_gemm_ln_args* a, int64_t tiles, double timeout_s,
+                             void* stream);
+int rp_debug_occupy(int blocks, int us, void* stream);
+int rp_debug_set_lnx_rows(int rows);
 
 #ifdef __cplusplus
 }

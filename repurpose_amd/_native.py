@@ -98,6 +98,11 @@ _SIGNATURES = {
     "rp_gemm_ln_fwd": (c_i, [c_i64, c_i64, ctypes.POINTER(GemmLnArgs), c_vp]),
     "rp_gemm_ln_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(GemmLnArgs), c_vp]),
     "rp_gemm_ln_xchg_bytes": (c_i64, [c_i64]),
+    "rp_gemm_ln_status": (c_i, []),
+    "rp_gemm_ln_reset": (c_i, [c_vp, c_i64, c_vp]),
+    "rp_debug_gemm_ln_partial": (c_i, [c_i, c_i64, c_i64, ctypes.POINTER(GemmLnArgs), c_i64, ctypes.c_double, c_vp]),
+    "rp_debug_occupy": (c_i, [c_i, c_i, c_vp]),
+    "rp_debug_set_lnx_rows": (c_i, [c_i]),
     "rp_layernorm_fwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnFwdArgs), c_vp]),
     "rp_layernorm_bwd_blocks": (c_i64, [c_i64]),
     "rp_layernorm_bwd": (c_i, [c_i64, c_i64, ctypes.POINTER(LnBwdArgs), c_vp]),

@@ -2815,7 +2815,8 @@ int make_dev(const char* fn, int dtype, int qpre, const rp_mha_args* p, int phas
 
 // the attention entry points take RP_ATTN_Q_PRESCALED or-ed into their dtype argument
 inline int attn_qpre(int dtype) { return (dtype & RP_ATTN_Q_PRESCALED) ? 1 : 0; }
-inline int attn_dtype(int dtype) { return dtype & ~RP_ATTN_Q_PRESCALED; }
+// 0x200 (the removed RP_ATTN_NO_SPLIT of rounds 1-4) is accepted as a no-op, so older callers keep working
+inline int attn_dtype(int dtype) { return dtype & ~(RP_ATTN_Q_PRESCALED | 0x200); }
 
 int mha_fwd_entry(int flagged, const rp_mha_args* p, void* stream) {
   const int dtype = attn_dtype(flagged);

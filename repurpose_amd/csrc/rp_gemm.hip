@@ -14,6 +14,9 @@
 // buffer (one barrier per K step), XCD-aware tile order.  bf16: v_mfma_f32_16x16x32_bf16, K-step
 // 64; f32 parity mode: exact v_mfma_f32_16x16x4_f32, K-step 32.
 #include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
 
 #include "rp_common.h"
 
@@ -2192,13 +2195,18 @@ __global__ __launch_bounds__(GL_NT, 1) void gemm_ln_bwd_kernel(int64_t M, int64_
 //   bwd: per row (sum g gamma, sum g gamma xhat) over the tile's columns (ln_bwd_kernel's s1, s2).
 // Protocol (cdna_hip_programming.md §6 Guideline 16, recipe R1): the payload stored write-through (sc1)
 // and drained by every storing wave, a barrier, one relaxed agent-scope arrive add per workgroup, one
-// polling lane (relaxed agent-scope loads + s_sleep, bounded: a wait that gives up sets the error word),
-// a barrier; the partners' payload read back with sc1 loads only.  The last of the four to finish
-// reading resets the row block's counters, so each launch starts from and leaves a zeroed workspace.
-// The four column tiles of a row block are consecutive logical tiles (blockIdx b, b + 8, b + 16, b + 24
-// after the XCD remap), dispatched in order, so the partners of a waiting workgroup are always
-// dispatched.  x_out is bitwise the unfused GEMM's; h / mean / rstd / dx agree with the unfused
-// LayerNorm to fp32 rounding of the row sums (associated per column tile, not per lane).
+// polling lane (relaxed agent-scope loads + s_sleep, bounded in time: a wait that gives up sets the
+// workspace's error word and the library's host-mapped fault word, which every later rp_gemm_ln_* call
+// and rp_gemm_ln_status() report as RP_ERR_LAUNCH until rp_gemm_ln_reset), a barrier; the partners'
+// payload read back with sc1 loads only.  The last of the four to finish reading resets the row block's
+// counters, so each launch starts from and leaves a zeroed workspace.
+// Forward progress (co-residency rule): the host splits a seam into launches whose grid is
+// at most the co-resident capacity (CUs x workgroups per CU, from the occupancy query, at most 2), so
+// every workgroup of a launch is resident at once, or becomes resident as soon as other streams' kernels
+// retire, whatever the dispatch order; lx_tile also places the four column tiles of a row block back to
+// back in dispatch order on one XCD (speed and a second line of defence, never relied on alone).
+// x_out is bitwise the unfused GEMM's; h / mean / rstd / dx agree with the unfused LayerNorm to fp32
+// rounding of the row sums (associated per column tile, not per lane).
 constexpr int LX_TN = GL_N / BN;  // column tiles of a 512-wide row
 // Workspace: a 256-byte error word, then one record per 128 rows (its layout independent of M and of the
 // tile height, so launches of any row counts and tile heights can share the workspace): four pairs of
@@ -2206,8 +2214,11 @@ constexpr int LX_TN = GL_N / BN;  // column tiles of a 512-wide row
 // of its half), 224 bytes of padding, then the [LX_TN][128] per-row partial pairs.
 constexpr int64_t LX_REC = 256 + LX_TN * BM * 8;
 struct LnxWs {
-  uint32_t* err;  // 1 when a wait gave up (never in a correct launch)
-  char* rec;      // rows [128 r, 128 r + 128): record r at rec + r * LX_REC
+  uint32_t* err;    // 1 when a wait gave up (never in a correct launch)
+  char* rec;        // rows [128 r, 128 r + 128): record r at rec + r * LX_REC
+  uint32_t* fault;  // the library's host-mapped fault word (lx_fault_word), also set on a give-up
+  uint64_t limit;   // give-up bound of a wait, s_memrealtime ticks (100 MHz)
+  int rb0, nrb;     // this launch's row blocks: [rb0, rb0 + nrb) of the seam (TR-row blocks)
   // the arrive / done counters of the row block (tile row group) that starts at row m0
   __device__ uint32_t* cnt(int64_t m0) const { return (uint32_t*)(rec + (m0 / BM) * LX_REC) + 2 * ((m0 / 32) & 3); }
   // row m's pair of column tile 0 (column tile nt's at + nt * BM)
@@ -2240,16 +2251,35 @@ __device__ __forceinline__ void lx_drain_arrive(uint32_t* cnt, int tid) {
 }
 __device__ __forceinline__ void lx_wait(const LnxWs& ws, uint32_t* cnt, int tid) {
   if (tid == 0) {
-    uint32_t n = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)LX_TN) {
       __builtin_amdgcn_s_sleep(1);
-      if (++n > (1u << 24)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > ws.limit) {
         __hip_atomic_store(ws.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ws.fault) __hip_atomic_store(ws.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
   }
   __syncthreads();
+}
+
+// (row block, column tile) of workgroup bid: the four column tiles of a row block are dispatched back to
+// back on one XCD under round-robin placement — blocks b, b + 8, b + 16, b + 24 of each 32-block chunk of
+// eight row blocks — whatever the grid size (the XCD remap of consecutive tiles split a row block across
+// two XCDs at chunk edges); a last partial chunk keeps them adjacent (b .. b + 3).  The A row panel stays
+// on the XCD of its four tiles, as before; W is read by every tile either way.
+__device__ __forceinline__ void lx_tile(int bid, const LnxWs& ws, int& rb, int& nt) {
+  const int g = bid >> 5;
+  if ((g + 1) * 8 <= ws.nrb) {
+    rb = g * 8 + (bid & 7);
+    nt = (bid >> 3) & 3;
+  } else {
+    const int l = bid - g * 32;
+    rb = g * 8 + (l >> 2);
+    nt = l & 3;
+  }
+  rb += ws.rb0;
 }
 // after a barrier that follows every thread's partner reads: the last of the four resets the counters
 __device__ __forceinline__ void lx_done(uint32_t* c, int tid) {
@@ -2611,10 +2641,12 @@ __device__ __forceinline__ void lx_bwd_tail(const GlnDev& a, const LnxWs& ws, in
       float* dst = k ? a.dbeta_part : a.dgamma_part;
       if (dst) dst[pr * a.ld_part + n0 + c] = s;
     }
-    for (int id = tid; id < (TR / 32 - 1) * 2 * BN; id += TNT) {
-      const int k = id / ((TR / 32 - 1) * BN), rr = (id / BN) % (TR / 32 - 1) + 1, c = id % BN;
-      float* dst = k ? a.dbeta_part : a.dgamma_part;
-      if (dst) dst[(pr + rr) * a.ld_part + n0 + c] = 0.f;
+    if constexpr (TR > 32) {
+      for (int id = tid; id < (TR / 32 - 1) * 2 * BN; id += TNT) {
+        const int k = id / ((TR / 32 - 1) * BN), rr = (id / BN) % (TR / 32 - 1) + 1, c = id % BN;
+        float* dst = k ? a.dbeta_part : a.dgamma_part;
+        if (dst) dst[(pr + rr) * a.ld_part + n0 + c] = 0.f;
+      }
     }
   }
 #ifdef RP_GEMM_PROBE
@@ -2629,8 +2661,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-  const int t = rp_xcd_remap(blockIdx.x, (int)gridDim.x);
-  const int rb = t / LX_TN, nt = t % LX_TN;
+  int rb, nt;
+  lx_tile(blockIdx.x, ws, rb, nt);
   const int64_t m0 = (int64_t)rb * BM, n0 = (int64_t)nt * BN;
   f32x4 acc[4][4];
 #pragma unroll
@@ -2664,8 +2696,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-  const int t = rp_xcd_remap(blockIdx.x, (int)gridDim.x);
-  const int rb = t / LX_TN, nt = t % LX_TN;
+  int rb, nt;
+  lx_tile(blockIdx.x, ws, rb, nt);
   const int64_t m0 = (int64_t)rb * BM, n0 = (int64_t)nt * BN;
   f32x4 acc[4][4];
 #pragma unroll
@@ -2713,9 +2745,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx64_kernel(int64_t M, int64_t K,
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-  const int t = rp_xcd_remap(blockIdx.x, (int)gridDim.x);
-  const int nt = t % LX_TN;
-  const int64_t m0 = (int64_t)(t / LX_TN) * TR, n0 = (int64_t)nt * BN;
+  int rb, nt;
+  lx_tile(blockIdx.x, ws, rb, nt);
+  const int64_t m0 = (int64_t)rb * TR, n0 = (int64_t)nt * BN;
   f32x4 acc[MI][4];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -2955,24 +2987,159 @@ extern "C" int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const v
 extern "C" int64_t rp_gemm_ln_xchg_bytes(int64_t M) {
   return 256 + (M > 0 ? (M + BM - 1) / BM : 0) * LX_REC;
 }
-static LnxWs lnx_ws(void* base, int64_t) { return LnxWs{(uint32_t*)base, (char*)base + 256}; }
+
+// The fault word: one host-mapped word per process (allocated on the first exchange launch, never in a
+// kernel), set by any exchange wait that gives up.  The host reads it without synchronising, so a fault
+// is reported by the next rp_gemm_ln_* call (or rp_gemm_ln_status) after the faulting kernel ran.
+static std::mutex g_lx_mu;
+static uint32_t* g_lx_fault_host = nullptr;
+static uint32_t* g_lx_fault_dev = nullptr;
+constexpr double LX_TIMEOUT_S = 10.0;  // give-up bound of a partner wait (co-resident partners: microseconds)
+
+static int lx_fault_word(uint32_t** dev) {
+  std::lock_guard<std::mutex> lk(g_lx_mu);
+  if (!g_lx_fault_host) {
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, 256, hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        !h) {
+      (void)hipGetLastError();
+      rp_set_error("rp_gemm_ln: cannot allocate the exchange fault word (hipHostMalloc)");
+      return RP_ERR_LAUNCH;
+    }
+    memset(h, 0, 256);
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+      (void)hipGetLastError();
+      (void)hipHostFree(h);
+      rp_set_error("rp_gemm_ln: no device address for the exchange fault word");
+      return RP_ERR_LAUNCH;
+    }
+    g_lx_fault_host = (uint32_t*)h;
+    g_lx_fault_dev = (uint32_t*)d;
+  }
+  *dev = g_lx_fault_dev;
+  return RP_OK;
+}
+
+static int lx_fault_check(const char* fn) {
+  const uint32_t* h = g_lx_fault_host;
+  if (h && __atomic_load_n(h, __ATOMIC_ACQUIRE) != 0) {
+    rp_set_error("%s: an earlier GEMM + LayerNorm exchange launch gave up waiting for the partner tiles of a row "
+                 "block (a partner workgroup was not resident within %.0f s): its LayerNorm outputs are invalid and "
+                 "its exchange workspace is inconsistent; call rp_gemm_ln_reset on that workspace",
+                 fn, LX_TIMEOUT_S);
+    return RP_ERR_LAUNCH;
+  }
+  return RP_OK;
+}
+
+extern "C" int rp_gemm_ln_status(void) { return lx_fault_check("rp_gemm_ln_status"); }
+
+extern "C" int rp_gemm_ln_reset(void* xchg, int64_t M, void* stream) {
+  RP_REQUIRE(M >= 0, "rp_gemm_ln_reset: negative M");
+  RP_REQUIRE(!xchg || (((uintptr_t)xchg) & 255u) == 0, "rp_gemm_ln_reset: xchg must be 256-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  // the faulting launch may still run (its give-up workgroups finish their tiles): drain it first
+  if (hipStreamSynchronize(s) != hipSuccess) return rp_check_launch("rp_gemm_ln_reset");
+  if (xchg && hipMemsetAsync(xchg, 0, (size_t)rp_gemm_ln_xchg_bytes(M), s) != hipSuccess)
+    return rp_check_launch("rp_gemm_ln_reset");
+  if (hipStreamSynchronize(s) != hipSuccess) return rp_check_launch("rp_gemm_ln_reset");
+  if (g_lx_fault_host) __atomic_store_n(g_lx_fault_host, 0u, __ATOMIC_RELEASE);
+  return RP_OK;
+}
 
 // Exchange tile height: the tallest of 128 / 64 / 32 rows whose grid gives every CU two workgroups, else
 // 32 (M is a multiple of 64).  Interleaved whole-step A/B (profiles/r05_lnx64_ab.txt): bench shape
 // (M = 16384) 13.98 ms on 128-row tiles vs 15.11 on 64-row ones; config 2 (M = 8192, one 128-row tile per
 // CU) 7.11 vs 7.04 on 64-row tiles; config 4 (M = 4096) 7.03 on 64-row tiles vs 7.12 unfused.
-// RP_LNX_ROWS = 32 | 64 | 128 (A/B, read per launch) prefers that height where M allows it.
+static int g_lnx_rows_forced = 0;  // rp_debug_set_lnx_rows (tests: every tile height at small M)
 static int lnx_rows(int64_t M) {
-  const char* e = getenv("RP_LNX_ROWS");
-  if (e && e[0] == '3') return 32;
-  if (e && e[0] == '6') return 64;
-  if (e && e[0] == '1') return M % 128 == 0 ? 128 : 64;
+  const int f = g_lnx_rows_forced;
+  if (f == 32 || f == 64) return f;
+  if (f == 128) return M % 128 == 0 ? 128 : 64;
   const int64_t two = 2 * gemm_cu_count();
   if (M % 128 == 0 && (M / 128) * LX_TN >= two) return 128;
   return (M / 64) * LX_TN >= two ? 64 : 32;
 }
 
+// Co-resident capacity of an exchange kernel: CUs x workgroups per CU (the occupancy query, at most 2 —
+// the __launch_bounds__ residency the tile shapes are sized for).  A launch never exceeds it.
+static int64_t lx_capacity(const void* kern) {
+  static std::mutex mu;
+  static const void* keys[16] = {nullptr};
+  static int vals[16] = {0};
+  int per = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (int i = 0; i < 16 && keys[i]; ++i)
+      if (keys[i] == kern) per = vals[i];
+    if (!per) {
+      int n = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, NT, 0) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        n = 1;
+      }
+      per = n < 2 ? n : 2;
+      for (int i = 0; i < 16; ++i)
+        if (!keys[i]) {
+          keys[i] = kern;
+          vals[i] = per;
+          break;
+        }
+    }
+  }
+  return gemm_cu_count() * per;
+}
+
+// One seam as launches of at most the co-resident capacity (whole row blocks each); max_tiles < 0: all
+// tiles (a debug launch passes fewer, leaving a row block without a partner)
+template <typename Kern>
+static int lx_launch(Kern kern, const char* fn, int tr, int64_t M, int64_t K, const GlnDev& d, void* xchg, int pf,
+                     hipStream_t s, int64_t max_tiles, double timeout_s) {
+  uint32_t* fault = nullptr;
+  const int rc = lx_fault_word(&fault);
+  if (rc) return rc;
+  const int64_t nrb = M / tr;
+  int64_t cap = lx_capacity(reinterpret_cast<const void*>(kern)) / LX_TN;
+  if (cap < 1) cap = 1;
+  const uint64_t limit = (uint64_t)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+  for (int64_t r0 = 0; r0 < nrb; r0 += cap) {
+    const int64_t n = nrb - r0 < cap ? nrb - r0 : cap;
+    int64_t grid = n * LX_TN;
+    if (max_tiles >= 0 && grid > max_tiles) grid = max_tiles;
+    if (grid <= 0) break;
+    const LnxWs ws{(uint32_t*)xchg, (char*)xchg + 256, fault, limit, (int)r0, (int)n};
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, M, K, d, ws, pf);
+    if (max_tiles >= 0) max_tiles -= grid;
+  }
+  return rp_check_launch(fn);
+}
+
+// the exchange launch of a seam (tile height by lnx_rows)
+static int lx_dispatch(bool fwd, int64_t M, int64_t K, const GlnDev& d, void* xchg, hipStream_t s, int64_t max_tiles,
+                       double timeout_s) {
+  const char* fn = fwd ? "rp_gemm_ln_fwd" : "rp_gemm_ln_bwd";
+  const int xrows = lnx_rows(M);
+  const int pf = lnx_prefetch();
+  if (xrows == 64)
+    return fwd ? lx_launch(gemm_lnx64_kernel<true, 2>, fn, 64, M, K, d, xchg, pf && K >= 64 * lx_pfs<2>(), s,
+                           max_tiles, timeout_s)
+               : lx_launch(gemm_lnx64_kernel<false, 2>, fn, 64, M, K, d, xchg, pf && K >= 64 * lx_pfs<2>(), s,
+                           max_tiles, timeout_s);
+  if (xrows == 32)
+    return fwd ? lx_launch(gemm_lnx64_kernel<true, 1>, fn, 32, M, K, d, xchg, pf && K >= 64 * lx_pfs<1>(), s,
+                           max_tiles, timeout_s)
+               : lx_launch(gemm_lnx64_kernel<false, 1>, fn, 32, M, K, d, xchg, pf && K >= 64 * lx_pfs<1>(), s,
+                           max_tiles, timeout_s);
+  return fwd ? lx_launch(gemm_lnx_fwd_kernel, fn, BM, M, K, d, xchg, pf && K >= 64 * lx_pfs<4>(), s, max_tiles,
+                         timeout_s)
+             : lx_launch(gemm_lnx_bwd_kernel, fn, BM, M, K, d, xchg, pf && K >= 64 * lx_pfs<4>(), s, max_tiles,
+                         timeout_s);
+}
+
 static int gemm_ln_common(const char* fn, int64_t M, int64_t K, const rp_gemm_ln_args* p, GlnDev& d) {
+  const int fc = lx_fault_check(fn);
+  if (fc) return fc;
   RP_REQUIRE(p, "%s: null args", fn);
   RP_REQUIRE(M >= 0 && K > 0 && M % GL_BM == 0 && K % GL_BK == 0, "%s: M must be a multiple of 64 and K of 64 (M=%lld K=%lld)",
              fn, (long long)M, (long long)K);
@@ -2993,8 +3160,7 @@ static int gemm_ln_common(const char* fn, int64_t M, int64_t K, const rp_gemm_ln
   return RP_OK;
 }
 
-extern "C" int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, void* stream) {
-  GlnDev d;
+static int gemm_ln_fwd_prep(int64_t M, int64_t K, const rp_gemm_ln_args* p, GlnDev& d) {
   const int rc = gemm_ln_common("rp_gemm_ln_fwd", M, K, p, d);
   if (rc) return rc;
   RP_REQUIRE(p->ldw >= K && p->ldw % 8 == 0, "rp_gemm_ln_fwd: W must be [512][ldw >= K]");
@@ -3008,28 +3174,10 @@ extern "C" int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   d.residual = p->residual; d.ldr = p->ldr;
   d.xo = p->x_out; d.ldxo = p->ldx_out;
   d.h = (bf16*)p->h_out; d.ldh = p->ldh;
-  if (M == 0) return RP_OK;
-  const int xrows = p->xchg ? lnx_rows(M) : 0;
-  if (xrows == 64 || xrows == 32) {
-    if (xrows == 64)
-      hipLaunchKernelGGL((gemm_lnx64_kernel<true, 2>), dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
-                         M, K, d, lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<2>() ? 1 : 0);
-    else
-      hipLaunchKernelGGL((gemm_lnx64_kernel<true, 1>), dim3((unsigned)(M / 32 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
-                         M, K, d, lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<1>() ? 1 : 0);
-    return rp_check_launch("rp_gemm_ln_fwd");
-  }
-  if (p->xchg) {
-    hipLaunchKernelGGL(gemm_lnx_fwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
-                       lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<4>() ? 1 : 0);
-    return rp_check_launch("rp_gemm_ln_fwd");
-  }
-  hipLaunchKernelGGL(gemm_ln_fwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
-  return rp_check_launch("rp_gemm_ln_fwd");
+  return RP_OK;
 }
 
-extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, void* stream) {
-  GlnDev d;
+static int gemm_ln_bwd_prep(int64_t M, int64_t K, const rp_gemm_ln_args* p, GlnDev& d) {
   const int rc = gemm_ln_common("rp_gemm_ln_bwd", M, K, p, d);
   if (rc) return rc;
   RP_REQUIRE(p->ldw >= 512 && p->ldw % 8 == 0, "rp_gemm_ln_bwd: W must be [K][ldw >= 512]");
@@ -3048,24 +3196,62 @@ extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, vo
   d.lp_scale = p->lp_dropout_p > 0.f ? 1.f / (1.f - p->lp_dropout_p) : 1.f;
   d.lp_seed = p->lp_seed;
   d.dgamma_part = p->dgamma_part; d.dbeta_part = p->dbeta_part; d.ld_part = p->ld_part;
+  return RP_OK;
+}
+
+extern "C" int rp_gemm_ln_fwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, void* stream) {
+  GlnDev d;
+  const int rc = gemm_ln_fwd_prep(M, K, p, d);
+  if (rc) return rc;
   if (M == 0) return RP_OK;
-  const int xrows = p->xchg ? lnx_rows(M) : 0;
-  if (xrows == 64 || xrows == 32) {
-    if (xrows == 64)
-      hipLaunchKernelGGL((gemm_lnx64_kernel<false, 2>), dim3((unsigned)(M / 64 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
-                         M, K, d, lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<2>() ? 1 : 0);
-    else
-      hipLaunchKernelGGL((gemm_lnx64_kernel<false, 1>), dim3((unsigned)(M / 32 * LX_TN)), dim3(NT), 0, (hipStream_t)stream,
-                         M, K, d, lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<1>() ? 1 : 0);
-    return rp_check_launch("rp_gemm_ln_bwd");
-  }
-  if (p->xchg) {
-    hipLaunchKernelGGL(gemm_lnx_bwd_kernel, dim3((unsigned)(M / BM * LX_TN)), dim3(NT), 0, (hipStream_t)stream, M, K, d,
-                       lnx_ws(p->xchg, M), lnx_prefetch() && K >= 64 * lx_pfs<4>() ? 1 : 0);
-    return rp_check_launch("rp_gemm_ln_bwd");
-  }
+  if (p->xchg) return lx_dispatch(true, M, K, d, p->xchg, (hipStream_t)stream, -1, LX_TIMEOUT_S);
+  hipLaunchKernelGGL(gemm_ln_fwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
+  return rp_check_launch("rp_gemm_ln_fwd");
+}
+
+extern "C" int rp_gemm_ln_bwd(int64_t M, int64_t K, const rp_gemm_ln_args* p, void* stream) {
+  GlnDev d;
+  const int rc = gemm_ln_bwd_prep(M, K, p, d);
+  if (rc) return rc;
+  if (M == 0) return RP_OK;
+  if (p->xchg) return lx_dispatch(false, M, K, d, p->xchg, (hipStream_t)stream, -1, LX_TIMEOUT_S);
   hipLaunchKernelGGL(gemm_ln_bwd_kernel, dim3((unsigned)(M / GL_BM)), dim3(GL_NT), 0, (hipStream_t)stream, M, K, d);
   return rp_check_launch("rp_gemm_ln_bwd");
+}
+
+// Test hooks (include/rp_api.h, "Debug"): an exchange launch with only the first `tiles` workgroups and
+// its own give-up bound (a row block left without a partner must fail loudly, not hang or corrupt
+// silently), and a kernel that holds CU slots for a while (a seam beside another stream's long kernel).
+extern "C" int rp_debug_gemm_ln_partial(int fwd, int64_t M, int64_t K, const rp_gemm_ln_args* p, int64_t tiles,
+                                        double timeout_s, void* stream) {
+  GlnDev d;
+  const int rc = fwd ? gemm_ln_fwd_prep(M, K, p, d) : gemm_ln_bwd_prep(M, K, p, d);
+  if (rc) return rc;
+  RP_REQUIRE(p->xchg && M > 0 && tiles >= 0 && timeout_s > 0.0 && timeout_s <= 60.0,
+             "rp_debug_gemm_ln_partial: needs an exchange workspace, M > 0, tiles >= 0, 0 < timeout_s <= 60");
+  return lx_dispatch(fwd != 0, M, K, d, p->xchg, (hipStream_t)stream, tiles, timeout_s);
+}
+
+extern "C" int rp_debug_set_lnx_rows(int rows) {
+  RP_REQUIRE(rows == 0 || rows == 32 || rows == 64 || rows == 128, "rp_debug_set_lnx_rows: 0 (automatic), 32, 64 or 128");
+  g_lnx_rows_forced = rows;
+  return RP_OK;
+}
+
+__global__ __launch_bounds__(NT) void occupy_kernel(uint64_t ticks, float* sink) {
+  __shared__ float lds[16384];  // 64 KiB: two such workgroups fill a CU's LDS with the seams' 69 KB tiles
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  lds[threadIdx.x] = (float)threadIdx.x;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  __syncthreads();
+  if (sink && threadIdx.x == 0 && lds[(blockIdx.x * 7) & (NT - 1)] < 0.f) sink[blockIdx.x] = 1.f;
+}
+
+extern "C" int rp_debug_occupy(int blocks, int us, void* stream) {
+  RP_REQUIRE(blocks > 0 && blocks <= 65536 && us > 0 && us <= 10000000, "rp_debug_occupy: 0 < blocks <= 65536, 0 < us <= 1e7");
+  hipLaunchKernelGGL(occupy_kernel, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, (uint64_t)us * 100u,
+                     (float*)nullptr);
+  return rp_check_launch("rp_debug_occupy");
 }
 
 #ifdef RP_GEMM_PROBE

@@ -25,6 +25,7 @@ import datetime
 import logging
 import os
 import socket
+import threading
 import time
 from typing import Any, Dict, Optional
 
@@ -250,6 +251,7 @@ class DataParallelModel(nn.Module):
         self._replicas = []  # replicas 1.. (plain list: not sub-modules, so state_dict / parameters are .module's)
         self._queued = False
         self._done_events = []
+        self._lock = threading.Lock()  # replica hooks run on the autograd engine's per-device threads
 
     def _replica(self, i):
         import copy
@@ -266,19 +268,22 @@ class DataParallelModel(nn.Module):
         # end, on the engine's thread for that device): an event there orders the cross-device read
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream())
-        self._done_events.append(ev)
-        if not self._queued:  # once per backward: after the engine has run every replica's backward
+        with self._lock:  # check-then-set and the event list shared by the per-device engine threads
+            self._done_events.append(ev)
+            queue = not self._queued
             self._queued = True
+        if queue:  # once per backward: after the engine has run every replica's backward
             torch.autograd.Variable._execution_engine.queue_callback(self._reduce)
 
     def _reduce(self):
-        self._queued = False
+        with self._lock:
+            self._queued = False
+            events, self._done_events = self._done_events, []
         g0 = self.module.flat_grads()
         n = self.module.trainable_numel()
         s0 = torch.cuda.current_stream(g0.device)
-        for ev in self._done_events:  # device 0 reads the replicas' gradients only once they are written
+        for ev in events:  # device 0 reads the replicas' gradients only once they are written
             s0.wait_event(ev)
-        self._done_events = []
         with torch.cuda.stream(s0):
             for r in self._active:
                 g0[:n].add_(r.flat_grads()[:n].to(g0.device, non_blocking=True))

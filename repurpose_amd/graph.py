@@ -146,6 +146,7 @@ class CapturedTrainStep:
         else:
             self._stage(torch.cuda.current_stream(self.device))
         self._graph.replay()
+        K.lnx_status()  # an exchange seam that gave up in an earlier replay fails loudly (host-mapped word)
         self.opt._step += 1
         if self.opt._step_t is not None:
             self.opt._step_t.fill_(float(self.opt._step))

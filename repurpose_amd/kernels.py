@@ -201,25 +201,64 @@ def linear_wgrad_grouped(items, accumulate=True):
 
 
 # ----------------------------------------------------------------------- GEMM + LayerNorm seams
-_LNX = {}
+_LNX = {}        # device -> [workspace (uint8), rows it serves, last stream that used it]
+_LNX_KEEP = []   # every workspace ever handed out: a captured graph holds their raw pointers
+_LNX_MIN_ROWS = 65536  # first allocation: 2.2 MB, enough for B * T up to 65,536 rows
 
 
 def _lnx_ws(dev, M):
-    """The exchange workspace of the GEMM + LayerNorm exchange kernels (128 x 128 tiles, or 64 x 128 where
-    the 128-row grid would leave CUs idle; rp_gemm_ln_xchg_bytes, zero-filled once; every launch leaves
-    it zeroed), one per device, grown as needed.  Launches sharing it must be ordered: the drop-in issues
-    every seam on the device's current stream (a captured step replays on the stream its eager steps
-    use), so one per device suffices — and the capture stream does not get a workspace of its own, whose
-    zero fill would be captured into every replay.  RP_GEMM_LNX=0 (A/B): None, i.e. the 64-row full-row
-    kernels."""
+    """The exchange workspace of the GEMM + LayerNorm exchange kernels (rp_gemm_ln_xchg_bytes, zero-filled
+    once; every launch leaves it zeroed), one per device.  It is never freed: a workspace that is too small
+    is replaced by a larger one but kept alive, because a captured step's graph holds the raw pointer of
+    the workspace it was captured with.  Launches sharing it must be ordered: when the current stream
+    differs from the one that used it last (and no capture is running), the current stream waits for the
+    other's work so far.  RP_GEMM_LNX=0 (A/B): None, i.e. the 64-row full-row kernels."""
     if M % 64 or os.environ.get("RP_GEMM_LNX", "1") != "1":
         return None
-    need = int(N.load().rp_gemm_ln_xchg_bytes(M))
-    ws = _LNX.get(dev)
-    if ws is None or ws.numel() < need:
-        ws = torch.zeros(need, device=dev, dtype=torch.uint8)
-        _LNX[dev] = ws
-    return ws
+    ent = _LNX.get(dev)
+    if ent is None or ent[1] < M:
+        rows = max(M, _LNX_MIN_ROWS if ent is None else 2 * ent[1])
+        ws = torch.zeros(int(N.load().rp_gemm_ln_xchg_bytes(rows)), device=dev, dtype=torch.uint8)
+        _LNX_KEEP.append(ws)
+        ent = [ws, rows, None]
+        _LNX[dev] = ent
+    cur = torch.cuda.current_stream(dev)
+    last = ent[2]
+    if last is not None and last != cur and not torch.cuda.is_current_stream_capturing():
+        ev = torch.cuda.Event()
+        ev.record(last)
+        cur.wait_event(ev)
+    ent[2] = cur
+    return ent[0]
+
+
+def lnx_status():
+    """Raise RuntimeError if an exchange wait has given up since the last reset (rp_gemm_ln_status: a
+    host-mapped word, no synchronisation); the workspaces are then re-zeroed and the fault cleared, so the
+    next launch starts clean."""
+    if N.load().rp_gemm_ln_status() != N.RP_OK:
+        msg = N.last_error()
+        lnx_reset()
+        raise RuntimeError(f"rp_gemm_ln_status: {msg}")
+
+
+def lnx_reset():
+    """rp_gemm_ln_reset on every device's exchange workspace (synchronises their streams)."""
+    for dev, (ws, rows, last) in _LNX.items():
+        st = last if last is not None else torch.cuda.current_stream(dev)
+        N.call("rp_gemm_ln_reset", _p(ws), int(rows), ctypes.c_void_p(st.cuda_stream))
+    if not _LNX:
+        N.call("rp_gemm_ln_reset", ctypes.c_void_p(0), 0, ctypes.c_void_p(0))
+
+
+def _lnx_call(name, M, K, args, stream):
+    """rp_gemm_ln_fwd / bwd; a fault reported by the call resets the workspaces before it raises."""
+    rc = getattr(N.load(), name)(M, K, ctypes.byref(args), stream)
+    if rc != N.RP_OK:
+        msg = N.last_error()
+        if N.load().rp_gemm_ln_status() != N.RP_OK:
+            lnx_reset()
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
 
 
 def linear_ln_fwd(x, W, b, residual, gamma, beta, eps=1e-5, dropout_p=0.0, seed=0, seed_base=None):
@@ -227,6 +266,16 @@ def linear_ln_fwd(x, W, b, residual, gamma, beta, eps=1e-5, dropout_p=0.0, seed=
     ``h = LayerNorm(y)`` (bf16) with its mean / rstd — linear_fwd(..., residual=...) followed by
     layernorm_fwd(y, out_f32=False, lp_dtype=bf16): y bitwise; h / mean / rstd bitwise on the 64-row
     kernels, to fp32 rounding of the row sums on the exchange kernels (the default; RP_GEMM_LNX=0 A/B).  x [M, K] bf16, W [512, K] bf16, M % 64 == 0.  Returns (y, h, mean, rstd)."""
+    a, outs = ln_fwd_args(x, W, b, residual, gamma, beta, eps, dropout_p, seed, seed_base)
+    M, K = x.shape
+    e0 = _tick("gemm_ln_fwd")
+    _lnx_call("rp_gemm_ln_fwd", M, K, a, _stream(x))
+    _tock(e0, 2.0 * M * 512 * K)
+    return outs
+
+
+def ln_fwd_args(x, W, b, residual, gamma, beta, eps=1e-5, dropout_p=0.0, seed=0, seed_base=None):
+    """(rp_gemm_ln_args, (y, h, mean, rstd)) of linear_ln_fwd, outputs allocated, nothing launched."""
     _gpu(x, W, b, residual, gamma, beta)
     _seed_word(seed_base)
     M, K = x.shape
@@ -240,10 +289,7 @@ def linear_ln_fwd(x, W, b, residual, gamma, beta, eps=1e-5, dropout_p=0.0, seed=
                      residual=_p(residual).value, ldr=residual.stride(0), x_out=_p(y).value, ldx_out=512,
                      gamma=_p(gamma).value, beta=_p(beta).value, eps=float(eps), h_out=_p(h).value, ldh=512,
                      mean=_p(mean).value, rstd=_p(rstd).value, xchg=_p(_lnx_ws(dev, M)).value)
-    e0 = _tick("gemm_ln_fwd")
-    N.call("rp_gemm_ln_fwd", M, K, ctypes.byref(a), _stream(x))
-    _tock(e0, 2.0 * M * 512 * K)
-    return y, h, mean, rstd
+    return a, (y, h, mean, rstd)
 
 
 def linear_ln_bwd(dy, W, x, mean, rstd, gamma, dres=None, lp_dtype=None, lp_dropout_p=0.0, lp_seed=0, dgamma=None,
@@ -253,6 +299,23 @@ def linear_ln_bwd(dy, W, x, mean, rstd, gamma, dres=None, lp_dtype=None, lp_drop
     layernorm_bwd(dh, x, mean, rstd, gamma, dres=..., lp_dtype=..., ...), bitwise on the 64-row kernels and
     to fp32 rounding of the row sums on the exchange kernels (as linear_ln_fwd); dh is never written.
     Returns (dx fp32, dx_lp or None); gamma / beta partials as layernorm_bwd (``defer`` / ``ws``)."""
+    a, (dx, dxl, jobs) = ln_bwd_args(dy, W, x, mean, rstd, gamma, dres, lp_dtype, lp_dropout_p, lp_seed, dgamma,
+                                     dbeta, seed_base)
+    M, K = dy.shape
+    e0 = _tick("gemm_ln_bwd")
+    _lnx_call("rp_gemm_ln_bwd", M, K, a, _stream(dy))
+    _tock(e0, 2.0 * M * 512 * K)
+    if defer is not None:
+        defer.extend(jobs)
+    else:
+        for p, o in jobs:
+            colsum(p, out=o, accumulate=True, ws=ws)
+    return dx, dxl
+
+
+def ln_bwd_args(dy, W, x, mean, rstd, gamma, dres=None, lp_dtype=None, lp_dropout_p=0.0, lp_seed=0, dgamma=None,
+                dbeta=None, seed_base=None):
+    """(rp_gemm_ln_args, (dx, dx_lp, gamma / beta partial jobs)) of linear_ln_bwd, nothing launched."""
     _gpu(dy, W, x, mean, rstd, gamma, dres)
     _seed_word(seed_base)
     M, K = dy.shape
@@ -277,17 +340,9 @@ def linear_ln_bwd(dy, W, x, mean, rstd, gamma, dres=None, lp_dtype=None, lp_drop
                      dx=_p(dx).value, lddx=D, dx_lp=_p(dxl).value, lddx_lp=D, lp_dropout_p=float(lp_dropout_p),
                      lp_seed=int(lp_seed) & 0xFFFFFFFF, dgamma_part=_p(pg).value, dbeta_part=_p(pb).value,
                      ld_part=ld_part, xchg=_p(_lnx_ws(dev, M)).value)
-    e0 = _tick("gemm_ln_bwd")
-    N.call("rp_gemm_ln_bwd", M, K, ctypes.byref(a), _stream(dy))
-    _tock(e0, 2.0 * M * 512 * K)
     jobs = [(part, dgamma.as_strided((2 * D,), (1,)))] if both else \
         [(p, o) for p, o in ((pg, dgamma), (pb, dbeta)) if o is not None]
-    if defer is not None:
-        defer.extend(jobs)
-    else:
-        for p, o in jobs:
-            colsum(p, out=o, accumulate=True, ws=ws)
-    return dx, dxl
+    return a, (dx, dxl, jobs)
 
 
 # ------------------------------------------------------------------------------------- LayerNorm

@@ -6,9 +6,12 @@ for bit; the 128 x 128 kernels whose column tiles exchange the row statistics wi
 LayerNorm outputs to fp32 rounding of the row sums, the exchange workspace left zeroed, no wait given up.
 Shapes are the encoder's: K = 512 (out_proj) and 2048 (linear2) forward, K = 2048 (linear1) and 1536
 (in_proj) backward, plus the bench's row count."""
+import ctypes
+
 import pytest
 import torch
 
+from repurpose_amd import _native as N
 from repurpose_amd import kernels as K
 
 
@@ -101,12 +104,17 @@ def test_model_fused_seams_bitwise(dev, monkeypatch):
     assert torch.equal(g0, g1), f"grads: {(g0 - g1).abs().max().item():.3e}"
 
 
+def _force_rows(rows):
+    N.call("rp_debug_set_lnx_rows", int(rows))
+
+
 @pytest.fixture(params=["32", "64", "128"])
-def lnx_rows(request, monkeypatch):
+def lnx_rows(request):
     """The exchange tile height: 32 x 128 or 64 x 128 tiles (the host's choices where taller tiles would
-    leave CUs idle) or 128 x 128 ones (M % 128 == 0, else 64), RP_LNX_ROWS read per launch."""
-    monkeypatch.setenv("RP_LNX_ROWS", request.param)
-    return request.param
+    leave CUs idle) or 128 x 128 ones (M % 128 == 0, else 64), forced by the rp_debug_set_lnx_rows hook."""
+    _force_rows(request.param)
+    yield request.param
+    _force_rows(0)
 
 
 def _ws_clean(dev, M):
@@ -224,13 +232,20 @@ def test_model_fused_seams_exchange(dev, lnx_rows, monkeypatch):
     _ws_clean(dev, 512)
 
 
-def test_linear_ln_exchange_mixed_rows(dev, monkeypatch):
+def test_linear_ln_exchange_mixed_rows(dev):
     """One workspace shared by launches of different row counts and tile heights (the record of a row
     block does not move with M or the kernel): each launch agrees with the unfused pair and leaves the
     counters zeroed."""
+    try:
+        _mixed_rows(dev)
+    finally:
+        _force_rows(0)
+
+
+def _mixed_rows(dev):
     for M, rows in ((4096, "128"), (8192, "64"), (16384, "128"), (1024, "64"), (8192, "128"), (384, "64"),
                     (4096, "32"), (320, "128"), (8192, "32"), (4096, "64"), (192, "32")):
-        monkeypatch.setenv("RP_LNX_ROWS", rows)
+        _force_rows(rows)
         g = torch.Generator().manual_seed(M)
         x, W = _r(g, M, 512, dev=dev), _r(g, D, 512, dev=dev, sc=0.03)
         b, res = _r(g, D, dev=dev, dt=torch.float32, sc=0.1), _r(g, M, D, dev=dev, dt=torch.float32)
@@ -242,3 +257,98 @@ def test_linear_ln_exchange_mixed_rows(dev, monkeypatch):
         torch.testing.assert_close(rs1, rs0, rtol=1e-5, atol=0)
         _close_bf16(h0, h1)
         _ws_clean(dev, M)
+
+
+# ------------------------------------------------------------------ exchange progress and fault reporting
+def _fwd_case(dev, M, Kd, seed):
+    g = torch.Generator().manual_seed(seed)
+    x, W = _r(g, M, Kd, dev=dev), _r(g, D, Kd, dev=dev, sc=0.03)
+    b, res = _r(g, D, dev=dev, dt=torch.float32, sc=0.1), _r(g, M, D, dev=dev, dt=torch.float32)
+    gm, bt = 1.0 + _r(g, D, dev=dev, dt=torch.float32, sc=0.1), _r(g, D, dev=dev, dt=torch.float32, sc=0.1)
+    return x, W, b, res, gm, bt
+
+
+def _fwd_check(x, W, b, res, gm, bt, p=0.1):
+    y0 = K.linear_fwd(x, W, b, out_dtype=torch.float32, dropout_p=p, seed=9, residual=res)
+    _, h0, mu0, rs0 = K.layernorm_fwd(y0, gm, bt, out_f32=False, lp_dtype=torch.bfloat16)
+    y1, h1, mu1, rs1 = K.linear_ln_fwd(x, W, b, res, gm, bt, dropout_p=p, seed=9)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    torch.testing.assert_close(mu1, mu0, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rs1, rs0, rtol=1e-5, atol=0)
+    _close_bf16(h0, h1)
+
+
+@pytest.mark.parametrize("fwd", [True, False])
+def test_exchange_missing_partner_fails_loudly(dev, fwd):
+    """A launch whose last row block lacks a partner tile (the test hook launches one workgroup fewer than
+    the grid) gives up after its bound and sets the library's fault word: rp_gemm_ln_status and the next
+    seam call raise RuntimeError (never a silent result), the workspace is reset, and the seams that follow
+    agree with the unfused pair again with the counters left zeroed."""
+    M, Kd = 4096, 512
+    x, W, b, res, gm, bt = _fwd_case(dev, M, Kd, 21)
+    assert N.load().rp_gemm_ln_status() == N.RP_OK
+    if fwd:
+        a, outs = K.ln_fwd_args(x, W, b, res, gm, bt)
+    else:
+        _, _, mu, rs = K.layernorm_fwd(res, gm, bt, out_f32=False, lp_dtype=torch.bfloat16)
+        a, outs = K.ln_bwd_args(x, W.t().contiguous(), res, mu, rs, gm, dres=res, lp_dtype=torch.bfloat16)
+    tiles = 127  # the first 127 workgroups: every row block of the first four 32-block chunks but the last is whole
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    N.call("rp_debug_gemm_ln_partial", int(fwd), M, Kd, ctypes.byref(a), tiles, 0.05, st)
+    torch.cuda.synchronize()
+    assert N.load().rp_gemm_ln_status() == N.RP_ERR_LAUNCH
+    assert "gave up" in N.last_error()
+    with pytest.raises(RuntimeError, match="gave up"):  # the next seam call refuses to run
+        K.linear_ln_fwd(x, W, b, res, gm, bt)
+    assert N.load().rp_gemm_ln_status() == N.RP_OK  # reset by the failing call's handler
+    _ws_clean(dev, M)
+    _fwd_check(x, W, b, res, gm, bt)
+    _ws_clean(dev, M)
+    # the same through the status check a captured step's replay runs
+    N.call("rp_debug_gemm_ln_partial", int(fwd), M, Kd, ctypes.byref(a), tiles, 0.05, st)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="gave up"):
+        K.lnx_status()
+    K.lnx_status()
+    _ws_clean(dev, M)
+
+
+def test_exchange_beside_long_kernel(dev):
+    """A seam launched while another stream's long kernel holds CU slots (384 workgroups with 64 KiB of LDS
+    each for 150 ms: half the CUs cannot take a seam workgroup until it retires): forward and backward
+    still equal the unfused pair, no wait gives up, the counters come back to zero."""
+    M = 16384
+    x, W, b, res, gm, bt = _fwd_case(dev, M, 512, 22)
+    dy = _r(torch.Generator().manual_seed(5), M, 2048, dev=dev)
+    W2 = _r(torch.Generator().manual_seed(6), 2048, D, dev=dev, sc=0.03)
+    _, _, mu, rs = K.layernorm_fwd(res, gm, bt, out_f32=False, lp_dtype=torch.bfloat16)
+    dh = K.linear_dgrad(dy, W2, out_dtype=torch.float32)
+    dx0, dl0 = K.layernorm_bwd(dh, res, mu, rs, gm, dres=res, lp_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream(dev)
+    for _ in range(2):
+        N.call("rp_debug_occupy", 384, 150000, ctypes.c_void_p(side.cuda_stream))
+        _fwd_check(x, W, b, res, gm, bt)
+        N.call("rp_debug_occupy", 384, 150000, ctypes.c_void_p(side.cuda_stream))
+        dx1, dl1 = K.linear_ln_bwd(dy, W2, res, mu, rs, gm, dres=res, lp_dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+        assert (dx1 - dx0).abs().max().item() <= 2e-6 * dx0.abs().max().item()
+        _close_bf16(dl0, dl1)
+    K.lnx_status()
+    _ws_clean(dev, M)
+
+
+@pytest.mark.parametrize("rows", ["128", "32"])
+def test_exchange_launches_split_at_capacity(dev, rows):
+    """Row counts whose exchange grid exceeds the co-resident capacity (CUs x 2) are issued as several
+    launches of whole row blocks: M = 32,768 on 128-row tiles (two launches on 256 CUs) and M = 16,384 on
+    forced 32-row tiles (four).  Results equal the unfused pair (dropout indices are the seam's global
+    rows), the counters return to zero."""
+    _force_rows(rows)
+    try:
+        M = 32768 if rows == "128" else 16384
+        _fwd_check(*_fwd_case(dev, M, 512, 23))
+        _ws_clean(dev, M)
+    finally:
+        _force_rows(0)

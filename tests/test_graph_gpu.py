@@ -154,3 +154,41 @@ def test_captured_backward_writes_every_gradient(dev, dtype):
     assert torch.equal(mg.flat_params()[:n], me.flat_params()[:n])
     assert torch.equal(og._m, oe._m) and torch.equal(og._v, oe._v)
     assert not mg._grad_fresh
+
+
+def test_replay_after_exchange_workspace_growth(dev, monkeypatch):
+    """The seams on the exchange kernels (forced at this small shape) inside a captured step: after the
+    capture a larger row count grows the device's exchange workspace (a new one is allocated; the one the
+    graph holds stays alive) and an eager seam runs on the new one; the replays that follow still equal
+    the eager steps bit for bit (a freed workspace under a live graph)."""
+    from repurpose_amd import kernels as K
+
+    monkeypatch.setenv("RP_GEMM_LN", "1")
+    batches = _batches(dev, 4)
+    me, oe = _model(dev, "bf16", 0.0)
+    for b in batches:
+        oe.zero_grad()
+        out = me(b)
+        (me.losses(*out)["cls_loss"] / 2).backward()
+        oe.step()
+    mg, og = _model(dev, "bf16", 0.0)
+    run = CapturedTrainStep(mg, og, {k: v.clone() for k, v in batches[0].items()}, warmup=1)
+    for i, b in enumerate(batches):
+        run.load(b)
+        run.step()
+        if i == 1:
+            held = K._LNX[dev][0].data_ptr()
+            big = 2 * K._LNX[dev][1] + 64
+            g = torch.Generator().manual_seed(3)
+            x = torch.randn(big, 512, generator=g).to(dev, torch.bfloat16)
+            W = (torch.randn(512, 512, generator=g) * 0.03).to(dev, torch.bfloat16)
+            v = torch.zeros(512, device=dev)
+            res = torch.randn(big, 512, generator=g).to(dev)
+            K.linear_ln_fwd(x, W, v, res, v + 1.0, v)
+            assert K._LNX[dev][0].data_ptr() != held
+            assert any(w.data_ptr() == held for w in K._LNX_KEEP)
+            del x, res
+    torch.cuda.synchronize()
+    n = me.trainable_numel()
+    assert torch.equal(mg.flat_params()[:n], me.flat_params()[:n])
+    K.lnx_status()
