@@ -207,6 +207,9 @@ def main():
                     help="replay the step as a captured HIP graph (auto: at N = 1 only; on: also the DP step "
                          "with its RCCL all-reduces captured)")
     ap.add_argument("--roofline-kernel", default="attn_bwd_dkdv", choices=list(KERNEL_FLOPS))
+    ap.add_argument("--no-adam-overlap", action="store_true",
+                    help="N > 1: one whole-buffer Adam after the exchange instead of one per all-reduce bucket "
+                         "right after its wait (FusedAdam.overlap_with)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ:
@@ -246,6 +249,8 @@ def main():
     model = MMCTransformer(**MODEL_CFG, compute_dtype=args.dtype).to(dev).train()
     opt = FusedAdam(model, lr=1e-3, weight_decay=1e-4)
     reducer = GradAllReducer(model) if dp else None
+    if reducer is not None and not args.no_adam_overlap:
+        opt.overlap_with(reducer)  # each bucket's Adam right after its wait: overlaps the exchange's tail
     B, T = args.batch, args.seq_len
     batch = synth_batch(B, T, dev, 1000 + rank)
 
@@ -303,9 +308,15 @@ def main():
     # events, and ~100 event pairs per eager step would themselves add ~0.6 ms to the timed steps)
     kern_steps = min(args.steps, 5)
     K.timer_start(*KERNEL_FLOPS, "gemm_wgrad", "adam")
+    if reducer is not None:
+        reducer.timing = []  # (before, after) events around every bucket's wait on the step stream
     for _ in range(kern_steps):
         eager_step()
     kern = K.timer_stop(detail=True)
+    waits = []
+    if reducer is not None:
+        waits = [a.elapsed_time(b) for a, b in reducer.timing]
+        reducer.timing = None
     kern_ms = {n: v[0] for n, v in kern.items()}
     value = world * B * T * args.steps / elapsed
 
@@ -340,7 +351,7 @@ def main():
                                  if n != rk and kern_ms.get(n) is not None]
         # the weight-gradient GEMMs (every Linear's dW = dY^T X + bias gradient, grouped or split-K):
         # algorithmic 2*N*K*T per launch summed over the timed launches
-        avg, n_l, tot, fl = kern["gemm_wgrad"]
+        avg, n_l, tot, fl, _ = kern["gemm_wgrad"]
         if n_l and fl:
             ach = fl / (tot * 1e-3) / 1e12
             roof["other_kernels"].append({"kernel": "gemm_wgrad (all shapes)", "bound": "mfma", "achieved": ach,
@@ -365,8 +376,20 @@ def main():
                "execution": ("hip-graph replay of the captured step" + (" (RCCL all-reduces captured)" if dp else ""))
                if use_graph else "eager (per-launch)"}
         if dp:
+            # where the DP step's time goes: the step stream's stalls on the bucket waits (the exchange not
+            # hidden behind the backward), the weight-gradient launches of one step in issue order (the
+            # grouped launch cut at each full round of tiles so early buckets' exchange overlaps the rest)
+            _, n_w, _, _, each_w = kern["gemm_wgrad"]
+            per = n_w // kern_steps if n_w else 0
             res["comm"] = {"backend": reducer.backend, "bucket_mb": reducer.bucket_elems * 4 / 2 ** 20,
-                           "allreduce_bytes_per_step": model.trainable_numel() * 4}
+                           "allreduce_bytes_per_step": model.trainable_numel() * 4,
+                           "buckets_per_step": len(waits) // kern_steps if waits else 0,
+                           "exposed_ms": sum(waits) / kern_steps if waits else None,
+                           "max_bucket_wait_ms": max(waits) if waits else None,
+                           "wgrad_launch_ms": each_w[-per:] if per else [],
+                           "adam": "per bucket after its wait" if reducer.on_bucket is not None else "whole buffer",
+                           "timing": "HIP events on the step stream around each bucket's wait, eager steps "
+                                     "after the timed region"}
         # SURVEY §8d reports the optimizer step separately: `value` includes it (whole train step)
         if kern.get("adam") and kern["adam"][0]:
             res["optimizer_ms_per_step"] = kern["adam"][2] / kern_steps

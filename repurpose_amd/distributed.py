@@ -129,8 +129,13 @@ class GradAllReducer:
     """Bucketed, backward-overlapped gradient averaging over a flat gradient buffer.
 
     ``ready(lo, hi)`` is called by the backward whenever flat range [lo, hi) holds final gradients
-    (ranges arrive in reverse layout order); ``finish()`` closes the step.  Works with any object
-    exposing ``flat_grads()``, ``trainable_numel()`` and ``_grad_ready_hooks``.
+    (ranges arrive in reverse layout order); ``finish()`` closes the step: it waits for every bucket
+    (stream-ordered under RCCL), so the gradients are final when ``backward()`` returns, as under DDP.
+    ``on_bucket(lo, hi)``, when set (``FusedAdam.overlap_with``), runs right after bucket [lo, hi)'s wait
+    on the step stream, before the next bucket's: the optimizer update of the first buckets then
+    overlaps the all-reduce of the last ones.  ``timing`` (a list, bench.py): a (before, after) pair
+    of HIP events around every wait, i.e. the time the step stream stalls on the exchange.  Works with
+    any object exposing ``flat_grads()``, ``trainable_numel()`` and ``_grad_ready_hooks``.
     """
 
     def __init__(self, model, bucket_mb: float = 25.0, group=None):
@@ -142,6 +147,8 @@ class GradAllReducer:
         self.pending = None  # [lo, hi) not yet launched
         self.works = []
         self.launched = []
+        self.on_bucket = None
+        self.timing = None
         model._grad_ready_hooks = [self.ready]
         model._grad_done_hooks = [self.finish]
 
@@ -153,10 +160,10 @@ class GradAllReducer:
             # moves nothing
             op = dist.ReduceOp.AVG if self.world > 1 else dist.ReduceOp.SUM
             w = dist.all_reduce(g, op=op, group=self.group, async_op=True)
-            self.works.append((w, None))
+            self.works.append((w, None, lo, hi))
         else:  # gloo has no AVG
             w = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            self.works.append((w, g))
+            self.works.append((w, g, lo, hi))
         self.launched.append((lo, hi))
 
     def ready(self, lo, hi):
@@ -181,11 +188,21 @@ class GradAllReducer:
         if self.pending is not None:
             self._launch(*self.pending)
             self.pending = None
-        for w, g in self.works:
+        works, self.works = self.works, []
+        for w, g, lo, hi in works:
+            e0 = None
+            if self.timing is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             w.wait()  # stream-ordered for RCCL: no host synchronisation
             if g is not None:
                 g.div_(self.world)
-        self.works = []
+            if e0 is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                self.timing.append((e0, e1))
+            if self.on_bucket is not None:
+                self.on_bucket(lo, hi)
 
     def wait(self):
         self.finish()

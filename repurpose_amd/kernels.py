@@ -31,7 +31,7 @@ def timer_start(*names):
 
 def timer_stop(detail=False):
     """{name: average duration (ms) of that kernel's launches since timer_start, or None}; with
-    detail, {name: (average ms, launches, total ms, total algorithmic FLOPs or None)}."""
+    detail, {name: (average ms, launches, total ms, total algorithmic FLOPs or None, [ms per launch])}."""
     ev = _timer["ev"]
     _timer["names"] = ()
     _timer["ev"] = {}
@@ -39,11 +39,12 @@ def timer_stop(detail=False):
     out = {}
     for n, v in ev.items():
         if not v:
-            out[n] = None if not detail else (None, 0, 0.0, None)
+            out[n] = None if not detail else (None, 0, 0.0, None, [])
             continue
-        tot = sum(a.elapsed_time(b) for a, b, _ in v)
+        each = [a.elapsed_time(b) for a, b, _ in v]
+        tot = sum(each)
         fl = sum(f for _, _, f in v) if all(f is not None for _, _, f in v) else None
-        out[n] = tot / len(v) if not detail else (tot / len(v), len(v), tot, fl)
+        out[n] = tot / len(v) if not detail else (tot / len(v), len(v), tot, fl, each)
     return out
 
 

@@ -66,6 +66,8 @@ class FusedAdam(torch.optim.Optimizer):
         self._step = 0
         self._step_t = None  # one shared CPU step tensor referenced by every trained param's state
         self._coef_dev = None  # graph capture (graph.py): coefficients read from this device buffer
+        self._pre = []  # ranges already updated for the coming step by overlap_with's per-bucket hook
+        self._pre_lp = None
 
     # ---------------------------------------------------------------- state <-> flat moments
     def _trained(self):
@@ -135,6 +137,51 @@ class FusedAdam(torch.optim.Optimizer):
             self._step_t = None
 
     # ---------------------------------------------------------------- update
+    def overlap_with(self, reducer):
+        """Data parallel: update each gradient bucket as soon as its all-reduce has been waited for, on
+        the step stream inside the backward (``GradAllReducer.on_bucket``), so the Adam of the first
+        buckets runs while the last buckets are still being exchanged; ``step()`` then updates only what no
+        bucket covered (nothing, when the buckets tile the gradient buffer) and does the bookkeeping.
+        Bitwise the whole-buffer update (Adam is elementwise).  The update of a step is applied when its
+        backward ends: every backward must be followed by ``step()`` with the gradients left as they are
+        (the reference trainer's loop, ``main.py:331-369``; reading them for logging is fine).  A step
+        captured as a HIP graph (``CapturedTrainStep``, its Adam coefficients on the device) keeps the
+        whole-buffer update: with the per-bucket updates captured between the RCCL waits, the process
+        group's watchdog failed on a captured event in 2 of 5 one-rank runs, never without them."""
+        reducer.on_bucket = self._bucket_update
+
+    def _coefs(self):
+        grp = self.param_groups[0]
+        if grp.get("amsgrad") or grp.get("maximize"):
+            raise NotImplementedError("FusedAdam: amsgrad / maximize are not used by the reference trainer")
+        b1, b2 = grp["betas"]
+        return grp["lr"], b1, b2, grp["eps"], grp["weight_decay"]
+
+    def _update(self, lo, hi, step, lp):
+        flat, n = self._ensure()
+        g = self.model.flat_grads()
+        lr, b1, b2, eps, wd = self._coefs()
+        K.adam_step(flat[lo:hi], g[lo:hi], self._m[lo:hi], self._v[lo:hi], lr, b1, b2, eps, wd, step,
+                    p_lp=lp[lo:hi] if lp is not None else None, coef_dev=self._coef_dev)
+
+    @torch.no_grad()
+    def _bucket_update(self, lo, hi):
+        n = self.model.trainable_numel()
+        hi = min(hi, n)
+        if lo >= hi or self._coef_dev is not None:  # being captured: step() updates the whole buffer
+            return
+        if any(lo < b and a < hi for a, b in self._pre):
+            raise RuntimeError("FusedAdam.overlap_with: a gradient range was updated twice before step(); every "
+                               "backward must be followed by optimizer.step()")
+        if not self._pre:  # the step's first bucket: the bf16 copy (refreshed first when stale), once
+            self._pre_lp = self._lowp()
+        self._update(lo, hi, self._step + 1, self._pre_lp)
+        self._pre.append((lo, hi))
+
+    def _lowp(self):
+        m = self.model
+        return m.lowp_weights()[:m.trainable_numel()] if m.compute_dtype == torch.bfloat16 else None
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -142,24 +189,25 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         model = self.model
-        grp = self.param_groups[0]
-        if grp.get("amsgrad") or grp.get("maximize"):
-            raise NotImplementedError("FusedAdam: amsgrad / maximize are not used by the reference trainer")
+        self._coefs()
         flat, n = self._ensure()
-        g = model.flat_grads()
         self._step += 1
         if self._step_t is None:
             self._step_t = torch.tensor(float(self._step))
             self._bind_state()
         else:
             self._step_t.fill_(float(self._step))
-        b1, b2 = grp["betas"]
-        lp = None
+        # the whole buffer, or (overlap_with) the ranges no bucket has updated yet; the bf16 operand copy
+        # is refreshed first when stale (e.g. after load_state_dict), by _lowp
+        done, self._pre = sorted(self._pre), []
+        lp = self._pre_lp if done else self._lowp()
+        self._pre_lp = None
+        lo = 0
+        for a, b in done + [(n, n)]:
+            if a > lo:
+                self._update(lo, a, self._step, lp)
+            lo = max(lo, b)
         if model.compute_dtype == torch.bfloat16:
-            lp = model.lowp_weights()[:n]  # refreshes a stale copy first (e.g. after load_state_dict)
-        K.adam_step(flat[:n], g[:n], self._m, self._v, grp["lr"], b1, b2, grp["eps"], grp["weight_decay"],
-                    self._step, p_lp=lp, coef_dev=self._coef_dev)
-        if lp is not None:
             model.mark_lowp_fresh()
         return loss
 

@@ -10,7 +10,9 @@
   tile ``[0, trainable_numel)`` exactly once, in reverse layout order;
 * the captured DP step (``CapturedTrainStep(capture_collectives=True)``: RCCL all-reduces captured into
   the HIP graph, tile cut active, backward writing the gradients) on a one-rank RCCL group gives bitwise
-  the parameters and Adam moments of eager DP steps;
+  the parameters and Adam moments of eager DP steps, with and without the per-bucket Adam
+  (``FusedAdam.overlap_with``: each bucket updated right after its wait), which is also bitwise the
+  whole-buffer update in eager DP steps, here and on two gloo ranks;
 * the DP update pinned to the oracle: two ranks through ``MultiGPUStrategy.setup`` / ``wrap_model`` /
   the HIP backward / ``FusedAdam`` against the CPU oracle's gradients of each rank's batch, averaged,
   then ``torch.optim.Adam`` (``/root/reference/main.py:331-369``, ``utils/distributed.py:415-428``).
@@ -118,6 +120,10 @@ def test_bench_two_ranks_gloo(dev, request, tmp_path):
     print({k: res[k] for k in ("value", "ms_per_step", "n_gpus", "ranks_seen", "param_checksums", "execution")})
     assert res["n_gpus"] == 2 and res["ranks_seen"] == 2
     assert res["config"]["parallelism"] == "dp2" and res["comm"]["backend"] == "gloo"
+    c = res["comm"]  # where the DP step's time goes (the driver's SCALE lines)
+    assert c["adam"] == "per bucket after its wait" and c["buckets_per_step"] >= 2
+    assert c["exposed_ms"] is not None and c["exposed_ms"] >= 0 and c["max_bucket_wait_ms"] >= 0
+    assert len(c["wgrad_launch_ms"]) >= 3 and all(t > 0 for t in c["wgrad_launch_ms"])
     assert res["execution"].startswith("eager")
     assert torch.isfinite(torch.tensor(res["loss"])).item()
     assert res["value"] > 0 and len(res["rank_ms_per_step"]) == 2
@@ -233,25 +239,41 @@ def _captured_worker(q, trace):
             oe.step()
             torch.cuda.synchronize()
             mark(f"eager DP step {i}")
-        mg, og, rg = fresh()
-        run = CapturedTrainStep(mg, og, {k: v.clone() for k, v in batches[0].items()}, warmup=1,
-                                capture_collectives=True)
-        torch.cuda.synchronize()
-        mark("captured")
-        for i, b in enumerate(batches):
-            run.load(b)
-            run.step()
-            torch.cuda.synchronize()
-            mark(f"replay {i}")
         n = me.trainable_numel()
-        ok = (run._graph is not None, len(rg.launched) > 0,
-              torch.equal(mg.flat_params()[:n], me.flat_params()[:n]),
-              torch.equal(og._m, oe._m), torch.equal(og._v, oe._v))
-        # the graph (and the RCCL plan resources it holds) goes before the communicator it was
-        # captured on is destroyed
-        del run
+        ok = []
+        for overlap in [c == "1" for c in os.environ.get("RP_TEST_CAPTURE_CASES", "01")]:
+            mg, og, rg = fresh()
+            if overlap:  # set, but a captured step keeps the whole-buffer Adam (FusedAdam.overlap_with)
+                og.overlap_with(rg)
+            run = CapturedTrainStep(mg, og, {k: v.clone() for k, v in batches[0].items()}, warmup=1,
+                                    capture_collectives=True)
+            torch.cuda.synchronize()
+            mark(f"captured (adam overlap {overlap})")
+            for i, b in enumerate(batches):
+                run.load(b)
+                run.step()
+                torch.cuda.synchronize()
+                mark(f"replay {i}")
+            ok.append((run._graph is not None, len(rg.launched) > 0,
+                       torch.equal(mg.flat_params()[:n], me.flat_params()[:n]),
+                       torch.equal(og._m, oe._m), torch.equal(og._v, oe._v)))
+            # the graph (and the RCCL plan resources it holds) goes before the communicator it was
+            # captured on is destroyed
+            del run
+            torch.cuda.synchronize()
+            mark("graph released")
+        # eager DP with the per-bucket Adam: bitwise the whole-buffer update
+        mo, oo, ro = fresh()
+        oo.overlap_with(ro)
+        for i, b in enumerate(batches):
+            oo.zero_grad()
+            (mo.losses(*mo(b))["cls_loss"] / 2).backward()
+            ro.wait()
+            oo.step()
         torch.cuda.synchronize()
-        mark("graph released")
+        ok.append((True, ro.on_bucket is not None, torch.equal(mo.flat_params()[:n], me.flat_params()[:n]),
+                   torch.equal(oo._m, oe._m), torch.equal(oo._v, oe._v)))
+        mark("eager overlap")
         q.put(("ok", ok))
     except Exception:
         import traceback
@@ -273,10 +295,11 @@ def test_captured_rccl_dp_step_equals_eager_dp(dev, tmp_path, request):
     p.start()
     status, res = _wait(q, p, request, "captured DP worker", 240, trace)
     assert status == "ok", res
-    captured, hooked, params, m1, m2 = res
-    assert captured, "the DP step was not captured"
-    assert hooked, "the captured backward issued no all-reduce"
-    assert params and m1 and m2, res
+    for name, (captured, hooked, params, m1, m2) in zip(("captured", "captured + per-bucket Adam",
+                                                          "eager per-bucket Adam"), res):
+        assert captured, f"{name}: the DP step was not captured"
+        assert hooked, f"{name}: the backward issued no all-reduce"
+        assert params and m1 and m2, (name, res)
 
 
 # ------------------------------------------------------------------- DP update pinned to the oracle
@@ -451,3 +474,59 @@ def test_dp_update_matches_oracle_adam(dev, tmp_path):
             assert (d <= 2 * DP_LR * (step + 1) * 1.001).all(), f"step {step} {n}: a parameter moved too far"
     print(f"worst averaged-gradient rel err {worst_g:.2e}, update (FusedAdam vs torch Adam) {worst_u:.2e}, "
           f"parameters vs oracle (determined elements) {worst_p:.2e}, zero-init tensors' updates {worst_z:.2e}")
+
+
+def _overlap_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        import torch.distributed as dist
+        from repurpose_amd.distributed import GradAllReducer
+        from repurpose_amd.MMCTransformer import MMCTransformer
+        from repurpose_amd.optim import FusedAdam
+        from tests.test_model_gpu import TRI, make_batch, to_dev
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+        dev = torch.device("cuda", 0)
+        cfg = dict(TRI, self_num_layers=16)
+        res = []
+        for overlap in (False, True):
+            torch.manual_seed(7)
+            m = MMCTransformer(**cfg, compute_dtype="bf16").to(dev).train()
+            m.DROPOUT = 0.0
+            o = FusedAdam(m, lr=1e-3, weight_decay=1e-4)
+            r = GradAllReducer(m, bucket_mb=4.0)
+            if overlap:
+                o.overlap_with(r)
+            for step in range(2):
+                b = to_dev(make_batch(cfg, 2, 128, [128, 70 + 30 * rank], seed=50 + 10 * rank + step), dev)
+                o.zero_grad()
+                (m.losses(*m(b))["cls_loss"] / 2).backward()
+                r.wait()
+                o.step()
+            torch.cuda.synchronize()
+            n = m.trainable_numel()
+            res.append((m.flat_params()[:n].cpu(), o._m.cpu(), o._v.cpu(), m.lowp_weights()[:n].cpu()))
+        q.put(("ok", tuple(bool(torch.equal(a, b)) for a, b in zip(*res))))
+    except Exception:
+        import traceback
+        q.put(("err", traceback.format_exc()))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_per_bucket_adam_bitwise_two_gloo_ranks(dev, request):
+    """FusedAdam.overlap_with on two gloo ranks (16 layers, 4 MB buckets: many per step): parameters, Adam
+    moments and the bf16 operand copy after two steps are bitwise those of the whole-buffer update."""
+    ctx = mp.get_context("spawn")
+    port = _port()
+    qs = [ctx.Queue() for _ in range(2)]
+    ps = [ctx.Process(target=_overlap_worker, args=(r, 2, port, qs[r])) for r in range(2)]
+    for p in ps:
+        p.start()
+    for r in range(2):
+        status, res = _wait(qs[r], ps[r], request, f"per-bucket Adam rank {r}", 240)
+        assert status == "ok", res
+        assert all(res), (r, res)
