@@ -276,7 +276,9 @@ def main():
     runner = None
     if use_graph:
         from repurpose_amd.graph import CapturedTrainStep
-        runner = CapturedTrainStep(model, opt, batch, warmup=1, seed=1000 + rank, capture_collectives=dp)
+        # two static input sets (graph.py): the fresh-batch loop writes the next batch into the free one
+        runner = CapturedTrainStep(model, opt, batch, warmup=1, seed=1000 + rank, capture_collectives=dp,
+                                   input_sets=1 if dp else 2)
         step = runner.step
     else:
         step = eager_step
@@ -510,47 +512,61 @@ def ragged_pool(B, T, n, seed):
 
 def fresh_batch_loop(runner, eager_step, batch, B, T, dev, rank, steps, world, dp, pool_n=3):
     """The trainer-shaped loop (main.py:302-313): every step a NEW batch goes host -> device (pinned
-    ragged rows: one H2D copy per modality on a copy stream, padded / converted by rp_pad_rows there,
-    overlapped with the previous step's replay), then CapturedTrainStep.load() copies it into the
-    graph's static inputs and the step replays.  Returns the loop's throughput beside the H2D volume."""
+    ragged rows on a copy stream, overlapped with the previous step: fp32 rows by DMA straight into
+    their padded places, fp16 / fp64 rows padded and converted by rp_pad_rows).  With a two-set captured
+    step (CapturedTrainStep(input_sets=2)) the batch is written straight into the static inputs the
+    next replay reads, so no copy is left between the replays; otherwise it is staged and copied in.
+    Returns the loop's throughput beside the H2D volume."""
     pool = ragged_pool(B, T, pool_n, 5000 + 97 * rank)
     copy = torch.cuda.Stream(device=dev)
     main = torch.cuda.current_stream(dev)
     h2d = sum(v.numel() * v.element_size() for v in pool[0].rows.values())
+    direct = runner is not None and len(runner.sets) > 1
+    done = [0]  # steps run so far
 
-    def stage(i):
+    def stage(j):  # global step j's batch
         with torch.cuda.stream(copy):
-            nb = pool[i % pool_n].to_device(dev)
+            if direct:
+                dst, used = runner.input_set(ahead=j - done[0])
+                if used is not None:
+                    copy.wait_event(used)  # the last step that read this set has finished
+                nb = pool[j % pool_n].to_device(dev, out=dst)
+            else:
+                nb = pool[j % pool_n].to_device(dev)
             ev = torch.cuda.Event()
             ev.record(copy)
         return nb, ev
 
-    def run(i, nxt):
+    def run(nxt):
         nb, ev = nxt
         main.wait_event(ev)
-        for v in nb.values():
-            if torch.is_tensor(v):
-                v.record_stream(main)
-        if runner is not None:
-            runner.load(nb)
+        if direct:
             runner.step()
         else:
-            for k, v in nb.items():
-                if torch.is_tensor(v) and k in batch:
-                    batch[k].copy_(v, non_blocking=True)
-            eager_step()
+            for v in nb.values():
+                if torch.is_tensor(v):
+                    v.record_stream(main)
+            if runner is not None:
+                runner.load(nb)
+                runner.step()
+            else:
+                for k, v in nb.items():
+                    if torch.is_tensor(v) and k in batch:
+                        batch[k].copy_(v, non_blocking=True)
+                eager_step()
+        done[0] += 1
 
     nxt = stage(0)
     for i in range(2):  # warm-up: pinned pool, pad kernels, allocator
         cur, nxt = nxt, stage(i + 1)
-        run(i, cur)
+        run(cur)
     torch.cuda.synchronize()
     if dp:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(steps):
         cur, nxt = nxt, stage(i + 3)
-        run(i, cur)
+        run(cur)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if dp:
@@ -559,8 +575,10 @@ def fresh_batch_loop(runner, eager_step, batch, B, T, dev, rank, steps, world, d
         el = float(t.item())
     return {"value": world * B * T * steps / el, "unit": "feature-timesteps/sec", "ms_per_step": el / steps * 1e3,
             "steps": steps, "h2d_bytes_per_step": h2d, "h2d_source": "pinned ragged rows (fp16 visual, fp32 audio, "
-            "fp64 text, labels, segments) -> rp_pad_rows on a copy stream, overlapped with the previous replay",
-            "pool": pool_n}
+            "fp64 text, labels, segments) on a copy stream, overlapped with the previous replay: fp32 rows by DMA "
+            "into their padded places, the others through rp_pad_rows",
+            "into": "the captured step's free static input set (no copy between replays)" if direct
+            else "staging tensors, copied into the step's inputs", "pool": pool_n}
 
 
 if __name__ == "__main__":

@@ -125,7 +125,7 @@ int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, in
  * whole K range in one workgroup — no split-K slabs, no workspace, deterministic.  Replaces the
  * per-layer weight-gradient launches of the encoder's backward (autograd of the nn.Linear layers of
  * models/MMCTransformer.py:41-55 under loss.backward(), main.py:365) when they are deferred to the
- * end of the backward.  At most 64 items per call (256 x 256 output tiles; RP_WGRAD8=0: 128 x 128);
+ * end of the backward.  At most 64 items per call (256 x 256 output tiles);
  * dY [K, ldy], X [K, ldx] bf16, dW fp32 [M, N]. */
 typedef struct {
   const void* dY;

@@ -432,20 +432,6 @@ def _sub_batch(batch, rows, tg):
     return out
 
 
-_SIDE = {}
-
-
-def _side_stream(device):
-    """Side stream for the weight-gradient GEMMs, opt-in (RP_SIDE_STREAM=1): measured 1.4 % slower
-    on MI355X at the bench shape (20.08 vs 19.80 ms), so the default keeps one stream."""
-    if os.environ.get("RP_SIDE_STREAM", "0") != "1":
-        return None
-    key = device.index if device.index is not None else torch.cuda.current_device()
-    if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=device)
-    return _SIDE[key]
-
-
 def _mix(base, site):
     x = (base * 0x9E3779B1 + site * 0x85EBCA77 + 0x165667B1) & 0xFFFFFFFF
     x ^= x >> 15
@@ -618,21 +604,16 @@ class _Schedule:
         wws = torch.empty(max(lib.rp_gemm_wgrad_workspace(a, b, M) for a, b in shapes) // 4 + 4,
                           device=dlogits.device, dtype=_F32)
         G = self.G
-        # Weight gradients (dW = dY^T X, split-K, + bias) depend on nothing downstream of the
-        # layer, so they run on a side stream beside the dgrad / attention-backward chain of the
-        # main stream: the latency-bound GEMMs fill the CUs that the VALU-bound attention backward
-        # and the dgrad GEMMs leave idle.  Flat-gradient ranges are announced to the all-reduce
-        # hooks one layer late, after the main stream has waited on that layer's side-stream event.
-        main = torch.cuda.current_stream(dlogits.device)
-        side = _side_stream(dlogits.device)
-        pending = []  # (event on the side stream, prefixes) not yet announced
+        # Weight gradients (dW = dY^T X + bias) run on the step's one stream (a side stream beside the
+        # dgrad chain measured 1.4 % slower, rounds 1-2); a layer's flat-gradient range is announced to
+        # the all-reduce hooks once its weight-gradient GEMMs are launched.
 
         # bf16 training: the encoder layers' weight gradients are deferred and computed by grouped
         # whole-K launches (all 16 layers x 4 GEMMs = 768 256x256 tiles, three per CU: no split-K
         # slabs and no reduce pass).  Under DP a layer's gradient range is announced to the all-reduce
         # hooks once all its GEMMs have been launched, so the first launch's exchange overlaps the
         # backward of the remaining layers.
-        deferred = [] if (dt == torch.bfloat16 and side is None and M % 64 == 0
+        deferred = [] if (dt == torch.bfloat16 and M % 64 == 0
                           and os.environ.get("RP_WGRAD_GROUPED", "1") != "0") else None
         held = []  # layer prefixes whose gradients wait for their group launch
         # one launch for the whole encoder on one GPU.  With gradient hooks (DP all-reduce) the launch is
@@ -676,16 +657,9 @@ class _Schedule:
                         cut["tiles"] = 0
                         flush_group()  # announces the layers already complete (held), not this one
                 return
-            if side is None:
-                K.linear_wgrad(dy, x, G(wname), db=G(bname), accumulate=acc, ws=wws)
-                return
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                K.linear_wgrad(dy, x, G(wname), db=G(bname), accumulate=acc, ws=wws)
-            dy.record_stream(side)
-            x.record_stream(side)
+            K.linear_wgrad(dy, x, G(wname), db=G(bname), accumulate=acc, ws=wws)
 
-        def ready(prefixes, flush=False):
+        def ready(prefixes):
             if deferred is not None and prefixes[0].startswith("multimodal_encoder."):
                 held.append(prefixes)
                 if not tile_cut and len(deferred) >= per_launch:
@@ -693,16 +667,7 @@ class _Schedule:
                 return
             if m._grad_ready_hooks:
                 flush_cs()
-            if side is None:
-                m._grads_ready(prefixes)
-                return
-            ev = torch.cuda.Event()
-            ev.record(side)
-            pending.append((ev, prefixes))
-            while pending and (flush or len(pending) > 1):
-                e, pf = pending.pop(0)
-                main.wait_event(e)
-                m._grads_ready(pf)
+            m._grads_ready(prefixes)
 
         dl = dlogits.reshape(M, 1).contiguous().float()
         # cls_head[7]  (N = 1)
@@ -790,10 +755,7 @@ class _Schedule:
         _, dproj = K.layernorm_bwd(dx, S["proj"], S["mu0"], S["rs0"], self.P("input_norm.weight"), want_f32=False,
                                    lp_dtype=dt, dgamma=G("input_norm.weight"), dbeta=G("input_norm.bias"), ws=ws, defer=cs)
         wgrad(dproj, S["xin"], "input_projection.weight", "input_projection.bias")
-        ready(["input_projection.", "input_norm."], flush=True)
-        if side is not None:
-            wws.record_stream(side)
-            main.wait_stream(side)
+        ready(["input_projection.", "input_norm."])
         flush_cs()
         for h in m._grad_done_hooks:
             h()

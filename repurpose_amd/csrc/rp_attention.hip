@@ -34,12 +34,6 @@ constexpr int NT = NW * 64;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float RESCALE_LOG2 = 8.f;  // forward: deferred-rescale threshold (log2 units)
 
-// RP_ATTN_SETPRIO: raise the wave priority around each MFMA cluster (cdna_hip_programming.md T5)
-#ifdef RP_ATTN_SETPRIO
-#define RP_PRIO(x) __builtin_amdgcn_s_setprio(x)
-#else
-#define RP_PRIO(x) ((void)0)
-#endif
 
 template <typename T>
 struct AttnCfg {
@@ -459,7 +453,6 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) s[kt][qt] = f32x4{-m[qt], -m[qt], -m[qt], -m[qt]};
     if constexpr (BF) {
-      RP_PRIO(1);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -468,7 +461,6 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 #pragma unroll
           for (int qt = 0; qt < QT; ++qt) s[kt][qt] = mfma_bf16(kf, qf[qt][ss], s[kt][qt]);
         }
-      RP_PRIO(0);
     } else {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
@@ -560,7 +552,6 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
             pf[qt][ks] = __builtin_bit_cast(bf16x8, u);
           }
         }
-      RP_PRIO(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -569,7 +560,6 @@ __global__ __launch_bounds__(NT, (std::is_same<T, bf16>::value && !DROP) ? 3 : 2
 #pragma unroll
           for (int qt = 0; qt < QT; ++qt) o[qt][dt] = mfma_bf16(vf, pf[qt][ks], o[qt][dt]);
         }
-      RP_PRIO(0);
     } else {
       if constexpr (DROP) {
 #pragma unroll
@@ -872,7 +862,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
       }
       if constexpr (BF) {
         // the row constants enter as the first MFMA's C operand (no register copies)
-        RP_PRIO(1);
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
 #pragma unroll
@@ -885,7 +874,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
               dp[qq][kt] = mfma_bf16(da, vf[kt][ss], ss == 0 ? ndq[qq] : dp[qq][kt]);
             }
           }
-        RP_PRIO(0);
       } else {
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
@@ -943,7 +931,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
           pa[kt] = pack8(s[0][kt], s[1][kt]);
           sa[kt] = pack8(dp[0][kt], dp[1][kt]);
         }
-        RP_PRIO(1);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
           const bf16x8 dob = col_frag_lds(dOl, hf * 32, dt * 16, lane);
@@ -954,7 +941,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_kv_kernel(MhaDev a) {
             dk[kt][dt] = mfma_bf16(sa[kt], qb, dk[kt][dt]);
           }
         }
-        RP_PRIO(0);
       } else {
 #pragma unroll
         for (int qq = 0; qq < 2; ++qq)
@@ -1344,7 +1330,6 @@ __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int 
         nl[qq] = *reinterpret_cast<const f32x4*>(lrow + r0);
         ndq[qq] = *reinterpret_cast<const f32x4*>(drow + r0);
       }
-      RP_PRIO(1);
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq)
 #pragma unroll
@@ -1357,7 +1342,6 @@ __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int 
             dp[qq][kt] = mfma_bf16(da, vf[kt][ss], ss == 0 ? ndq[qq] : dp[qq][kt]);
           }
         }
-      RP_PRIO(0);
     };
     auto prob = [&](int hf, f32x4 (&s)[2][KTW], f32x4 (&dp)[2][KTW], const f32x4 (&ndq)[2], bf16x8 (&pa)[KTW],
                     bf16x8 (&sa)[KTW]) {
@@ -1396,7 +1380,6 @@ __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int 
       }
     };
     auto dvdk = [&](int hf, const bf16x8 (&pa)[KTW], const bf16x8 (&sa)[KTW]) {
-      RP_PRIO(1);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x8 dob = col_frag_lds(dOl, hf * 32, dt * 16, lane);
@@ -1407,7 +1390,6 @@ __device__ __forceinline__ void attn_bwd_kv_dma_body(const MhaDev& a, const int 
           dk[kt][dt] = mfma_bf16(sa[kt], qb, dk[kt][dt]);
         }
       }
-      RP_PRIO(0);
     };
     if constexpr (PIPE) {
       // both halves' S / dP products are issued before the first half's VALU, so the VALU of half 0
@@ -1679,7 +1661,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
         s0[qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
         d0[qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
       }
-      RP_PRIO(1);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -1692,7 +1673,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
             dp[kt][qt] = mfma_bf16(va, df[qt][ss], ss == 0 ? d0[qt] : dp[kt][qt]);
           }
         }
-      RP_PRIO(0);
       if (!full) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
@@ -1749,7 +1729,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
     }
     // dQ[q][dk] += dS K : A = dS (q on row = lane i, key slots), B = K columns (tr read)
     if constexpr (BF) {
-      RP_PRIO(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8 sa[QT];
@@ -1762,7 +1741,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_q_kernel(MhaDev a) {
           for (int qt = 0; qt < QT; ++qt) dqa[qt][dt] = mfma_bf16(sa[qt], kb, dqa[qt][dt]);
         }
       }
-      RP_PRIO(0);
     } else {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
@@ -2027,7 +2005,6 @@ __device__ __forceinline__ void attn_bwd_q_dma_body(const MhaDev& a, const int b
         s0[qt] = f32x4{nlq[qt], nlq[qt], nlq[qt], nlq[qt]};
         d0[qt] = f32x4{dq[qt], dq[qt], dq[qt], dq[qt]};
       }
-      RP_PRIO(1);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -2040,7 +2017,6 @@ __device__ __forceinline__ void attn_bwd_q_dma_body(const MhaDev& a, const int b
             dp[kt][qt] = mfma_bf16(va, df[qt][ss], ss == 0 ? d0[qt] : dp[kt][qt]);
           }
         }
-      RP_PRIO(0);
     }
     if (!full) {  // key bias 0 / -inf from the staged valid bytes of keys kt*16 + 4g + r
 #pragma unroll
@@ -2068,7 +2044,6 @@ __device__ __forceinline__ void attn_bwd_q_dma_body(const MhaDev& a, const int b
             s[kt][qt][r] = p * dp[kt][qt][r];
           }
         }
-    RP_PRIO(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 sa[QT];
@@ -2081,7 +2056,6 @@ __device__ __forceinline__ void attn_bwd_q_dma_body(const MhaDev& a, const int b
         for (int qt = 0; qt < QT; ++qt) dqa[qt][dt] = mfma_bf16(sa[qt], kb, dqa[qt][dt]);
       }
     }
-    RP_PRIO(0);
   };
   const int nsteps = SPL == 1 ? nkt : nh0;
   for (int it = 0; it < nsteps; it += NBUF) {
@@ -2328,7 +2302,6 @@ __global__ __launch_bounds__(NT * SPL, SPL == 1 ? 3 : 1) void attn_fwd_dma_kerne
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) s[kt][qt] = f32x4{-m[qt], -m[qt], -m[qt], -m[qt]};
-    RP_PRIO(1);
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -2337,7 +2310,6 @@ __global__ __launch_bounds__(NT * SPL, SPL == 1 ? 3 : 1) void attn_fwd_dma_kerne
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) s[kt][qt] = mfma_bf16(kf, qf[qt][ss], s[kt][qt]);
       }
-    RP_PRIO(0);
     if (!full) {  // key bias 0 / -inf of keys kt*16 + 4g + r
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
@@ -2420,7 +2392,6 @@ __global__ __launch_bounds__(NT * SPL, SPL == 1 ? 3 : 1) void attn_fwd_dma_kerne
           pf[qt][ks] = __builtin_bit_cast(bf16x8, u);
         }
       }
-    RP_PRIO(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -2429,7 +2400,6 @@ __global__ __launch_bounds__(NT * SPL, SPL == 1 ? 3 : 1) void attn_fwd_dma_kerne
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) o[qt][dt] = mfma_bf16(vf, pf[qt][ks], o[qt][dt]);
       }
-    RP_PRIO(0);
   };
   const int nsteps = SPL == 1 ? nkt : nh0;
   for (int it = 0; it < nsteps; it += NBUF) {
@@ -2562,18 +2532,8 @@ static int64_t attn_cu_count() {
 
 // 128-row blocks (the LDS-DMA kernels) from one workgroup per CU up; 64-row blocks below.  At one per
 // CU the 128-row LDS-DMA kernel still beats the 64-row register-staged one at twice the workgroups
-// (config 4, B = 1, T = 4096: fwd 85 vs 96 us; dQ 78 vs 101; step 9.59 -> 9.06 ms).  RP_ATTN_BLOCK=64 |
-// 128 forces one (tuning; read once)
-static bool attn_small(int64_t big_grid) {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_ATTN_BLOCK");
-    v = e ? atoi(e) : 0;
-  }
-  if (v == 64) return true;
-  if (v == 128) return false;
-  return big_grid < attn_cu_count();
-}
+// (config 4, B = 1, T = 4096: fwd 85 vs 96 us; dQ 78 vs 101; step 9.59 -> 9.06 ms)
+static bool attn_small(int64_t big_grid) { return big_grid < attn_cu_count(); }
 
 // Split workgroups (SPL = 2: eight waves, the reduced sequence range in two halves, partials merged in
 // LDS) for grids of 128-row blocks that fill the CUs once but not twice (config 4: B = 1, T = 4096 is

@@ -39,14 +39,6 @@ int rp_check_launch(const char* what);
 
 static inline bool rp_aligned16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
 
-// Output store cache policy of a kernel family (rp_st16): the environment variable var (A/B) or
-// dflt.  0 plain, 1 sc1 write-through, 2 nt.  Callers cache the answer.
-static inline int rp_store_policy_env(const char* var, int dflt) {
-  const char* e = getenv(var);
-  const int v = e ? atoi(e) : dflt;
-  return (v < 0 || v > 2) ? dflt : v;
-}
-
 // ----------------------------------------------------------------------------------------------
 // dropout hash: lowbias32-style finaliser over (seed, index).  keep <=> (h & 0xffff) >= thresh16
 // thresh16 = round(p * 65536); kept values are scaled by 1/(1-p).

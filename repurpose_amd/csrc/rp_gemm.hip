@@ -575,11 +575,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(int64_t M, int64_t N, int64
 // co-resident workgroups hide each other's load latency (qkv fwd 43.1 -> 41.3 us, linear1 fwd
 // 54.3 -> 50.5, K = 512 dgrad into d_ff 64.3 -> 52.8), deeper K on CFG 0 (linear2 fwd 39.5 vs 43.0);
 // CFG 2 lost to CFG 1 everywhere and serves only K % 64 == 32.  In the whole training step, though,
-// CFG 1 on the K = 512, N >= 1536 shapes (RP_GEMM_POLICY=1) measured 20.30 vs 20.15 ms per step in
-// round 1 (eager step, per-kernel events inside the timed region); in the graph-replayed step of
-// round 2 it measures 16.03 vs 16.21 ms (three interleaved pairs, one box), so it is the default
-// now (RP_GEMM_POLICY=0 restores CFG 0).  CFG 1 on every short-K shape (N = 512 too) measured the
-// same as on the wide ones only; CFG 1 everywhere (RP_GEMM_CFG=1) 16.52 ms.
+// CFG 1 on the K = 512, N >= 1536 shapes measured 20.30 vs 20.15 ms per step in round 1 (eager step,
+// per-kernel events inside the timed region); in the graph-replayed step of round 2 it measures 16.03
+// vs 16.21 ms (three interleaved pairs, one box), so it is the default (rp_gemm_cfg).  CFG 1 on every
+// short-K shape (N = 512 too) measured the same as on the wide ones only; CFG 1 everywhere 16.52 ms.
 // Rows past M/N are clamped to the last valid row (their outputs are discarded), so the path needs
 // whole BK-deep K steps.
 typedef __attribute__((address_space(3))) void lds_void;
@@ -797,11 +796,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
 // One launch computes up to WG_MAX weight gradients dW_i = dY_i^T X_i (+ db_i = colsum dY_i) that
 // share the token count K, every output tile over the WHOLE K range (no split-K slabs, no reduce
 // pass).  The deferred per-layer weight gradients of the encoder (16 layers x {linear2, linear1,
-// out_proj, in_proj}) are the intended use: by default on 256 x 256 tiles (wgrad8_grouped_kernel
-// below, 48 tiles per layer, all 16 layers = 768 tiles = three per CU), here on 128 x 128 tiles
-// (RP_WGRAD8=0: 192 tiles per layer, 8 layers = 1536 tiles = three waves at two workgroups per CU);
-// the XCD remap deals each XCD consecutive tiles, i.e. whole layers, whose operand panels its L2
-// then shares.
+// out_proj, in_proj}) are the intended use, on 256 x 256 tiles (wgrad8_grouped_kernel below, 48
+// tiles per layer, all 16 layers = 768 tiles = three per CU; the 128 x 128 form of rounds 2-4 ran
+// ~0.3 ms slower per step and was removed in round 6); the XCD remap deals each XCD consecutive tiles,
+// i.e. whole layers, whose operand panels its L2 then shares.
 constexpr int WG_MAX = 64;
 struct WgItem {
   const bf16* dY;
@@ -812,57 +810,12 @@ struct WgItem {
 };
 struct WgGroup {
   int n, accumulate, tiles_total;
-  int order;  // tile order (A/B): 0 XCD chunks, m-major; 1 XCD chunks, n-major; 2 no XCD remap
+  int order;  // tile order: 0 XCD chunks, m-major (orders 1 n-major / 2 no remap measured alike)
   int st_pol;  // output store cache policy (rp_st16)
   int64_t K;
   int start[WG_MAX + 1];
   WgItem it[WG_MAX];
 };
-
-__global__ __launch_bounds__(NT, 2) void wgrad_grouped_kernel(const WgGroup g) {
-  using D = DmaCfg<0>;
-  __shared__ __attribute__((aligned(16))) char lds[D::LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
-  const int t = rp_xcd_remap(blockIdx.x, g.tiles_total);
-  int k = 0;
-  while (k + 1 < g.n && t >= g.start[k + 1]) ++k;
-  const WgItem w = g.it[k];
-  const int local = t - g.start[k];
-  const int tiles_n = (w.N + BN - 1) / BN;
-  const int64_t m0 = (int64_t)(local / tiles_n) * BM;
-  const int64_t n0 = (int64_t)(local % tiles_n) * BN;
-  const bool want_bias = w.db != nullptr && n0 == 0;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bacc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
-  dma_mainloop<false, false, 0>(w.dY, w.ldy, w.M, w.X, w.ldx, w.N, m0, n0, 0, g.K, want_bias, acc, bacc, lds, tid,
-                                lane, wid, wm, wn);
-  EpiDev ep{};
-  ep.gate_scale = 1.f;
-  ep.accumulate = g.accumulate;
-  ep.st_pol = g.st_pol;
-  gemm_epilogue<float, 0, D::HALVES>(acc, lds, tid, lane, wm, wn, m0, n0, w.M, w.N, w.dW, w.N, 1.f, ep, 0);
-  if (want_bias) {  // the tile's rows' whole-K column sums: the bias gradient itself
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(lds);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bacc[j];
-    __syncthreads();
-    if (tid < BM && m0 + tid < w.M) {
-      const int c = tid / 8, e = tid % 8;
-      float sum = 0.f;
-      for (int j = 0; j < NT / (BM / 8); ++j) sum += red[(c + (BM / 8) * j) * 8 + e];
-      w.db[m0 + tid] = g.accumulate ? w.db[m0 + tid] + sum : sum;
-    }
-  }
-}
 
 // ====================== 256-row tiles: 8 waves, whole-K-tile LDS-DMA ring =======================
 // One workgroup of 512 threads (8 waves as 2 (M) x 4 (N)) owns a 256 x BNT output tile (BNT = 256
@@ -1312,143 +1265,6 @@ __device__ __forceinline__ void gemm8_tile(int64_t M, int64_t N, const bf16* __r
   }
 }
 
-// One 256 x 128 output tile (BNT = 128: the d_model = 512 outputs, 256 tiles at M = 16384 — one per
-// CU — where 256 x 256 tiles would leave half the CUs idle), eight waves: wm = wid >> 2 the 128-row
-// half, wn = wid & 3 the 32-column quarter (acc[8][2] per wave).  A K-tile (64 deep) is TWO phases
-// of 16 MFMAs: phase 0 reads A rows 0-63 of the wave's half and the wave's 32 B columns, phase 1 A
-// rows 64-127 (the B fragments stay in registers); each phase is a read segment and an MFMA segment
-// closed by raw s_barriers, waves 4-7 one barrier behind waves 0-3 (the two waves of a SIMD alternate
-// reading and multiplying).  Two LDS slots (A 2 x 16 KiB + B 16 KiB each), K-tile t in slot t & 1.
-// Barrier events of K-tile t on the leading half's clock: 4t+1 after R0, 4t+2 after M0, 4t+3 after
-// R1, 4t+4 after M1; the lagging half's R0 / M0 / R1 / M1 end at 4t+2 .. 4t+5.  So the B image of
-// K-tile t is last read before event 4t+2 and its A images before 4t+4: B(t+2) is issued in R1(t)
-// (after 4t+2 on both halves), A(t+1) in M0(t) (after 4t+1 > 4t+0, when slot (t+1) & 1's A images
-// of K-tile t-1 died), and every piece of K-tile t+1 must have landed by event 4t+4, the first
-// barrier before any wave reads it: the leading half waits before its fourth barrier of K-tile t,
-// the lagging half before its third (both event 4t+4), vmcnt(2) leaving only B(t+2) in flight.
-// Same MFMA order per output element as the 128 x 128 kernel (K-tiles ascending, 32-deep halves).
-// The main loop of the 256 x 128 phased tile (eight waves of 128 x 32: wm = wid >> 2 the row half, wn the
-// 32-column quarter), acc[i][j] = C[m0 + 128 wm + 16 i + 4 g + r][n0 + 32 wn + 16 j + c]; returns after the
-// last barrier (the caller synchronises before reusing the LDS)
-template <bool AK, bool BKM>
-__device__ __forceinline__ void g8_128_mainloop(int64_t M, int64_t N, const bf16* __restrict__ A, int64_t lda,
-                                                const bf16* __restrict__ B, int64_t ldb, int64_t kbeg, int64_t kend,
-                                                int64_t m0, int64_t n0, f32x4 (&acc)[8][2], char* lds) {
-  using G = G8<128, 64, 2>;
-  static_assert(G::NBH == 1 && G::JT == 2, "256 x 128 tile");
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int bcol = wn * 32;
-  const int nk = kend > kbeg ? (int)((kend - kbeg) / 64) : 0;
-  auto fill_a = [&](int kt) {
-    char* buf = lds + (kt & 1) * G::SLOT;
-    const int64_t k0 = kbeg + (int64_t)kt * 64;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        glds_piece8<AK, 64>(A, lda, M, m0 + 128 * h, k0, buf + h * G::HB, wid * 2 + j, lane);
-  };
-  auto fill_b = [&](int kt) {
-    char* buf = lds + (kt & 1) * G::SLOT;
-    const int64_t k0 = kbeg + (int64_t)kt * 64;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) glds_piece8<BKM, 64>(B, ldb, N, n0, k0, buf + 2 * G::HB, wid * 2 + j, lane);
-  };
-  auto ra = [&](const char* img, int i, int kk) -> bf16x8 {
-    return AK ? frag_k_swz<64>(img, i * 16, kk, lane) : frag_m_swz(img, i * 16, kk, lane);
-  };
-  auto rb = [&](const char* img, int j, int kk) -> bf16x8 {
-    return BKM ? frag_k_swz<64>(img, bcol + j * 16, kk, lane) : frag_m_swz(img, bcol + j * 16, kk, lane);
-  };
-  if (nk > 0) {
-    fill_a(0);
-    fill_b(0);
-    if (nk > 1) {
-      fill_b(1);
-      rp_waitcnt<2, 15>();  // A(0), B(0) landed; B(1) may stay in flight
-    } else {
-      rp_waitcnt<0, 15>();
-    }
-  }
-  rp_raw_barrier();
-  if (wm == 1) rp_raw_barrier();  // the second wave of each SIMD runs one barrier behind
-
-  bf16x8 fa[4][2], fb[2][2];
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = lds + (kt & 1) * G::SLOT;
-    const char* ai = cur + wm * G::HB;
-    const char* bi = cur + 2 * G::HB;
-    // ---- phase 0: A rows 0-63 and the B columns ----
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = ra(ai, i, kk * 32);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fb[j][kk] = rb(bi, j, kk * 32);
-    rp_raw_barrier();
-    if (kt + 1 < nk) fill_a(kt + 1);  // slot (kt+1)&1's A images (K-tile kt-1) died at event 4kt
-    rp_lgkm0();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    rp_raw_barrier();
-    // ---- phase 1: A rows 64-127; the B pieces of K-tile kt+2 (this slot's B image died at 4kt+2) ----
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = ra(ai, 4 + i, kk * 32);
-    if (kt + 2 < nk) fill_b(kt + 2);
-    auto wait_next = [&]() {
-      if (kt + 2 < nk)
-        rp_waitcnt<2, 15>();  // only B(kt+2) may stay in flight
-      else
-        rp_waitcnt<0, 15>();
-    };
-    if (wm == 1) wait_next();  // the lagging half's third barrier of K-tile kt is event 4kt+4
-    rp_raw_barrier();
-    rp_lgkm0();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], fb[j][kk], acc[4 + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (wm == 0) wait_next();  // the leading half's fourth barrier of K-tile kt is event 4kt+4
-    rp_raw_barrier();
-  }
-  if (wm == 0) rp_raw_barrier();  // match the lagging half's barrier count
-}
-
-template <bool AK, bool BKM, typename TC, int MODE>
-__device__ __forceinline__ void gemm8_tile128(int64_t M, int64_t N, const bf16* __restrict__ A, int64_t lda,
-                                              const bf16* __restrict__ B, int64_t ldb, TC* __restrict__ Cout,
-                                              int64_t ldc, float alpha, const EpiDev& ep, int64_t kbeg, int64_t kend,
-                                              int64_t m0, int64_t n0, int split, char* lds) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
-  f32x4 acc[8][2];
-  g8_128_mainloop<AK, BKM>(M, N, A, lda, B, ldb, kbeg, kend, m0, n0, acc, lds);
-  __syncthreads();
-  gemm8_epilogue<TC, MODE, 128>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep, split);
-}
-
 template <bool AK, bool BKM, typename TC, int MODE, int BNT, bool GATEB = false>
 __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int64_t K, const bf16* __restrict__ A,
                                                        int64_t lda, const bf16* __restrict__ B, int64_t ldb,
@@ -1466,17 +1282,12 @@ __global__ __launch_bounds__(NT8, 2) void gemm8_kernel(int64_t M, int64_t N, int
     kbeg = (int64_t)split * kchunk;
     kend = kbeg + kchunk < K ? kbeg + kchunk : K;
   }
-  if constexpr (BNT == 128) {
-    static_assert(MODE == 0 && !GATEB, "256 x 128 tiles: plain / fused-epilogue forward and dgrad");
-    gemm8_tile128<AK, BKM, TC, MODE>(M, N, A, lda, B, ldb, Cout, ldc, alpha, ep, kbeg, kend, m0, n0, split, lds);
-  } else {
-    float* bias_dst = (MODE == 1 && bslab != nullptr && n0 == 0) ? bslab + (int64_t)split * M : nullptr;
-    gemm8_tile<AK, BKM, TC, MODE, BNT, GATEB>(M, N, A, lda, B, ldb, Cout, ldc, alpha, ep, kbeg, kend, m0, n0, split,
-                                              bias_dst, 0, lds);
-  }
+  float* bias_dst = (MODE == 1 && bslab != nullptr && n0 == 0) ? bslab + (int64_t)split * M : nullptr;
+  gemm8_tile<AK, BKM, TC, MODE, BNT, GATEB>(M, N, A, lda, B, ldb, Cout, ldc, alpha, ep, kbeg, kend, m0, n0, split,
+                                            bias_dst, 0, lds);
 }
 
-// grouped weight gradients on 256 x 256 tiles (the WgGroup of wgrad_grouped_kernel, whole K): twice
+// grouped weight gradients on 256 x 256 tiles (a WgGroup, every tile over the whole K): twice
 // the MFMA work per staged operand byte of the 128 x 128 tile, which the whole-K L2 -> LDS stream of
 // the grouped launch is bound by; one workgroup of 8 waves per CU
 __global__ __launch_bounds__(NT8, 1) void wgrad8_grouped_kernel(const WgGroup g) {
@@ -1522,12 +1333,6 @@ static int rp_gemm8_mode() {
 }
 static int rp_gemm8_bn(int64_t M, int64_t N, int64_t kext) {
   if (kext % 64 != 0 || kext < 128 || M < 256 || N % 8 != 0) return 0;
-  // RP_GEMM8_128=1 (opt-in): the 256 x 128 phased tile for the d_model = 512 outputs over K >= 1024
-  // (linear2 forward, linear1 and QKV dgrad).  Warm and plain it beats the 128 x 128 kernel by 7-10 %
-  // (scripts/gemm_vs_blas.py), cold with the fused epilogues it loses on the dgrad shapes, and the step
-  // moved 15.16 -> 15.14 ms (three interleaved pairs): off by default.  Read per call.
-  const char* e128 = getenv("RP_GEMM8_128");
-  if (e128 && e128[0] == '1' && N <= 512 && kext >= 1024) return 128;
   const int mode = rp_gemm8_mode();
   if (mode == 0) return 0;
   if (mode == 1) return 256;
@@ -1576,65 +1381,23 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, int S, int6
   hipLaunchKernelGGL((gemm_kernel<T, AKV, BKV, TC, MODEV>), GRID, dim3(NT), 0, s, M, N, K, a, lda, b, ldb, c, \
                      ldc, alpha, ep, kchunk, bslab)
 
-// DMA kernel configuration for a K extent (per split): RP_GEMM_CFG=0|1|2 forces one, for tuning.
-// Configuration 1 only where the 128 x 128 grid exceeds two workgroups per CU: at fewer (config 4,
-// M = 4096: the QKV forward's 384 and the d_ff = 2048 shapes' 512 tiles) configuration 0 — which also
-// opens the 64-row tiles to the QKV forward — measured 7.08 / 7.07 -> 6.93 / 6.97 ms per step.
+// DMA kernel configuration for a K extent (per split): 2 for K % 64 == 32; configuration 1 (one stage,
+// four workgroups per CU) for short-K wide shapes where the 128 x 128 grid exceeds two workgroups per CU
+// (the metric shape's QKV forward: 15.46 -> 15.66 ms per step with configuration 0 everywhere); at fewer
+// (config 4, M = 4096: the QKV forward's 384 and the d_ff = 2048 shapes' 512 tiles) configuration 0 —
+// which also opens the 64-row tiles to the QKV forward — measured 7.08 / 7.07 -> 6.93 / 6.97 ms per step.
 static int rp_gemm_cfg(int64_t kext, int64_t n, int64_t m) {
-  static int forced = -2, policy = 0;
-  if (forced == -2) {
-    const char* e = getenv("RP_GEMM_CFG");
-    forced = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
-    const char* pe = getenv("RP_GEMM_POLICY");
-    policy = pe ? atoi(pe) : 1;
-  }
-  if (forced >= 0) return (forced == 2 || kext % 64 == 0) ? forced : 2;
   if (kext % 64 != 0) return 2;
   const int64_t tiles = ((m + BM - 1) / BM) * ((n + BN - 1) / BN);
-  return (kext <= 1024 && n >= 1536 && policy == 1 && tiles > 2 * gemm_cu_count()) ? 1 : 0;
+  return (kext <= 1024 && n >= 1536 && tiles > 2 * gemm_cu_count()) ? 1 : 0;
 }
 
-// RP_WGRAD8=0: the grouped weight gradients on 128 x 128 tiles instead of 256 x 256 (A/B tuning)
-static bool rp_wgrad8_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_WGRAD8");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v != 0;
-}
 
-// RP_GEMM_PF=0 disables the gate-line prefetch of the 256-row kernel (A/B tuning)
-static int rp_gemm_prefetch_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_GEMM_PF");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v;
-}
-
-// RP_STORE_POLICY (A/B): the GEMM epilogues' output stores plain (0), write-through sc1 (1) or nt (2,
-// the default: 15.47 -> 15.08 ms per step)
-static int rp_store_policy() {
-  static const int v = rp_store_policy_env("RP_STORE_POLICY", 2);
-  return v;
-}
-// RP_LOAD_POLICY_RES (A/B): the epilogues' fp32 residual loads plain (0) or nt (2, the default: -0.09 ms
-// per step, three interleaved pairs; the residual stream is next read in the backward)
-static int rp_residual_load_policy() {
-  static const int v = rp_store_policy_env("RP_LOAD_POLICY_RES", 2);
-  return v;
-}
-
-static bool rp_dma_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RP_GEMM_DMA");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v != 0;
-}
+// the GEMM epilogues' output stores non-temporal (policy 2; plain 15.47, sc1 write-through 15.26 vs nt
+// 15.08 ms per step), their fp32 residual loads too (-0.09 ms per step: the residual
+// stream is next read in the backward)
+static int rp_store_policy() { return 2; }
+static int rp_residual_load_policy() { return 2; }
 
 template <typename TC>
 int launch_gemm8(int bn, int64_t M, int64_t N, int64_t K, const bf16* a, int64_t lda, int ak, const bf16* b,
@@ -1645,20 +1408,6 @@ int launch_gemm8(int bn, int64_t M, int64_t N, int64_t K, const bf16* a, int64_t
   hipLaunchKernelGGL((gemm8_kernel<AKV, BKV, TC, MODEV, 256>), GRID, dim3(NT8), 0, s, M, N, K, a, lda, b, ldb, c, \
                      ldc, alpha, ep, kchunk, bslab)
 #define RP_G8_LAUNCH(AKV, BKV, MODEV, GRID) RP_G8_LAUNCH1(AKV, BKV, MODEV, 256, GRID)
-  if (bn == 128) {  // 256 x 128 tiles (MODE 0 only)
-    const dim3 grid((unsigned)(((M + 255) / 256) * ((N + 127) / 128)));
-    if (ak && bk)
-      hipLaunchKernelGGL((gemm8_kernel<true, true, TC, 0, 128>), grid, dim3(NT8), 0, s, M, N, K, a, lda, b, ldb, c, ldc,
-                         alpha, ep, kchunk, bslab);
-    else if (ak && !bk)
-      hipLaunchKernelGGL((gemm8_kernel<true, false, TC, 0, 128>), grid, dim3(NT8), 0, s, M, N, K, a, lda, b, ldb, c,
-                         ldc, alpha, ep, kchunk, bslab);
-    else {
-      rp_set_error("rp_gemm: 256 x 128 tiles need a k-major A");
-      return RP_ERR_ARG;
-    }
-    return rp_check_launch("rp_gemm");
-  }
   if constexpr (!std::is_same<TC, float>::value) {
     if (splits == 0 && ak && !bk && ep.gate && ep.gate_bf16) {  // the linear2 dgrad: see GATEB
       hipLaunchKernelGGL((gemm8_kernel<true, false, TC, 0, 256, true>), dim3((unsigned)tiles), dim3(NT8), 0, s, M, N, K,
@@ -1719,11 +1468,11 @@ int launch_gemm_t(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, i
   TC* c = (TC*)Cp;
   if constexpr (std::is_same<T, bf16>::value) {
     const int bn8 = splits == 0 ? rp_gemm8_bn(M, N, K) : 0;
-    if (bn8 > 0 && rp_dma_enabled())
+    if (bn8 > 0)
       return launch_gemm8<TC>(bn8, M, N, K, (const bf16*)A, lda, ak, (const bf16*)B, ldb, bk, c, ldc, alpha, ep, s,
                               splits, kchunk, bslab);
     const bool full_k = K % 32 == 0 && (splits == 0 || kchunk % 32 == 0);
-    if (full_k && rp_dma_enabled()) {
+    if (full_k) {
       const int cfg = rp_gemm_cfg(splits == 0 ? K : kchunk, N, M);
       const bf16* ab = (const bf16*)A;
       const bf16* bb = (const bf16*)B;
@@ -1860,12 +1609,7 @@ void wgrad_plan(int64_t M, int64_t N, int64_t K, int bk, int& splits, int64_t& k
     return;
   }
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  static int target = -1;  // workgroups to aim at (RP_WGRAD_BLOCKS overrides, for tuning)
-  if (target < 0) {
-    const char* e = getenv("RP_WGRAD_BLOCKS");
-    target = e ? atoi(e) : 512;
-    if (target < 1) target = 512;
-  }
+  const int64_t target = 512;  // workgroups to aim at (256 / 384 / 768 / 1024 measured slower)
   int64_t sp = target / (tiles > 0 ? tiles : 1);
   const int64_t maxsp = K / (8 * bk);
   if (sp > maxsp) sp = maxsp;
@@ -1875,8 +1619,7 @@ void wgrad_plan(int64_t M, int64_t N, int64_t K, int bk, int& splits, int64_t& k
   if (splits < 1) splits = 1;
 }
 
-// the 256 x 256 phased kernel's wgrad plan (only under RP_GEMM8=1): ~one workgroup per CU
-// (RP_WGRAD8_BLOCKS overrides), splits of whole 64-deep K-tiles, at least 8 per split; returns 0
+// the 256 x 256 phased kernel's wgrad plan (only under RP_GEMM8=1): ~one workgroup per CU, splits of whole 64-deep K-tiles, at least 8 per split; returns 0
 // when the 128 x 128 kernel runs.  Measured (scripts/gemm_ab.py, M = 16384, split-major mapping on
 // both): 46.0 / 31.2 / 53.2 / 53.4 / 67.3 us for the qkv / out_proj / linear1 / linear2 / input
 // projection weight gradients against 40.9 / 23.9 / 49.2 / 47.5 / 68.1 us on the 128 x 128 kernel
@@ -1886,12 +1629,7 @@ int wgrad8_plan(int64_t M, int64_t N, int64_t K, int& splits, int64_t& kchunk) {
   const int mode = rp_gemm8_mode();
   if (mode != 1 || K % 64 != 0 || K < 512 || M < 256) return 0;
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  static int target = -1;
-  if (target < 0) {
-    const char* e = getenv("RP_WGRAD8_BLOCKS");
-    target = e ? atoi(e) : 256;
-    if (target < 1) target = 256;
-  }
+  const int64_t target = 256;
   int64_t sp = target / tiles;
   const int64_t maxsp = K / (8 * 64);
   if (sp > maxsp) sp = maxsp;
@@ -2434,11 +2172,9 @@ __device__ __forceinline__ void lx_mainloop(const bf16* __restrict__ A, int64_t 
   }
 }
 
-// RP_LNX_PF=0 (A/B): the exchange kernels on dma_mainloop, their epilogue operand loaded after it
-static int lnx_prefetch() {
-  static const int v = (getenv("RP_LNX_PF") && getenv("RP_LNX_PF")[0] == '0') ? 0 : 1;
-  return v;
-}
+// the exchange kernels' epilogue operand prefetched over the untracked main loop (lx_mainloop; the
+// dma_mainloop form with the operand loaded after it measured 14.51 vs 14.46 ms per step)
+static int lnx_prefetch() { return 1; }
 
 // Forward epilogue of a staged TR x 128 accumulator tile cs (r: the thread's residual chunks)
 template <int TR, int TNT>
@@ -2821,7 +2557,7 @@ extern "C" int rp_gemm(int dtype, int64_t M, int64_t N, int64_t K, const void* A
     e.accumulate = ep->accumulate;
     e.col_scale_n = ep->col_scale_n;
     e.col_scale = ep->col_scale;
-    e.prefetch_gate = rp_gemm_prefetch_enabled();
+    e.prefetch_gate = 1;
     RP_REQUIRE(ep->dropout_p >= 0.f && ep->dropout_p < 1.f, "rp_gemm: dropout_p must be in [0, 1)");
     RP_REQUIRE(e.col_scale_n >= 0 && e.col_scale_n % 8 == 0, "rp_gemm: col_scale_n must be a multiple of 8");
     RP_REQUIRE(!e.accumulate || c_dtype == RP_F32, "rp_gemm: accumulate needs an fp32 C");
@@ -2848,11 +2584,9 @@ extern "C" int rp_gemm_wgrad_grouped(int64_t K, const rp_wgrad_item* items, int 
   g.n = n_items;
   g.accumulate = accumulate;
   g.K = K;
-  const char* oe = getenv("RP_WGRAD_ORDER");  // A/B (read per call)
-  g.order = oe ? atoi(oe) : 0;
+  g.order = 0;  // the XCD remap of consecutive tiles (orders 1 / 2 measured alike, profiles/r05_wgrad_order_probe.txt)
   g.st_pol = rp_store_policy();
   int64_t tiles = 0;
-  const bool big = rp_wgrad8_enabled();  // 256 x 256 tiles (wgrad8_grouped_kernel)
   for (int i = 0; i < n_items; ++i) {
     const rp_wgrad_item& it = items[i];
     RP_REQUIRE(it.M > 0 && it.N > 0 && it.M % 8 == 0 && it.N % 8 == 0 && it.ldy % 8 == 0 && it.ldx % 8 == 0 &&
@@ -2865,15 +2599,12 @@ extern "C" int rp_gemm_wgrad_grouped(int64_t K, const rp_wgrad_item* items, int 
     g.start[i] = (int)tiles;
     g.it[i] = WgItem{(const bf16*)it.dY, (const bf16*)it.X, it.dW, it.db, (int)it.M, (int)it.N, (int)it.ldy,
                      (int)it.ldx};
-    tiles += big ? ((it.M + 255) / 256) * ((it.N + 255) / 256) : ((it.M + BM - 1) / BM) * ((it.N + BN - 1) / BN);
+    tiles += ((it.M + 255) / 256) * ((it.N + 255) / 256);
   }
   RP_REQUIRE(tiles < (1 << 30), "rp_gemm_wgrad_grouped: too many tiles");
   g.start[n_items] = (int)tiles;
   g.tiles_total = (int)tiles;
-  if (big)
-    hipLaunchKernelGGL(wgrad8_grouped_kernel, dim3((unsigned)tiles), dim3(NT8), 0, (hipStream_t)stream, g);
-  else
-    hipLaunchKernelGGL(wgrad_grouped_kernel, dim3((unsigned)tiles), dim3(NT), 0, (hipStream_t)stream, g);
+  hipLaunchKernelGGL(wgrad8_grouped_kernel, dim3((unsigned)tiles), dim3(NT8), 0, (hipStream_t)stream, g);
   return rp_check_launch("rp_gemm_wgrad_grouped");
 }
 
@@ -2951,7 +2682,7 @@ extern "C" int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const v
   const int bk = dtype == RP_BF16 ? GemmCfg<bf16>::BK : GemmCfg<float>::BK;
   int splits;
   int64_t kchunk;
-  const int bn8 = (dtype == RP_BF16 && rp_dma_enabled()) ? wgrad8_plan(M, N, K, splits, kchunk) : 0;
+  const int bn8 = dtype == RP_BF16 ? wgrad8_plan(M, N, K, splits, kchunk) : 0;
   if (!bn8) wgrad_plan(M, N, K, bk, splits, kchunk);
   RP_REQUIRE(ws_bytes >= (int64_t)splits * (M * N + M) * 4, "rp_gemm_wgrad: workspace too small");
   float* slab = (float*)workspace;
@@ -2961,8 +2692,7 @@ extern "C" int rp_gemm_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const v
   e.gate_scale = 1.f;
   e.st_pol = rp_store_policy();
   e.ld_pol = rp_residual_load_policy();
-  const char* sm = getenv("RP_WGRAD_SPLIT_MAJOR");  // read per call (A/B scripts); default on
-  e.split_major = !(sm && sm[0] == '0');
+  e.split_major = 1;
   int rc;
   if (bn8)
     rc = launch_gemm8<float>(bn8, M, N, K, (const bf16*)dY, ldy, 0, (const bf16*)X, ldx, 0, slab, N, 1.f, e, s, splits,

@@ -96,6 +96,22 @@ def collate_fn_test(batch):
 
 
 # ----------------------------------------------------------------------------- device path
+def _dma_rows(src, offs, dst, padding_val):
+    """fp32 pinned rows [sum len, D] -> padded dst [B, T, D] by DMA (current stream): one copy when every
+    sequence fills T (the rows are then dst's layout), else one per sequence and a fill of its padding."""
+    B, T, _ = dst.shape
+    lens = np.diff(offs)
+    if np.all(lens == T):
+        dst.view(-1, dst.shape[2]).copy_(src[:B * T], non_blocking=True)
+        return
+    for b in range(B):
+        n = int(lens[b])
+        if n:
+            dst[b, :n].copy_(src[int(offs[b]):int(offs[b]) + n], non_blocking=True)
+        if n < T:
+            dst[b, n:].fill_(padding_val)
+
+
 @dataclass
 class RaggedBatch:
     """One modality per entry: rows of all videos concatenated + prefix offsets (int64 [B+1])."""
@@ -114,9 +130,13 @@ class RaggedBatch:
                 for k, v in self.offsets.items()}
         return RaggedBatch(self.video_id, self.duration, rows, offs, dict(self.extra))
 
-    def to_device(self, device, padding_val=0.0):
+    def to_device(self, device, padding_val=0.0, out=None):
         """collate_fn's dict with every tensor on ``device``: one pinned H2D copy per modality, then
-        rp_pad_rows pads and converts on the GPU (all enqueued on the current stream)."""
+        rp_pad_rows pads and converts on the GPU (all enqueued on the current stream).  fp32 rows (PANNs
+        audio, labels, segments) need no conversion: from pinned memory they are copied by DMA straight
+        into their padded places (one copy when no sequence is short, else one per sequence plus a fill
+        of the padding).  ``out``: an existing dict of device tensors of the padded shapes (e.g. a
+        captured training step's static inputs, ``CapturedTrainStep.input_set``) written in place."""
         if not torch.device(device).type == "cuda":
             raise RuntimeError("RaggedBatch.to_device: the device path needs a ROCm device (use collate_fn on CPU)")
         B = len(self.video_id)
@@ -127,7 +147,7 @@ class RaggedBatch:
             raise ValueError("All sequences in the batch have zero length")
         if int(np.diff(host_offs["segments"]).max()) == 0:
             raise ValueError("All segments in the batch have zero length")
-        out = {"video_id": self.video_id, "duration": self.duration}
+        res = {"video_id": self.video_id, "duration": self.duration}
         names = {"visual": "visual_feats", "audio": "audio_feats", "text": "text_feats", "labels": "labels",
                  "segments": "segments"}
         for name, key in names.items():
@@ -140,20 +160,37 @@ class RaggedBatch:
             else:
                 rows = np.ascontiguousarray(rows)
                 hsrc, code = torch.from_numpy(rows).pin_memory(), _NP_DT[rows.dtype]
-            hoff = self.offsets[name]
-            if not (torch.is_tensor(hoff) and hoff.is_pinned()):
-                hoff = torch.from_numpy(offs.astype(np.int64)).pin_memory()
             D = rows.shape[1] if rows.ndim > 1 else 1
-            src = hsrc.to(device, non_blocking=True)
-            off = hoff.to(device, non_blocking=True)
-            dst = torch.empty(B, T, D, device=device, dtype=torch.float32)
-            N.call("rp_pad_rows", ctypes.c_void_p(src.data_ptr()), code, ctypes.c_void_p(off.data_ptr()),
-                   B, T, D, float(padding_val), ctypes.c_void_p(dst.data_ptr()), K._stream(dst))
-            out[key] = dst.view(B, T) if name == "labels" else dst
-        lens_dev = torch.from_numpy(vlens.astype(np.int64)).to(device, non_blocking=True)
-        out["masks"] = (torch.arange(T, device=device)[None] < lens_dev[:, None]).unsqueeze(1)
-        out.update(self.extra)
-        return out
+            if out is not None:
+                dst = out[key]
+                if dst.device != torch.device(device) or dst.dtype != torch.float32 or not dst.is_contiguous() \
+                        or dst.numel() != B * T * D:
+                    raise ValueError(f"RaggedBatch.to_device: out[{key!r}] must be a contiguous fp32 tensor of "
+                                     f"{B} x {T} x {D} on {device}")
+                dst = dst.view(B, T, D)
+            else:
+                dst = torch.empty(B, T, D, device=device, dtype=torch.float32)
+            if code == N.RP_F32:
+                _dma_rows(hsrc.view(-1, D), offs, dst, padding_val)
+            else:
+                hoff = self.offsets[name]
+                if not (torch.is_tensor(hoff) and hoff.is_pinned()):
+                    hoff = torch.from_numpy(offs.astype(np.int64)).pin_memory()
+                src = hsrc.to(device, non_blocking=True)
+                off = hoff.to(device, non_blocking=True)
+                N.call("rp_pad_rows", ctypes.c_void_p(src.data_ptr()), code, ctypes.c_void_p(off.data_ptr()),
+                       B, T, D, float(padding_val), ctypes.c_void_p(dst.data_ptr()), K._stream(dst))
+            res[key] = dst.view(B, T) if name == "labels" else dst
+        # the lengths from pinned memory: a pageable H2D copy would hold the host until the stream reached
+        # it (e.g. behind a wait for the step that last read ``out``)
+        lens_dev = torch.from_numpy(vlens.astype(np.int64)).pin_memory().to(device, non_blocking=True)
+        m = (torch.arange(T, device=device)[None] < lens_dev[:, None]).unsqueeze(1)
+        if out is not None:
+            out["masks"].copy_(m)
+            m = out["masks"]
+        res["masks"] = m
+        res.update(self.extra)
+        return res
 
 
 def collate_ragged(batch, test=False):

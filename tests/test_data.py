@@ -63,3 +63,28 @@ def test_device_collate_matches_reference(dev, seed):
     _same(got, ref)
     got_t = D.collate_ragged(batch, test=True).to_device(dev)
     assert got_t["gt_segments"] == [it["gt_segments"] for it in batch]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("lens", [(37, 80, 5, 64), (64, 64, 64)])
+def test_device_collate_in_place(dev, pinned, lens):
+    """to_device(out=...): the batch written into existing tensors (a captured step's static inputs, poisoned
+    first) equals the reference collate bit for bit — ragged lengths (fp32 rows copied per sequence by DMA
+    and their padding filled) and full lengths (one DMA copy per fp32 modality); pinned or pageable rows."""
+    batch = _batch(5, lens)
+    ref = O.collate_fn(batch)
+    rb = D.collate_ragged(batch)
+    if pinned:
+        rb = rb.pin()
+    T = max(lens)
+    out = {k: torch.full_like(v, float("nan"), device=dev) if v.is_floating_point() else torch.ones_like(v, device=dev)
+           for k, v in ref.items() if torch.is_tensor(v)}
+    keep = {k: v.data_ptr() for k, v in out.items()}
+    got = rb.to_device(dev, out=out)
+    _same(got, ref)
+    for k, v in out.items():  # written in place
+        assert got[k].data_ptr() == keep[k], k
+    assert got["visual_feats"].shape == (len(lens), T, 512)
+    with pytest.raises(ValueError, match="contiguous fp32"):
+        rb.to_device(dev, out=dict(out, audio_feats=out["audio_feats"][:, :-1]))

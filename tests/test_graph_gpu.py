@@ -192,3 +192,64 @@ def test_replay_after_exchange_workspace_growth(dev, monkeypatch):
     n = me.trainable_numel()
     assert torch.equal(mg.flat_params()[:n], me.flat_params()[:n])
     K.lnx_status()
+
+
+def test_two_input_sets_write_in_place_and_match_eager(dev):
+    """CapturedTrainStep(input_sets=2): two graphs over two static input sets, alternating; each step's batch
+    written into the free set through input_set(ahead=1) on a copy stream while the previous step runs
+    (RaggedBatch.to_device(out=...), as bench.py's fresh-batch loop) — losses and parameters bitwise those
+    of eager steps on the same batches (dropout off)."""
+    from repurpose_amd import data as D
+
+    from .test_data import _batch as items_batch
+
+    cfg_items = [items_batch(30 + i, lens=(96, 96)) for i in range(5)]
+    rbs = [D.collate_ragged(b).pin() for b in cfg_items]
+    eager_batches = [{k: v for k, v in rb.to_device(dev).items() if torch.is_tensor(v)} for rb in rbs]
+    torch.cuda.synchronize()
+    me, oe = _model_items(dev)
+    eager_losses = []
+    for b in eager_batches:
+        oe.zero_grad()
+        out = me(b)
+        loss = me.losses(*out)["cls_loss"] / 2
+        loss.backward()
+        oe.step()
+        eager_losses.append(loss.item())
+
+    mg, og = _model_items(dev)
+    run = CapturedTrainStep(mg, og, {k: v.clone() for k, v in eager_batches[0].items()}, warmup=1, input_sets=2)
+    copy = torch.cuda.Stream(dev)
+    main = torch.cuda.current_stream(dev)
+    losses = []
+
+    def stage(j, done):
+        with torch.cuda.stream(copy):
+            dst, used = run.input_set(ahead=j - done)
+            if used is not None:
+                copy.wait_event(used)
+            rbs[j].to_device(dev, out=dst)
+            ev = torch.cuda.Event()
+            ev.record(copy)
+        return ev
+
+    ev = stage(0, 0)
+    for j in range(len(rbs)):
+        nxt = stage(j + 1, j) if j + 1 < len(rbs) else None
+        main.wait_event(ev)
+        losses.append(run.step().item())
+        ev = nxt
+    torch.cuda.synchronize()
+    assert run._graphs[0] is not None and run._graphs[1] is not None
+    assert losses == eager_losses
+    n = me.trainable_numel()
+    assert torch.equal(mg.flat_params()[:n], me.flat_params()[:n])
+
+
+def _model_items(dev):
+    torch.manual_seed(0)
+    cfg = dict(vis_dim=512, aud_dim=2048, text_dim=384, d_model=512, self_num_layers=2, text_num_layers=3,
+               cross_num_layers=3, num_heads=8)
+    m = MMCTransformer(**cfg, compute_dtype="bf16").to(dev).train()
+    m.DROPOUT = 0.0
+    return m, FusedAdam(m, lr=1e-3, weight_decay=1e-4)

@@ -691,10 +691,9 @@ def test_gemm_64_row_tiles_bitwise(dev, monkeypatch, M):
     gated bf16 dgrad are bitwise the 128-row kernel's (RP_GEMM_BM64=1 vs 0), ragged M included, and
     match fp64."""
     outs = {}
-    # "g8": the 256 x 128 phased tiles (RP_GEMM8_128=1) on the K = 2048 shapes; "32": 32 x 128 tiles
-    for flag in ("1", "0", "g8", "32"):
-        monkeypatch.setenv("RP_GEMM_BM64", "0" if flag == "g8" else ("1" if flag == "32" else flag))
-        monkeypatch.setenv("RP_GEMM8_128", "1" if flag == "g8" else "0")
+    # "32": 32 x 128 tiles
+    for flag in ("1", "0", "32"):
+        monkeypatch.setenv("RP_GEMM_BM64", "1" if flag == "32" else flag)
         monkeypatch.setenv("RP_GEMM_BM32", "1" if flag == "32" else "0")
         res = []
         for (n, k) in [(512, 512), (512, 2048)]:
@@ -712,8 +711,8 @@ def test_gemm_64_row_tiles_bitwise(dev, monkeypatch, M):
                 close(res[-2], dy.double() @ w.double(), atol=2e-3 * math.sqrt(n), what=f"dgrad {n}x{k} M={M}")
                 close(res[-3], x.double() @ w.double().T + b.double(), atol=2e-2, rtol=1e-2, what=f"fwd {n}x{k}")
         outs[flag] = res
-    for a, c, d, e in zip(outs["1"], outs["0"], outs["g8"], outs["32"]):
-        assert torch.equal(a, c) and torch.equal(c, d) and torch.equal(a, e)
+    for a, c, e in zip(outs["1"], outs["0"], outs["32"]):
+        assert torch.equal(a, c) and torch.equal(a, e)
 
 
 @pytest.mark.parametrize("M", [384, 4096, 8192])
