@@ -54,9 +54,10 @@ struct EpiDev {
   float col_scale;
   int split_major;  // split-K: deal the (split, tile) work items split-major over the XCDs (see tile_split)
   int prefetch_gate;  // 256-row kernel: touch the tile's bf16 gate lines one K-tile before the epilogue
-  // attention delta fused into the attention-output gradient GEMM (rp_gemm_attn_dout_delta; bf16 C,
-  // 128 x 128 tiles, M % 128 == N % 128 == 0): per (row, 64-column head) the row dot of the STORED bf16
-  // output with (dot_hi + dot_lo) -> the delta workspace planes, exactly as attn_delta_kernel forms them
+  // attention delta fused into the attention-output gradient GEMM (rp_gemm_attn_dout_delta; bf16 C, the
+  // RESB 2 epilogue of gemm_epilogue, M % 128 == N % 128 == 0): per (row, 64-column head) the row dot of
+  // the STORED bf16 output with (dot_hi + dot_lo) -> the delta workspace planes, exactly as
+  // attn_delta_kernel forms them
   const bf16* dot_hi;
   const bf16* dot_lo;  // may be null
   int64_t ld_dot;
@@ -233,11 +234,16 @@ constexpr int gemm_lds_bytes() {
 // previous chunk's store (the compiler cannot prove the output and residual rows apart): one HBM
 // round trip per chunk — s_memtime stamps put that epilogue at 1.5x the K = 512 main loop
 // (out_proj forward).  Only the residual shapes take it: the batched registers cost the others
-// their occupancy.
-template <typename TC, int MODE, bool HALVES = false, bool RESB = false, int MI = 4>
+// their occupancy.  RESB == 2 (bf16 C with the attention delta, rp_gemm_attn_dout_delta): the tile's
+// attention-output chunks (hi, lo) are requested by the kernel BEFORE its main loop (gemm_bf16_dma_kernel)
+// and land while it runs.  Per chunk after its store they cost one HBM round trip each (28.8 us for the
+// metric shape's launch), batched at the epilogue's start 23.2 us, before the main loop 21.8 us (the
+// plain dgrad alone: 14.9 us; profiles/r06_dout_delta_ab.txt).
+template <typename TC, int MODE, bool HALVES = false, int RESB = 0, int MI = 4>
 __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* lds, int tid, int lane, int wm, int wn,
                                               int64_t m0, int64_t n0, int64_t M, int64_t N, TC* __restrict__ Cout,
-                                              int64_t ldc, float alpha, const EpiDev& ep, int split) {
+                                              int64_t ldc, float alpha, const EpiDev& ep, int split,
+                                              const bf16x8* poh = nullptr, const bf16x8* pol = nullptr) {
   static_assert(MI == 4 || !HALVES, "64-row tiles stage whole");
   float* cs = reinterpret_cast<float*>(lds);
   constexpr int OV = 16 / (int)sizeof(TC);
@@ -273,7 +279,46 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* l
           cs[((HALVES ? 0 : wm * (MI * 16)) + i * 16 + g * 4 + r) * CST + wn * 64 + j * 16 + cl] = acc[i][j][r];
   }
   __syncthreads();
-  if constexpr (RESB && std::is_same<TC, bf16>::value) {
+  if constexpr (RESB == 2) {
+    // the out_proj dgrad with the delta epilogue: alpha only (no bias / relu / dropout / gate / residual,
+    // rp_gemm_attn_dout_delta sets none), M and N whole tiles; the arithmetic of the per-chunk loop below
+    static_assert(std::is_same<TC, bf16>::value && MODE == 0 && OV == 8, "delta epilogue: bf16 C, MODE 0");
+    constexpr int ITER = HR * CPRO / NT;
+    static_assert(HR * CPRO % NT == 0, "whole chunks per thread");
+    bf16x8 oh[ITER], ol[ITER];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {  // loaded by the kernel before its main loop
+      oh[it] = poh[it];
+      if (ep.dot_lo) ol[it] = pol[it];
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int id = tid + it * NT;
+      const int row = id / CPRO + half * HR, cc = (id % CPRO) * OV;
+      const int64_t m = m0 + row, n = n0 + cc;
+      uint4 o;
+      bf16* ob = reinterpret_cast<bf16*>(&o);
+#pragma unroll
+      for (int e = 0; e < OV; e += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(cs + (row - half * HR) * CST + cc + e);
+        ob[e] = (bf16)(q.x * alpha); ob[e + 1] = (bf16)(q.y * alpha);
+        ob[e + 2] = (bf16)(q.z * alpha); ob[e + 3] = (bf16)(q.w * alpha);
+      }
+      rp_st16((TC*)Cbase + m * ldc + n, o, ep.st_pol);
+      float dsum = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum += ((float)oh[it][e] + (ep.dot_lo ? (float)ol[it][e] : 0.f)) * (float)ob[e];
+      dsum = rp_sum8(dsum);
+      if ((n & 63) == 0) {
+        const int b = (int)(m / ep.dT), t = (int)(m % ep.dT);
+        const int64_t at = ((int64_t)b * ep.dH + n / 64) * ep.dT + t, plane = (M / ep.dT) * ep.dH * ep.dT;
+        ep.delta[at] = dsum;
+        ep.delta[plane + at] = -dsum / ep.dscale;
+        ep.delta[2 * plane + at] = -(ep.lse[at] * 1.4426950408889634f - log2f(ep.dscale));
+      }
+    }
+    continue;
+  } else if constexpr (RESB && std::is_same<TC, bf16>::value) {
     // bf16 C gated by a bf16 tensor (the d_ff dgrad through ReLU + dropout; no residual, no delta): the
     // pass's gate chunks loaded before its first store, as the residual below
     static_assert(MODE == 0 && OV == 8, "RESB bf16: MODE 0");
@@ -442,26 +487,6 @@ __device__ __forceinline__ void gemm_epilogue(const f32x4 (&acc)[MI][4], char* l
 #pragma unroll
       for (int e = 0; e < 8; ++e) ob[e] = (bf16)v[e];
       rp_st16(dst, o, ep.st_pol);
-      if (MODE == 0 && ep.delta) {
-        // the row dot of this chunk's 8 stored values with the output (hi + lo), then the 8 chunks of
-        // the head (consecutive lanes: 16 chunks per row, M and N whole tiles so every lane is here)
-        // by rp_sum8 — attn_delta_kernel's order, so the planes are bitwise its
-        // the attention output (hi, lo) is read once, here: non-temporal
-        const bf16x8 oh = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(ep.dot_hi + m * ep.ld_dot + n));
-        bf16x8 ol;
-        if (ep.dot_lo) ol = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(ep.dot_lo + m * ep.ld_dot + n));
-        float dsum = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dsum += ((float)oh[e] + (ep.dot_lo ? (float)ol[e] : 0.f)) * (float)ob[e];
-        dsum = rp_sum8(dsum);
-        if ((n & 63) == 0) {
-          const int b = (int)(m / ep.dT), t = (int)(m % ep.dT);
-          const int64_t at = ((int64_t)b * ep.dH + n / 64) * ep.dT + t, plane = (M / ep.dT) * ep.dH * ep.dT;
-          ep.delta[at] = dsum;
-          ep.delta[plane + at] = -dsum / ep.dscale;
-          ep.delta[2 * plane + at] = -(ep.lse[at] * 1.4426950408889634f - log2f(ep.dscale));
-        }
-      }
     }
   }
   }
@@ -736,7 +761,7 @@ __device__ uint64_t g_lnx_probe[RP_PROBE_MAX * 8];  // exchange kernels: 6 stamp
 #define LX_STAMP(i)
 #endif
 
-template <bool AK, bool BKM, typename TC, int MODE, int CFG, bool RESB = false, int MI = 4>
+template <bool AK, bool BKM, typename TC, int MODE, int CFG, int RESB = 0, int MI = 4>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t N, int64_t K,
                                                               const bf16* __restrict__ A, int64_t lda,
                                                               const bf16* __restrict__ B, int64_t ldb,
@@ -769,6 +794,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
   float bacc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  // RESB == 2: the delta epilogue's attention-output chunks requested before the main loop
+  constexpr int PRE = RESB == 2 ? 2 * MI : 1;
+  bf16x8 poh[PRE], pol[PRE];
+  if constexpr (RESB == 2) {
+    static_assert(!D::HALVES && MI * 32 * (BN / 8) == PRE * NT, "one staging pass, whole chunks");
+#pragma unroll
+    for (int it = 0; it < PRE; ++it) {
+      const int id = tid + it * NT;
+      const int64_t m = m0 + id / (BN / 8), n = n0 + (id % (BN / 8)) * 8;
+      poh[it] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(ep.dot_hi + m * ep.ld_dot + n));
+      if (ep.dot_lo) pol[it] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(ep.dot_lo + m * ep.ld_dot + n));
+    }
+  }
 #ifdef RP_GEMM_PROBE
   const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -778,7 +816,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_dma_kernel(int64_t M, int64_t
   const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
 #endif
   gemm_epilogue<TC, MODE, D::HALVES, RESB, MI>(acc, lds, tid, lane, wm, wn, m0, n0, M, N, Cout, ldc, alpha, ep,
-                                               split);
+                                               split, poh, pol);
   if (MODE == 1 && want_bias) bias_reduce<8>(bacc, lds, tid, m0, M, bslab, split);
 #ifdef RP_GEMM_PROBE
   // tuning build only (never the shipping library): per-workgroup phase stamps of wave 0 at the
@@ -2638,20 +2676,21 @@ extern "C" int rp_gemm_attn_dout_delta(const void* dY, int64_t ldy, const void* 
   e.dscale = dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f;
   // dO = dY W: k-major A = dY [M, K], B = W [K, N] row-major (the nn.Linear weight's dgrad layout),
   // configuration 0 — the only path that carries the fused delta — on 128-, 64- or 32-row tiles by the
-  // plain GEMMs' rule (rp_gemm_bm64 / rp_gemm_bm32: config 4's 128 tiles -> 512)
+  // plain GEMMs' rule (rp_gemm_bm64 / rp_gemm_bm32: config 4's 128 tiles -> 512); the delta epilogue
+  // (RESB 2) with its operand chunks requested before the main loop
   const int mi = rp_gemm_bm64(M, N) ? (rp_gemm_bm32(M, N) ? 1 : 2) : 4;
   const dim3 grid((unsigned)((M / (32 * mi)) * (N / BN)));
+#define RP_DOUT_LAUNCH(MI_)                                                                                           \
+  hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, bf16, 0, 0, 2, MI_>), grid, dim3(NT), 0, (hipStream_t)stream, \
+                     M, N, K, (const bf16*)dY, ldy, (const bf16*)W, ldw, (bf16*)dO, ldo, 1.f, e, (int64_t)0,           \
+                     (float*)nullptr)
   if (mi == 4)
-    hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, bf16, 0, 0>), grid, dim3(NT), 0, (hipStream_t)stream, M, N,
-                       K, (const bf16*)dY, ldy, (const bf16*)W, ldw, (bf16*)dO, ldo, 1.f, e, (int64_t)0, (float*)nullptr);
+    RP_DOUT_LAUNCH(4);
   else if (mi == 2)
-    hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, bf16, 0, 0, false, 2>), grid, dim3(NT), 0, (hipStream_t)stream,
-                       M, N, K, (const bf16*)dY, ldy, (const bf16*)W, ldw, (bf16*)dO, ldo, 1.f, e, (int64_t)0,
-                       (float*)nullptr);
+    RP_DOUT_LAUNCH(2);
   else
-    hipLaunchKernelGGL((gemm_bf16_dma_kernel<true, false, bf16, 0, 0, false, 1>), grid, dim3(NT), 0, (hipStream_t)stream,
-                       M, N, K, (const bf16*)dY, ldy, (const bf16*)W, ldw, (bf16*)dO, ldo, 1.f, e, (int64_t)0,
-                       (float*)nullptr);
+    RP_DOUT_LAUNCH(1);
+#undef RP_DOUT_LAUNCH
   return rp_check_launch("rp_gemm_attn_dout_delta");
 }
 
