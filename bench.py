@@ -413,7 +413,7 @@ def main():
         dist.destroy_process_group()
 
 
-PMC_TRAFFIC_FILES = ("r05_pmc_traffic.json", "r05_pmc_traffic_T4096_B1.json", "r05_pmc_traffic_T1024_B8.json")
+PMC_TRAFFIC_FILES = ("r06_pmc_traffic.json", "r06_pmc_traffic_T4096_B1.json", "r06_pmc_traffic_T1024_B8.json")
 
 
 def pmc_traffic(B, T, files=PMC_TRAFFIC_FILES, root=None):

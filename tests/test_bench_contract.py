@@ -90,5 +90,5 @@ def test_traffic_is_keyed_by_the_measured_shape(tmp_path):
 
 
 def test_committed_traffic_files_are_this_rounds():
-    """bench.py reads only r05 PMC files (the kernels changed in every round)."""
-    assert all(n.startswith("r05_") for n in _bench().PMC_TRAFFIC_FILES)
+    """bench.py reads only r06 PMC files (the kernels changed in every round)."""
+    assert all(n.startswith("r06_") for n in _bench().PMC_TRAFFIC_FILES)
