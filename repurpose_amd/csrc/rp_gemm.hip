@@ -2242,6 +2242,7 @@ __device__ __forceinline__ void lx_fwd_tail(const GlnDev& a, const LnxWs& ws, in
     rp_st16(a.xo + m * a.ldxo + n, o, 2);
     *reinterpret_cast<float4*>(c) = o;
   }
+  LX_STAMP(7);
   __syncthreads();
   // the tile's per-row (sum, M2): TPR threads per row (adjacent lanes), 128 / TPR columns each
   constexpr int CPT = BN / L::TPR / 4;  // float4 chunks per thread
@@ -2461,6 +2462,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_fwd_kernel(int64_t M, int64_t 
   float* cs = reinterpret_cast<float*>(lds);
   lx_stage(acc, cs, lane, wm, wn);
   __syncthreads();
+  LX_STAMP(6);
   lx_fwd_tail<BM, NT>(a, ws, m0, n0, nt, cs, r, tid);
 }
 
@@ -2499,6 +2501,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_lnx_bwd_kernel(int64_t M, int64_t 
   lx_stage(acc, cs, lane, wm, wn);
   if (tid < 2 * BM) mr[tid] = mrv;
   __syncthreads();
+  LX_STAMP(6);
   lx_bwd_tail<BM, NT>(a, ws, m0, n0, nt, cs, xh, tid);
 }
 

@@ -17,7 +17,7 @@ from repurpose_amd import kernels as K  # noqa: E402
 def stamps(n):
     buf = (ctypes.c_uint64 * (8 * n))()
     assert N.load().rp_debug_lnx_probe(buf, 8 * n) == 0
-    return np.frombuffer(buf, dtype=np.uint64).reshape(n, 8)[:, :6].astype(np.int64)
+    return np.frombuffer(buf, dtype=np.uint64).reshape(n, 8).astype(np.int64)
 
 
 def main():
@@ -56,6 +56,11 @@ def main():
         span = s[:, 5].max() - s[:, 0].min()
         parts = "  ".join(f"{n} {np.median(s[:, i + 1] - s[:, i]):5.2f}/{(s[:, i + 1] - s[:, i]).max():5.2f}"
                           for i, n in enumerate(names))
+        d = lambda a, b: f"{np.median(s[:, b] - s[:, a]):5.2f}"  # noqa: E731
+        if name.startswith("fwd"):
+            parts += f"\n           stage {d(1, 6)}  pass1 (x_out) {d(6, 7)}  row stats {d(7, 2)}"
+        else:
+            parts += f"\n           stage {d(1, 6)}  pass1 (row sums) {d(6, 2)}"
         print(f"{name:10s} event {e0.elapsed_time(e1) * 1e3:6.1f} us  span {span:6.2f}  start spread "
               f"{np.median(t0):4.2f}/{t0.max():4.2f}  {parts}", flush=True)
 
