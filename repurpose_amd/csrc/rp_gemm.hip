@@ -2074,14 +2074,49 @@ __device__ __forceinline__ float lx_sum4(float v) {  // the lane's quad
   v += rp_dpp<0xB1>(v);
   return v + rp_dpp<0x4E>(v);
 }
-// the sum over the 32 lanes of the lane's half-wave, in every lane of it
-__device__ __forceinline__ float lx_sum32(float v) {
-  v += rp_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += rp_dpp<0x4E>(v);   // quad_perm [2,3,0,1]: the quad
-  v += rp_dpp<0x141>(v);  // row_half_mirror: the other quad of the 8
-  v += rp_dpp<0x140>(v);  // row_mirror: the other 8 of the row of 16
-  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(a[0]) + __uint_as_float(a[1]);  // rows 0 + 1 (2 + 3)
+// Row sums of a half-wave's partials: each of the 32 lanes holds IT partials per sum (a, b), one per row
+// r0 + RS it, and every row's total over the 32 lanes is wanted.  Recursive halving instead of one
+// 32-lane reduction per row: at each lane bit (4, then 3 .. 0) a lane pair splits its rows, each lane keeping
+// one half and adding its partner's values for that half, until one row is left; the remaining bits add
+// plainly.  Bit 4 pairs lanes l, l ^ 16 through v_permlane16_swap (odd 16-lane rows of the first operand
+// trade with even rows of the second: one instruction moves both halves of a pair of rows), bits 3 .. 0
+// through DPP row_mirror, row_half_mirror and quad perms (partners differ in that bit; the rows a lane
+// holds depend only on the bits above, which partners share).  2 (IT - 1) + 3 adds / selects per sum
+// instead of 6 IT.  Returns the row index (it) whose totals land in a[0] / b[0], in lanes l and l ^ 1.
+template <int N, int CTRL, int IT>
+__device__ __forceinline__ void lx_halve(float (&a)[IT], float (&b)[IT], int l, int bit, int& row) {
+  const bool hi = (l >> bit) & 1;
+  if constexpr (N > 1) {  // N rows held: keep half, add the partner's values for it
+#pragma unroll
+    for (int j = 0; j < N / 2; ++j) {
+      const float ka = hi ? a[j + N / 2] : a[j], sa = hi ? a[j] : a[j + N / 2];
+      const float kb = hi ? b[j + N / 2] : b[j], sb = hi ? b[j] : b[j + N / 2];
+      a[j] = ka + rp_dpp<CTRL>(sa);
+      b[j] = kb + rp_dpp<CTRL>(sb);
+    }
+    row += hi ? N / 2 : 0;
+  } else {  // one row left: plain add
+    a[0] += rp_dpp<CTRL>(a[0]);
+    b[0] += rp_dpp<CTRL>(b[0]);
+  }
+}
+template <int IT>
+__device__ __forceinline__ int lx_rowsums(float (&a)[IT], float (&b)[IT], int l) {
+  static_assert(IT >= 2 && (IT & (IT - 1)) == 0, "a power-of-two row count");
+#pragma unroll
+  for (int j = 0; j < IT / 2; ++j) {
+    const auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[j]), __float_as_uint(a[j + IT / 2]), false, false);
+    const auto y = __builtin_amdgcn_permlane16_swap(__float_as_uint(b[j]), __float_as_uint(b[j + IT / 2]), false, false);
+    a[j] = __uint_as_float(x[0]) + __uint_as_float(x[1]);
+    b[j] = __uint_as_float(y[0]) + __uint_as_float(y[1]);
+  }
+  int row = ((l >> 4) & 1) * (IT / 2);
+  constexpr int N3 = IT / 2, N2 = N3 > 1 ? N3 / 2 : 1, N1 = N2 > 1 ? N2 / 2 : 1, N0 = N1 > 1 ? N1 / 2 : 1;
+  lx_halve<N3, 0x140>(a, b, l, 3, row);  // row_mirror: partner l ^ 15 within 16
+  lx_halve<N2, 0x141>(a, b, l, 2, row);  // row_half_mirror: l ^ 7 within 8
+  lx_halve<N1, 0x4E>(a, b, l, 1, row);   // quad_perm [2,3,0,1]: l ^ 2
+  lx_halve<N0, 0xB1>(a, b, l, 0, row);   // quad_perm [1,0,3,2]: l ^ 1
+  return row;
 }
 
 // dma_mainloop's (32 MI) x 128 accumulator tile -> cs[row][CST]
@@ -2328,6 +2363,7 @@ __device__ __forceinline__ void lx_bwd_tail(const GlnDev& a, const LnxWs& ws, in
   const float4 gm = *reinterpret_cast<const float4*>(a.gamma + n0 + cc);
   const float gam[4] = {gm.x, gm.y, gm.z, gm.w};
   float pg[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f};  // the tile's gamma / beta partials
+  float ps1[L::IT], ps2[L::IT];  // the thread's partials of each row's sums
 #pragma unroll
   for (int it = 0; it < L::IT; ++it) {
     const int row = r0 + it * L::RS;
@@ -2346,10 +2382,13 @@ __device__ __forceinline__ void lx_bwd_tail(const GlnDev& a, const LnxWs& ws, in
       pb[e] += g[e];
     }
     xh[it] = make_float4(x[0], x[1], x[2], x[3]);
-    static_assert(LX_CPR == 32, "a row's chunks fill a half-wave");
-    s1 = lx_sum32(s1);
-    s2 = lx_sum32(s2);
-    if ((tid % LX_CPR) == 0) lx_store_sc1(ws.part(m0 + row) + nt * BM, f32x2{s1, s2});
+    ps1[it] = s1;
+    ps2[it] = s2;
+  }
+  static_assert(LX_CPR == 32, "a row's chunks fill a half-wave");
+  {
+    const int rit = lx_rowsums<L::IT>(ps1, ps2, tid % LX_CPR);
+    if ((tid & 1) == 0) lx_store_sc1(ws.part(m0 + r0 + rit * L::RS) + nt * BM, f32x2{ps1[0], ps2[0]});
   }
   LX_STAMP(2);
   lx_drain_arrive(cnt, tid);
