@@ -157,6 +157,19 @@ template <int CTRL>
 __device__ __forceinline__ float rp_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
+// rp_keep_bits<4> of a lane's 4-element chunks in two rows (element indices ia, ib), where the lane pair
+// l, l ^ 1 holds the two halves of each aligned 8-element group (even lane: elements 0-3): each lane draws
+// ONE group (the even lane row a's, the odd lane row b's) and takes the other from its partner, so the
+// pair makes two rp_keep8 draws instead of four.  Bitwise rp_keep_bits<4>.
+__device__ __forceinline__ void rp_keep4_pair(uint32_t seed, uint32_t ia, uint32_t ib, uint32_t thresh16, bool odd,
+                                              uint32_t& ka, uint32_t& kb) {
+  const uint32_t mine = rp_keep8(seed, (odd ? ib : ia) >> 3, thresh16);
+  const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, false);  // l ^ 1
+  const int sh = odd ? 4 : 0;
+  ka = ((odd ? other : mine) >> sh) & 0xFu;
+  kb = ((odd ? mine : other) >> sh) & 0xFu;
+}
+
 __device__ __forceinline__ float rp_sum8(float s) {
   s += rp_dpp<0xB1>(s);
   s += rp_dpp<0x4E>(s);

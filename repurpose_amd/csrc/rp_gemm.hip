@@ -2260,6 +2260,8 @@ __device__ __forceinline__ void lx_fwd_tail(const GlnDev& a, const LnxWs& ws, in
   // x_out = dropout(acc + bias) + residual: gemm_epilogue's RESB arithmetic, op for op
   const float4 bi = *reinterpret_cast<const float4*>(a.bias + n0 + cc);
   const uint32_t dseed = a.drop_thresh ? rp_seed_eff(a.seed_base, a.drop_seed) : 0u;
+  static_assert(L::IT % 2 == 0, "rows in pairs (rp_keep4_pair)");
+  uint32_t knext = 0u;  // keep bits of the odd row of a pair, drawn with the even row's
 #pragma unroll
   for (int it = 0; it < L::IT; ++it) {
     const int row = tid / LX_CPR + it * L::RS;
@@ -2268,7 +2270,10 @@ __device__ __forceinline__ void lx_fwd_tail(const GlnDev& a, const LnxWs& ws, in
     const float4 v = *reinterpret_cast<const float4*>(c);
     float e4[4] = {v.x * 1.f + bi.x, v.y * 1.f + bi.y, v.z * 1.f + bi.z, v.w * 1.f + bi.w};
     if (a.drop_thresh) {
-      const uint32_t kb = rp_keep_bits<4>(dseed, (uint32_t)(m * GL_N + n), a.drop_thresh);
+      uint32_t kb = knext;
+      if ((it & 1) == 0)
+        rp_keep4_pair(dseed, (uint32_t)(m * GL_N + n), (uint32_t)((m + L::RS) * GL_N + n), a.drop_thresh, tid & 1, kb,
+                      knext);
 #pragma unroll
       for (int e = 0; e < 4; ++e) e4[e] = ((kb >> e) & 1u) ? e4[e] * a.drop_scale : 0.f;
     }
@@ -2409,6 +2414,7 @@ __device__ __forceinline__ void lx_bwd_tail(const GlnDev& a, const LnxWs& ws, in
   __syncthreads();
   lx_done(cnt, tid);
   const uint32_t lseed = a.lp_thresh ? rp_seed_eff(a.seed_base, a.lp_seed) : 0u;
+  uint32_t knext = 0u;  // keep bits of the odd row of a pair (rp_keep4_pair)
 #pragma unroll
   for (int it = 0; it < L::IT; ++it) {
     const int row = r0 + it * L::RS;
@@ -2425,7 +2431,10 @@ __device__ __forceinline__ void lx_bwd_tail(const GlnDev& a, const LnxWs& ws, in
     *reinterpret_cast<float4*>(a.dx + m * a.lddx + n) = make_float4(dx[0], dx[1], dx[2], dx[3]);
     if (a.dx_lp) {
       if (a.lp_thresh) {
-        const uint32_t kb = rp_keep_bits<4>(lseed, (uint32_t)(m * GL_N + n), a.lp_thresh);
+        uint32_t kb = knext;
+        if ((it & 1) == 0)
+          rp_keep4_pair(lseed, (uint32_t)(m * GL_N + n), (uint32_t)((m + L::RS) * GL_N + n), a.lp_thresh, tid & 1, kb,
+                        knext);
 #pragma unroll
         for (int e = 0; e < 4; ++e) dx[e] = ((kb >> e) & 1u) ? dx[e] * a.lp_scale : 0.f;
       }
