@@ -470,6 +470,12 @@ int rp_attn_bwd_dq(int dtype, const void* qkv, const void* dout, const float* ls
  *      array when grad_per_elem != 0) */
 int rp_focal_fwd_sum(const float* x, const float* t, const uint8_t* mask, int64_t n, float alpha,
                      float gamma, float* loss, void* stream);
+/* The same sum over many workgroups (the training step's form): per-chunk partials into ws (at least
+ * rp_focal_ws_elems(n) floats), then one wave sums them in index order — deterministic for a given n, a
+ * different summation order from rp_focal_fwd_sum's single workgroup. */
+int64_t rp_focal_ws_elems(int64_t n);
+int rp_focal_fwd_sum_ws(const float* x, const float* t, const uint8_t* mask, int64_t n, float alpha,
+                        float gamma, float* ws, int64_t ws_elems, float* loss, void* stream);
 int rp_focal_elementwise(const float* x, const float* t, int64_t n, float alpha, float gamma,
                          float* out, void* stream);
 int rp_focal_bwd(const float* x, const float* t, const uint8_t* mask, int64_t n, float alpha,

@@ -134,6 +134,8 @@ _SIGNATURES = {
     "rp_diou_fwd": (c_i, [c_vp, c_vp, c_i64, c_f, c_i, c_vp, c_vp]),
     "rp_diou_bwd": (c_i, [c_vp, c_vp, c_i64, c_f, c_vp, c_i, c_f, c_vp, c_vp, c_vp]),
     "rp_focal_fwd_sum": (c_i, [c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_vp]),
+    "rp_focal_ws_elems": (c_i64, [c_i64]),
+    "rp_focal_fwd_sum_ws": (c_i, [c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_i64, c_vp, c_vp]),
     "rp_focal_elementwise": (c_i, [c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_vp]),
     "rp_focal_bwd": (c_i, [c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_vp, c_i, c_vp, c_vp]),
     "rp_rowdot_fwd": (c_i, [c_i, c_vp, c_i64, c_i64, c_i, c_vp, c_vp, c_i, c_i, c_vp, c_i64, c_vp]),

@@ -233,6 +233,40 @@ __global__ __launch_bounds__(1024) void focal_sum_kernel(const float* __restrict
   }
 }
 
+// Multi-workgroup form (rp_focal_fwd_sum_ws): workgroup b sums elements [b chunk, (b + 1) chunk) in the
+// order of focal_sum_kernel's loop (thread-strided, wave sums, the waves in order) into ws[b]; one wave
+// then sums the partials in index order.  Deterministic for a given n (the chunking depends on n only).
+constexpr int FOCAL_WG = 256;
+constexpr int64_t FOCAL_CHUNK = 4096;
+__global__ __launch_bounds__(FOCAL_WG) void focal_part_kernel(const float* __restrict__ x, const float* __restrict__ t,
+                                                              const uint8_t* __restrict__ mask, int64_t n, float alpha,
+                                                              float gamma, float* __restrict__ ws) {
+  const int64_t lo = (int64_t)blockIdx.x * FOCAL_CHUNK;
+  const int64_t hi = lo + FOCAL_CHUNK < n ? lo + FOCAL_CHUNK : n;
+  float s = 0.f;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += FOCAL_WG) {
+    if (mask && !mask[i]) continue;
+    s += focal_eval(x[i], t[i], alpha, gamma, false).loss;
+  }
+  s = rp_wave_sum(s);
+  __shared__ float red[FOCAL_WG / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int w = 0; w < FOCAL_WG / 64; ++w) tot += red[w];
+    ws[blockIdx.x] = tot;
+  }
+}
+
+__global__ __launch_bounds__(64) void focal_final_kernel(const float* __restrict__ ws, int64_t parts,
+                                                         float* __restrict__ loss) {
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < parts; i += 64) s += ws[i];
+  s = rp_wave_sum(s);
+  if (threadIdx.x == 0) *loss = s;
+}
+
 __global__ void focal_elem_kernel(const float* __restrict__ x, const float* __restrict__ t, int64_t n, float alpha,
                                   float gamma, float* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -270,6 +304,40 @@ __global__ __launch_bounds__(256) void rowdot_fwd_kernel(const T* __restrict__ X
     float s = rp_wave_sum(acc[j]) + (b ? b[j] : 0.f);
     if (relu) s = fmaxf(s, 0.f);
     if (lane == 0) out[r * ldo + j] = s;
+  }
+}
+
+// bf16 rows with 16-byte chunks (K % 8 == 0, X and ldx 16-byte aligned): eight lanes per row, each a
+// bf16x8 chunk per 64-column step, the row's partials summed over its eight lanes (quad perms +
+// half-mirror); 32 rows per workgroup.  The heads' [M, 256] projections: one wave per row spent its time
+// on 2-byte loads and a 64-lane reduction per row.
+__global__ __launch_bounds__(256) void rowdot_fwd8_kernel(const bf16* __restrict__ X, int64_t ldx, int64_t rows, int K,
+                                                          const float* __restrict__ W, const float* __restrict__ b,
+                                                          int nout, int relu, float* __restrict__ out, int64_t ldo) {
+  const int l8 = threadIdx.x & 7;
+  const int64_t r = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const bool live = r < rows;  // every lane runs the reductions (DPP)
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (live) {
+    const bf16* xr = X + r * ldx;
+    for (int k = l8 * 8; k < K; k += 64) {
+      const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xr + k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j >= nout) break;
+        const float4 w0 = *reinterpret_cast<const float4*>(W + (int64_t)j * K + k);
+        const float4 w1 = *reinterpret_cast<const float4*>(W + (int64_t)j * K + k + 4);
+        acc[j] += (((float)xv[0] * w0.x + (float)xv[1] * w0.y) + ((float)xv[2] * w0.z + (float)xv[3] * w0.w)) +
+                  (((float)xv[4] * w1.x + (float)xv[5] * w1.y) + ((float)xv[6] * w1.z + (float)xv[7] * w1.w));
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j >= nout) break;
+    float s = rp_sum8(acc[j]) + (b ? b[j] : 0.f);
+    if (relu) s = fmaxf(s, 0.f);
+    if (live && l8 == 0) out[r * ldo + j] = s;
   }
 }
 
@@ -439,6 +507,25 @@ extern "C" int rp_colsum(const void* X, int dtype, int64_t rows, int64_t cols, i
   return rp_check_launch("rp_colsum");
 }
 
+extern "C" int64_t rp_focal_ws_elems(int64_t n) { return n > 0 ? (n + FOCAL_CHUNK - 1) / FOCAL_CHUNK : 1; }
+
+extern "C" int rp_focal_fwd_sum_ws(const float* x, const float* t, const uint8_t* mask, int64_t n, float alpha,
+                                   float gamma, float* ws, int64_t ws_elems, float* loss, void* stream) {
+  RP_REQUIRE(n >= 0 && loss, "rp_focal_fwd_sum_ws: bad args");
+  RP_REQUIRE(n == 0 || (x && t), "rp_focal_fwd_sum_ws: null input");
+  const int64_t parts = rp_focal_ws_elems(n);
+  RP_REQUIRE(ws && ws_elems >= parts, "rp_focal_fwd_sum_ws: workspace of %lld floats needed", (long long)parts);
+  RP_REQUIRE(parts < (1 << 30), "rp_focal_fwd_sum_ws: n too large");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    hipLaunchKernelGGL(focal_final_kernel, dim3(1), dim3(64), 0, s, ws, (int64_t)0, loss);
+    return rp_check_launch("rp_focal_fwd_sum_ws");
+  }
+  hipLaunchKernelGGL(focal_part_kernel, dim3((unsigned)parts), dim3(FOCAL_WG), 0, s, x, t, mask, n, alpha, gamma, ws);
+  hipLaunchKernelGGL(focal_final_kernel, dim3(1), dim3(64), 0, s, ws, parts, loss);
+  return rp_check_launch("rp_focal_fwd_sum_ws");
+}
+
 extern "C" int rp_focal_fwd_sum(const float* x, const float* t, const uint8_t* mask, int64_t n, float alpha, float gamma,
                                 float* loss, void* stream) {
   RP_REQUIRE(n >= 0 && loss, "rp_focal_fwd_sum: bad args");
@@ -474,7 +561,10 @@ extern "C" int rp_rowdot_fwd(int x_dtype, const void* X, int64_t ldx, int64_t ro
   RP_REQUIRE(X && W && out, "rp_rowdot_fwd: null");
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
-  if (x_dtype == RP_BF16)
+  if (x_dtype == RP_BF16 && K % 8 == 0 && ldx % 8 == 0 && rp_aligned16(X) && rp_aligned16(W))
+    hipLaunchKernelGGL(rowdot_fwd8_kernel, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, s, (const bf16*)X, ldx,
+                       rows, K, W, b, nout, relu, out, ldo);
+  else if (x_dtype == RP_BF16)
     hipLaunchKernelGGL(rowdot_fwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)X, ldx, rows, K, W, b, nout, relu, out, ldo);
   else
     hipLaunchKernelGGL(rowdot_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)X, ldx, rows, K, W, b, nout, relu, out, ldo);

@@ -712,11 +712,15 @@ def _general_args(q, k, v, mask4, B, Tq, Tk, H, dk, scale, probs):
 
 
 def focal_fwd_sum(x, t, mask=None, alpha=0.7, gamma=2.0):
+    """sum_i mask_i * focal(x_i, t_i) on the device: per-chunk partials over many workgroups, then one
+    wave sums them in order (rp_focal_fwd_sum_ws; deterministic for a given n)."""
     _gpu(x, t, mask)
     x, t = x.contiguous().float(), t.contiguous().float()
     m = mask.contiguous().view(torch.uint8) if mask is not None else None
     loss = torch.empty((), device=x.device, dtype=torch.float32)
-    N.call("rp_focal_fwd_sum", _p(x), _p(t), _p(m), x.numel(), float(alpha), float(gamma), _p(loss),
+    nw = int(N.load().rp_focal_ws_elems(x.numel()))
+    ws = torch.empty(nw, device=x.device, dtype=torch.float32)
+    N.call("rp_focal_fwd_sum_ws", _p(x), _p(t), _p(m), x.numel(), float(alpha), float(gamma), _p(ws), nw, _p(loss),
            _stream(x))
     return loss
 

@@ -487,8 +487,14 @@ def test_focal_fused(dev):
     pt = pr * t + (1 - pr) * (1 - t)
     fl = (0.7 * t + 0.3 * (1 - t)) * ce * (1 - pt) ** 2
     ref = (fl * m).sum()
-    s = K.focal_fwd_sum(x, t, m)
+    s = K.focal_fwd_sum(x, t, m)  # many workgroups (rp_focal_fwd_sum_ws): 5000 frames = two chunks
     close(s, ref.detach(), atol=1e-3, rtol=1e-5, what="focal sum")
+    assert torch.equal(s, K.focal_fwd_sum(x, t, m))  # deterministic
+    one = torch.empty((), device=dev)  # the single-workgroup entry point
+    from repurpose_amd import _native as N
+    N.call("rp_focal_fwd_sum", K._p(x), K._p(t), K._p(m), n, 0.7, 2.0, K._p(one), K._stream(x))
+    close(one, ref.detach(), atol=1e-3, rtol=1e-5, what="focal sum (one workgroup)")
+    assert K.focal_fwd_sum(x[:0], t[:0]).item() == 0.0
     g = torch.tensor(1.7, device=dev)
     dx = K.focal_bwd(x, t, m, g.view(1))
     gr = torch.autograd.grad(ref * 1.7, xr)[0]
@@ -503,6 +509,12 @@ def test_rowdot_colsum_concat_cast(dev):
     b = rnd(2, dev=dev, seed=3)
     out = K.rowdot_fwd(X, W, b, relu=True)
     close(out, torch.relu(X.double() @ W.double().T + b.double()), atol=1e-5, what="rowdot")
+    # bf16 rows: the eight-lanes-per-row kernel (K % 8 == 0) and the one-wave-per-row fallback (K = 100)
+    for kk, nn in ((256, 1), (256, 4), (200, 3), (100, 2)):
+        Xb = rnd(rows, kk, dev=dev, seed=kk + nn).to(torch.bfloat16)
+        Wb = rnd(nn, kk, dev=dev, seed=kk - nn) * 0.1
+        bb = rnd(nn, dev=dev, seed=nn)
+        close(K.rowdot_fwd(Xb, Wb, bb), Xb.double() @ Wb.double().T + bb.double(), atol=1e-5, what=f"rowdot bf16 {kk}")
     dout = rnd(rows, 2, dev=dev, seed=4)
     G = rnd(rows, Kd, dev=dev, seed=5)
     dX = K.rowdot_bwd_dx(dout, W, gate=G, gate_scale=2.0)
