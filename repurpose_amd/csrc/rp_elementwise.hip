@@ -237,7 +237,7 @@ __global__ __launch_bounds__(1024) void focal_sum_kernel(const float* __restrict
 // order of focal_sum_kernel's loop (thread-strided, wave sums, the waves in order) into ws[b]; one wave
 // then sums the partials in index order.  Deterministic for a given n (the chunking depends on n only).
 constexpr int FOCAL_WG = 256;
-constexpr int64_t FOCAL_CHUNK = 4096;
+constexpr int64_t FOCAL_CHUNK = 512;  // two elements per thread: 32 workgroups for 16,384 frames
 __global__ __launch_bounds__(FOCAL_WG) void focal_part_kernel(const float* __restrict__ x, const float* __restrict__ t,
                                                               const uint8_t* __restrict__ mask, int64_t n, float alpha,
                                                               float gamma, float* __restrict__ ws) {

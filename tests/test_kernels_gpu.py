@@ -487,7 +487,7 @@ def test_focal_fused(dev):
     pt = pr * t + (1 - pr) * (1 - t)
     fl = (0.7 * t + 0.3 * (1 - t)) * ce * (1 - pt) ** 2
     ref = (fl * m).sum()
-    s = K.focal_fwd_sum(x, t, m)  # many workgroups (rp_focal_fwd_sum_ws): 5000 frames = two chunks
+    s = K.focal_fwd_sum(x, t, m)  # many workgroups (rp_focal_fwd_sum_ws): 5000 frames = ten chunks
     close(s, ref.detach(), atol=1e-3, rtol=1e-5, what="focal sum")
     assert torch.equal(s, K.focal_fwd_sum(x, t, m))  # deterministic
     one = torch.empty((), device=dev)  # the single-workgroup entry point
