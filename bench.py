@@ -492,17 +492,21 @@ def parity_mode(B, T, dev, rank, warmup=2, steps=5):
     return res
 
 
-def ragged_pool(B, T, n, seed):
+def ragged_pool(B, T, n, seed, f32=True):
     """n host batches in the layout the trainer's DataLoader hands over (repurpose_amd.data.collate_ragged:
-    each modality's rows concatenated in the feature files' dtypes — fp16 CLIP, fp32 PANNs, fp64 text
-    — labels and segments), pinned as a DataLoader's pin_memory thread leaves them."""
+    each modality's rows concatenated — the feature files hold fp16 CLIP, fp32 PANNs and fp64 text rows —
+    labels and segments), pinned as a DataLoader's pin_memory thread leaves them.  ``f32`` (default): the
+    workers also convert the rows to fp32 (collate_ragged(f32=True), as the reference's collate builds fp32
+    batches), so the loop's device work is DMA only; otherwise the fp16 / fp64 rows go to rp_pad_rows."""
     from repurpose_amd.data import RaggedBatch
     pool = []
     for i in range(n):
         b = synth_batch(B, T, torch.device("cpu"), seed + i)
-        rows = {"visual": b["visual_feats"].reshape(B * T, -1).numpy().astype("float16"),
+        vis = b["visual_feats"].reshape(B * T, -1).numpy().astype("float16")
+        txt = b["text_feats"].reshape(B * T, -1).numpy().astype("float64")
+        rows = {"visual": vis.astype("float32") if f32 else vis,
                 "audio": b["audio_feats"].reshape(B * T, -1).numpy(),
-                "text": b["text_feats"].reshape(B * T, -1).numpy().astype("float64"),
+                "text": txt.astype("float32") if f32 else txt,
                 "labels": b["labels"].reshape(B * T, 1).numpy(),
                 "segments": b["segments"].reshape(B * T, 2).numpy()}
         offs = {k: (torch.arange(B + 1) * T).numpy() for k in rows}
@@ -574,9 +578,10 @@ def fresh_batch_loop(runner, eager_step, batch, B, T, dev, rank, steps, world, d
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return {"value": world * B * T * steps / el, "unit": "feature-timesteps/sec", "ms_per_step": el / steps * 1e3,
-            "steps": steps, "h2d_bytes_per_step": h2d, "h2d_source": "pinned ragged rows (fp16 visual, fp32 audio, "
-            "fp64 text, labels, segments) on a copy stream, overlapped with the previous replay: fp32 rows by DMA "
-            "into their padded places, the others through rp_pad_rows",
+            "steps": steps, "h2d_bytes_per_step": h2d, "h2d_source": "pinned ragged rows (visual, audio, text, labels, "
+            "segments; converted to fp32 by the loader workers as the reference's collate does) on a copy stream, "
+            "overlapped with the previous replay: every modality by DMA into its padded place, masks from the host "
+            "lengths",
             "into": "the captured step's free static input set (no copy between replays)" if direct
             else "staging tensors, copied into the step's inputs", "pool": pool_n}
 

@@ -183,20 +183,26 @@ class RaggedBatch:
             res[key] = dst.view(B, T) if name == "labels" else dst
         # the lengths from pinned memory: a pageable H2D copy would hold the host until the stream reached
         # it (e.g. behind a wait for the step that last read ``out``)
-        lens_dev = torch.from_numpy(vlens.astype(np.int64)).pin_memory().to(device, non_blocking=True)
-        m = (torch.arange(T, device=device)[None] < lens_dev[:, None]).unsqueeze(1)
+        # the padding masks from the host lengths (collate's arange(T) < len, dataset/RepurposeClip.py:449-567):
+        # one pinned copy, no device kernels beside a running step
+        mh = torch.from_numpy(np.arange(T)[None, :] < vlens[:, None]).unsqueeze(1).pin_memory()
         if out is not None:
-            out["masks"].copy_(m)
+            out["masks"].copy_(mh, non_blocking=True)
             m = out["masks"]
+        else:
+            m = mh.to(device, non_blocking=True)
         res["masks"] = m
         res.update(self.extra)
         return res
 
 
-def collate_ragged(batch, test=False):
-    """Worker-side collate: concatenation only (no padding, no torch tensors)."""
+def collate_ragged(batch, test=False, f32=False):
+    """Worker-side collate: concatenation only (no padding, no torch tensors).  ``f32``: the rows also
+    converted to float32 in the worker, as the reference's collate does while padding
+    (dataset/RepurposeClip.py:449-567 builds fp32 batches) — ``to_device`` then moves every modality by
+    DMA into its padded place and runs no conversion kernel beside the training step."""
     def cat(arrs, D=None):
-        arrs = [np.asarray(a) for a in arrs]
+        arrs = [np.asarray(a, dtype=np.float32) if f32 else np.asarray(a) for a in arrs]
         lens = [a.shape[0] for a in arrs]
         offs = np.zeros(len(arrs) + 1, dtype=np.int64)
         offs[1:] = np.cumsum(lens)

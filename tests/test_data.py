@@ -52,29 +52,36 @@ def test_ragged_layout():
     assert rb.rows["visual"].dtype == np.float16 and rb.rows["text"].dtype == np.float64
     assert list(np.diff(rb.offsets["visual"])) == [37, 80, 5, 64]
     assert list(np.diff(rb.offsets["text"])) == [37, 73, 5, 64]
+    r32 = D.collate_ragged(batch, f32=True)  # worker-side conversion: every row array fp32, same values
+    assert all(v.dtype == np.float32 for v in r32.rows.values())
+    assert np.array_equal(r32.rows["text"], rb.rows["text"].astype(np.float32))
+    assert np.array_equal(r32.rows["visual"], rb.rows["visual"].astype(np.float32))
+    assert all(np.array_equal(r32.offsets[k], rb.offsets[k]) for k in rb.offsets)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("f32", [False, True])
 @pytest.mark.parametrize("seed", [0, 3])
-def test_device_collate_matches_reference(dev, seed):
+def test_device_collate_matches_reference(dev, seed, f32):
     batch = _batch(seed)
     ref = O.collate_fn(batch)
-    got = D.collate_ragged(batch).to_device(dev)
+    got = D.collate_ragged(batch, f32=f32).to_device(dev)
     _same(got, ref)
     got_t = D.collate_ragged(batch, test=True).to_device(dev)
     assert got_t["gt_segments"] == [it["gt_segments"] for it in batch]
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("f32", [False, True])
 @pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("lens", [(37, 80, 5, 64), (64, 64, 64)])
-def test_device_collate_in_place(dev, pinned, lens):
+def test_device_collate_in_place(dev, pinned, lens, f32):
     """to_device(out=...): the batch written into existing tensors (a captured step's static inputs, poisoned
     first) equals the reference collate bit for bit — ragged lengths (fp32 rows copied per sequence by DMA
     and their padding filled) and full lengths (one DMA copy per fp32 modality); pinned or pageable rows."""
     batch = _batch(5, lens)
     ref = O.collate_fn(batch)
-    rb = D.collate_ragged(batch)
+    rb = D.collate_ragged(batch, f32=f32)
     if pinned:
         rb = rb.pin()
     T = max(lens)
