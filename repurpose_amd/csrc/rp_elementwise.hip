@@ -75,6 +75,19 @@ __global__ void colsum_pass1(const T* __restrict__ X, int64_t rows, int64_t cols
   const int n = (int)(rows - r0 < CS_ROWS ? rows - r0 : CS_ROWS);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int r = 0;
+  if (n == CS_ROWS) {
+    // a whole block: every row's load issued before the first add (one memory round trip instead of
+    // one per eight rows), the sums in the loop's order below (bitwise the same)
+    float x[CS_ROWS], wr[CS_ROWS];
+#pragma unroll
+    for (int u = 0; u < CS_ROWS; ++u) {
+      x[u] = rp_ld(X + (r0 + u) * ldx + c);
+      wr[u] = w ? w[r0 + u] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < CS_ROWS; ++u) s[u & 7] += w ? wr[u] * x[u] : x[u];
+    r = n;
+  }
   for (; r + 8 <= n; r += 8) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
