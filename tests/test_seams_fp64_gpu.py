@@ -28,10 +28,13 @@ D = 512
 M = 16384
 
 
-@pytest.fixture(params=[0, 64, 32])
+@pytest.fixture(params=[(0, 16384), (64, 16384), (32, 16384), (0, 8192), (0, 4096)],
+                ids=["auto-16384", "64rows-16384", "32rows-16384", "auto-8192", "auto-4096"])
 def rows(request):
-    """0: the host's own choice (128-row exchange tiles at M = 16384); 64 / 32: forced smaller tiles."""
-    N.call("rp_debug_set_lnx_rows", int(request.param))
+    """(tile rows, M): 0 = the host's own choice — 128-row exchange tiles at the metric shape
+    (M = 16384), 64-row at config 2 (M = 8192), 32-row at config 4 (M = 4096); 64 / 32 forced at the
+    metric shape."""
+    N.call("rp_debug_set_lnx_rows", int(request.param[0]))
     yield request.param
     N.call("rp_debug_set_lnx_rows", 0)
 
@@ -53,6 +56,7 @@ def _drop(z, seed, p):
 
 @pytest.mark.parametrize("Kd,p", [(512, 0.1), (2048, 0.1), (2048, 0.0)])
 def test_seam_fwd_against_fp64(dev, rows, Kd, p):
+    M = rows[1]
     x = rnd(M, Kd, dev=dev, seed=Kd + 1).to(torch.bfloat16)
     W = rnd(D, Kd, dev=dev, seed=Kd + 2, scale=0.03).to(torch.bfloat16)
     b = rnd(D, dev=dev, seed=Kd + 3, scale=0.1)
@@ -75,6 +79,7 @@ def test_seam_fwd_against_fp64(dev, rows, Kd, p):
 
 @pytest.mark.parametrize("Kd,lp", [(2048, 0.1), (1536, 0.1), (1536, 0.0)])
 def test_seam_bwd_against_fp64(dev, rows, Kd, lp):
+    M = rows[1]
     dy = rnd(M, Kd, dev=dev, seed=3 * Kd + 1).to(torch.bfloat16)
     W = rnd(Kd, D, dev=dev, seed=3 * Kd + 2, scale=0.03).to(torch.bfloat16)
     x = rnd(M, D, dev=dev, seed=3 * Kd + 3) + 0.5
@@ -96,9 +101,11 @@ def test_seam_bwd_against_fp64(dev, rows, Kd, lp):
     close(flat[D:], dbet, atol=2e-5 * dbet.abs().max().item() + 2e-3, what="dbeta")
 
 
-def test_dff_gemms_against_fp64(dev):
+@pytest.mark.parametrize("M", [16384, 4096])
+def test_dff_gemms_against_fp64(dev, M):
     """linear1 forward (ReLU + dropout, bf16 out) and linear2 dgrad through the saved activation's
-    gate (bf16 out) at the metric shape: the 256-row phased kernel's shapes."""
+    gate (bf16 out): the 256-row phased kernel at the metric shape; at config 4 (M = 4096) the
+    gate-batched 32 / 64-row tiles."""
     Kd, F, p = 512, 2048, 0.1
     x = rnd(M, Kd, dev=dev, seed=21).to(torch.bfloat16)
     W1 = rnd(F, Kd, dev=dev, seed=22, scale=0.05).to(torch.bfloat16)
@@ -118,10 +125,12 @@ def test_dff_gemms_against_fp64(dev):
 
 
 @pytest.mark.parametrize("p", [0.1, 0.0])
-def test_dout_delta_against_fp64(dev, p):
+@pytest.mark.parametrize("B,T", [(8, 2048), (8, 1024), (1, 4096)])
+def test_dout_delta_against_fp64(dev, p, B, T):
     """dO = g1 W (bf16) and the three delta planes, from the stored bf16 dO and the attention output
-    hi + lo, against fp64."""
-    B, T, H = 8, 2048, 8
+    hi + lo, against fp64 — at the metric shape (128-row tiles) and configs 2 / 4 (64- / 32-row)."""
+    H = 8
+    M = B * T
     g1 = rnd(M, D, dev=dev, seed=31).to(torch.bfloat16)
     W = rnd(D, D, dev=dev, seed=32, scale=0.05).to(torch.bfloat16)
     o = rnd(M, D, dev=dev, seed=33).to(torch.bfloat16)
