@@ -634,6 +634,25 @@ def test_wgrad_grouped_whole_k(dev):
         close(w, dy.double().T @ x.double(), atol=tol, what="grouped wgrad overwrite")
 
 
+def test_wgrad_grouped_metric_shape(dev):
+    """The grouped weight gradients as the step launches them at the metric shape: one encoder layer's
+    four items (linear2, linear1, out_proj, in_proj) over T = 16,384 tokens on the 256 x 256 whole-K
+    tiles, with their biases, against fp64."""
+    T = 16384
+    shapes = [(512, 2048), (2048, 512), (512, 512), (1536, 512)]
+    items, refs = [], []
+    for i, (n_out, n_in) in enumerate(shapes):
+        dy = rnd(T, n_out, dev=dev, seed=70 + i).to(torch.bfloat16)
+        x = rnd(T, n_in, dev=dev, seed=80 + i).to(torch.bfloat16)
+        items.append((dy, x, torch.empty(n_out, n_in, device=dev), torch.empty(n_out, device=dev)))
+        refs.append((dy.double().T @ x.double(), dy.double().sum(0)))
+    K.linear_wgrad_grouped(items, accumulate=False)
+    tol = 2e-4 * math.sqrt(T)
+    for (dy, x, dW, db), (rw, rb) in zip(items, refs):
+        close(dW, rw, atol=tol, what=f"grouped wgrad {tuple(dW.shape)}")
+        close(db, rb, atol=tol, what=f"grouped bias {tuple(db.shape)}")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("qpre", [False, True])
