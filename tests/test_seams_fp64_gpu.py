@@ -144,3 +144,19 @@ def test_dout_delta_against_fp64(dev, p, B, T):
     close(delta[0], dd, atol=1e-4, rtol=1e-5, what="delta")
     close(delta[1], -dd / ds, atol=1e-4, rtol=1e-5, what="-delta / ds")
     close(delta[2], -(lse.double() * math.log2(math.e) - math.log2(ds)), atol=1e-5, rtol=1e-6, what="lse plane")
+
+
+def test_qkv_forward_against_fp64(dev):
+    """The QKV projection as the step launches it (bf16 out, the Q columns prescaled by
+    scale * log2(e) after the bias — the attention kernels' RP_ATTN_Q_PRESCALED input) at the metric
+    shape: 1,536 tiles of 128 x 128 on the one-stage LDS configuration."""
+    x = rnd(M, D, dev=dev, seed=41).to(torch.bfloat16)
+    W = rnd(3 * D, D, dev=dev, seed=42, scale=0.05).to(torch.bfloat16)
+    b = rnd(3 * D, dev=dev, seed=43, scale=0.1)
+    c = 0.125 * math.log2(math.e)
+    y = K.linear_fwd(x, W, b, out_dtype=torch.bfloat16, col_scale_n=D, col_scale=c)
+    torch.cuda.synchronize()
+    ref = x.double() @ W.double().T + b.double()
+    ref[:, :D] *= c
+    _bf16_close(y, ref, "qkv", extra=2e-5)
+
